@@ -1,0 +1,223 @@
+/*
+ * pfloor.h — C ABI of the MI355X-native Parquet column-chunk decoder.
+ *
+ * This is the drop-in boundary beneath parquet-floor's
+ *   ParquetReader.streamContent(File|InputFile, HydratorSupplier[, columns])
+ *   (reference: src/main/java/blue/strategic/parquet/ParquetReader.java:47-61)
+ * Today that call pulls every value through parquet-mr 1.12.2's ColumnReader
+ * (ParquetReader.java:141-168, :176-212) and decompresses pages through the
+ * Hadoop codec shim into snappy-java (src/main/java/org/apache/hadoop/io/compress/
+ * DecompressorStream.java:61-70,101-173; ReflectionUtils.java:10-21; CodecPool.java:6-8).
+ *
+ * The Java side keeps footer / schema / page-header (Thrift) parsing and fills the
+ * POD descriptors below; chunk bytes are handed over in one buffer (pinned host memory
+ * from pf_host_alloc, or device memory already resident in HBM).  The library decodes
+ * every page on the GPU and returns columnar buffers (values, validity, BYTE_ARRAY
+ * offsets + chars, list offsets, raw levels) that the Java adapter walks in
+ * ParquetReader.tryAdvance order to call Hydrator.add(record, path[0], value).
+ *
+ * Rules of the ABI: plain C, no C++/torch types, every function returns a pf_status
+ * (0 = OK, negative = error) except pf_abi_version / pf_last_error. No callbacks into
+ * the caller. One context per GPU; one host thread drives a context at a time.
+ * Error text for the last failing call on a context (or, for ctx-less calls, the
+ * calling thread) is returned by pf_last_error.
+ */
+#ifndef PFLOOR_H
+#define PFLOOR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PF_ABI_VERSION 1
+
+/* ---- status codes (mapped by the Java bridge onto the reference's exceptions:
+ *      IOException for open/footer errors, RuntimeException("Failed to read parquet", cause)
+ *      for iteration errors — ParquetReader.java:120, :209-211) ---------------------- */
+typedef enum pf_status {
+    PF_OK = 0,
+    PF_ERR_INVALID_ARG = -1,
+    PF_ERR_CORRUPT_PAGE = -2,         /* bounds / varint / RLE overrun; never an OOB read */
+    PF_ERR_UNSUPPORTED_ENCODING = -3,
+    PF_ERR_UNSUPPORTED_CODEC = -4,
+    PF_ERR_HIP = -5,
+    PF_ERR_CAPACITY = -6,             /* caller buffer too small; required sizes are reported */
+    PF_ERR_UNSUPPORTED_TYPE = -7,     /* ParquetReader.java:162-163 "Unsupported type" */
+    PF_ERR_IO = -8,
+    PF_ERR_STATE = -9
+} pf_status;
+
+/* ---- Parquet enums (Thrift ids of parquet-format; values are the wire values) ---- */
+typedef enum pf_physical_type {
+    PF_BOOLEAN = 0, PF_INT32 = 1, PF_INT64 = 2, PF_INT96 = 3,
+    PF_FLOAT = 4, PF_DOUBLE = 5, PF_BYTE_ARRAY = 6, PF_FIXED_LEN_BYTE_ARRAY = 7
+} pf_physical_type;
+
+typedef enum pf_codec {
+    PF_CODEC_UNCOMPRESSED = 0, PF_CODEC_SNAPPY = 1, PF_CODEC_GZIP = 2, PF_CODEC_LZO = 3,
+    PF_CODEC_BROTLI = 4, PF_CODEC_LZ4 = 5, PF_CODEC_ZSTD = 6, PF_CODEC_LZ4_RAW = 7
+} pf_codec;
+
+typedef enum pf_page_type {
+    PF_PAGE_DATA = 0, PF_PAGE_INDEX = 1, PF_PAGE_DICTIONARY = 2, PF_PAGE_DATA_V2 = 3
+} pf_page_type;
+
+typedef enum pf_encoding {
+    PF_ENC_PLAIN = 0, PF_ENC_PLAIN_DICTIONARY = 2, PF_ENC_RLE = 3, PF_ENC_BIT_PACKED = 4,
+    PF_ENC_DELTA_BINARY_PACKED = 5, PF_ENC_DELTA_LENGTH_BYTE_ARRAY = 6,
+    PF_ENC_DELTA_BYTE_ARRAY = 7, PF_ENC_RLE_DICTIONARY = 8, PF_ENC_BYTE_STREAM_SPLIT = 9
+} pf_encoding;
+
+/* ---- descriptors filled from the Java Thrift parse (PageHeader / ColumnMetaData) ---- */
+
+/* One page of a column chunk. `offset` locates the page BODY (the bytes after the
+ * Thrift PageHeader) relative to the chunk's first byte. */
+typedef struct pf_page_desc {
+    uint64_t offset;
+    uint32_t compressed_size;     /* PageHeader.compressed_page_size   (field 3) */
+    uint32_t uncompressed_size;   /* PageHeader.uncompressed_page_size (field 2) */
+    int32_t  page_type;           /* pf_page_type                       (field 1) */
+    int32_t  encoding;            /* values encoding (DataPageHeader[V2] / DictionaryPageHeader) */
+    int32_t  def_encoding;        /* v1 only: RLE or BIT_PACKED */
+    int32_t  rep_encoding;        /* v1 only */
+    int32_t  num_values;          /* level entries (data) / dictionary entries (dict) */
+    int32_t  num_nulls;           /* v2 only */
+    int32_t  num_rows;            /* v2 only */
+    int32_t  def_bytes;           /* v2 only: definition_levels_byte_length */
+    int32_t  rep_bytes;           /* v2 only: repetition_levels_byte_length */
+    int32_t  is_compressed;       /* v2 only (Thrift default true); v1 pages: 1 */
+} pf_page_desc;
+
+/* One column chunk (one leaf column of one row group). */
+typedef struct pf_chunk_desc {
+    int32_t  physical_type;       /* pf_physical_type */
+    int32_t  type_length;         /* FIXED_LEN_BYTE_ARRAY width; ignored otherwise */
+    int32_t  max_def;             /* ColumnDescriptor.getMaxDefinitionLevel() */
+    int32_t  max_rep;             /* ColumnDescriptor.getMaxRepetitionLevel() (<= 1 supported for list offsets) */
+    int32_t  repeated_def;        /* def level of the innermost REPEATED ancestor (0 if max_rep == 0):
+                                     an entry is a list element ("slot") iff def >= repeated_def */
+    int32_t  list_null_def;       /* the innermost list is non-null iff def >= list_null_def */
+    int32_t  codec;               /* pf_codec */
+    int32_t  n_pages;             /* pages, including the dictionary page if present */
+    const pf_page_desc* pages;
+    uint64_t chunk_offset;        /* offset of the chunk's first byte in the bytes buffer */
+    uint64_t chunk_size;          /* ColumnMetaData.total_compressed_size */
+    int64_t  num_rows;            /* RowGroup.num_rows (flat columns: = level entries) */
+} pf_chunk_desc;
+
+/* Decoded layout of one column chunk ("slots" = rows for flat columns, list elements for
+ * max_rep == 1; null slots hold zero bytes / zero-length strings):
+ *   values        slots * width bytes (BOOLEAN: 1 byte 0/1; INT96: 12; FLBA: type_length)
+ *   validity      ceil(slots/8) bytes, LSB-first, bit = (def == max_def)     [max_def > 0]
+ *   offsets       (slots+1) int32, BYTE_ARRAY only; chars = concatenated bytes
+ *   list_offsets  (rows+1) int32, max_rep == 1: slots before each row
+ *   list_validity ceil(rows/8) bytes, bit = (def of the row's first entry >= list_null_def)
+ *   def_levels / rep_levels  one byte per level entry                          [max_rep > 0]
+ * Capacities are in BYTES. Any pointer may be NULL to skip that array. */
+typedef struct pf_column_out {
+    void*    values;        size_t values_cap;
+    uint8_t* validity;      size_t validity_cap;
+    int32_t* offsets;       size_t offsets_cap;
+    uint8_t* chars;         size_t chars_cap;
+    int32_t* list_offsets;  size_t list_offsets_cap;
+    uint8_t* list_validity; size_t list_validity_cap;
+    uint8_t* def_levels;    size_t def_levels_cap;
+    uint8_t* rep_levels;    size_t rep_levels_cap;
+} pf_column_out;
+
+/* Sizes (and device pointers) of one decoded chunk, valid after pf_wait. */
+typedef struct pf_column_info {
+    int64_t num_entries;          /* level entries (= Σ page num_values) */
+    int64_t num_slots;
+    int64_t num_values;           /* non-null leaf values (def == max_def) */
+    int64_t num_rows;             /* entries with rep == 0 */
+    int64_t num_chars;            /* BYTE_ARRAY bytes */
+    int32_t width;                /* bytes per slot in `values` (0 for BYTE_ARRAY) */
+    int32_t status;               /* per-chunk pf_status */
+    const void*    d_values;      /* device pointers (owned by the context, valid until the next decode) */
+    const uint8_t* d_validity;
+    const int32_t* d_offsets;
+    const uint8_t* d_chars;
+    const int32_t* d_list_offsets;
+    const uint8_t* d_list_validity;
+    const uint8_t* d_def_levels;
+    const uint8_t* d_rep_levels;
+} pf_column_info;
+
+typedef struct pf_ctx pf_ctx;
+
+int         pf_abi_version(void);
+const char* pf_last_error(pf_ctx* ctx);           /* ctx may be NULL: thread-local message */
+
+int pf_device_count(int* count);
+int pf_ctx_create(int device, pf_ctx** out);
+int pf_ctx_destroy(pf_ctx* ctx);
+
+/* Pinned host memory (hipHostMalloc) for chunk bytes and outputs; Java wraps it with
+ * MemorySegment.reinterpret. */
+int pf_host_alloc(pf_ctx* ctx, size_t bytes, void** out);
+int pf_host_free(pf_ctx* ctx, void* ptr);
+
+/* Device memory owned by the context (for callers that keep inputs resident in HBM). */
+int pf_device_alloc(pf_ctx* ctx, size_t bytes, void** out);
+int pf_device_free(pf_ctx* ctx, void* ptr);
+int pf_memcpy_h2d(pf_ctx* ctx, void* dst, const void* src, size_t bytes);   /* async on ctx stream */
+
+/* Enqueue the decode of n_chunks column chunks whose bytes live in `bytes`
+ * (n_bytes long; host memory, ideally pinned, unless bytes_on_device != 0).
+ * Asynchronous: returns after enqueueing H2D + kernels on the context's stream.
+ * Descriptor arrays are copied before return. Results live in context-owned device
+ * buffers until the next pf_decode_row_group on this context. */
+int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* chunks, int n_chunks,
+                        const uint8_t* bytes, size_t n_bytes, int bytes_on_device);
+
+/* Block until the enqueued decode has finished; returns the first per-chunk error. */
+int pf_wait(pf_ctx* ctx);
+
+/* Sizes + device pointers of chunk i of the last decode (after pf_wait). */
+int pf_column_info_get(pf_ctx* ctx, int chunk, pf_column_info* out);
+
+/* Copy chunk i's decoded arrays into caller buffers (host, synchronous).
+ * Fails with PF_ERR_CAPACITY (nothing copied) if any non-NULL buffer is too small. */
+int pf_copy_column(pf_ctx* ctx, int chunk, const pf_column_out* out);
+
+/* Kernel timing of the last decode (sum of per-stage HIP-event times, ms). */
+int pf_last_timing(pf_ctx* ctx, float* stage_ms, int n_stages, int* n_written);
+
+/* ---- host-side metadata parse: the stand-in for the Java side's parquet-mr footer /
+ *      PageHeader parse (ParquetFileReader.open + readNextRowGroup,
+ *      ParquetReader.java:120, :183). Builds the descriptors above from a file. ---- */
+typedef struct pf_file pf_file;
+
+typedef struct pf_column_meta {
+    const char* path;             /* dotted path_in_schema */
+    const char* top_name;         /* ColumnDescriptor.getPath()[0] (the Hydrator heading) */
+    int32_t physical_type, type_length, max_def, max_rep, repeated_def, list_null_def;
+    int32_t converted_type;       /* SchemaElement.converted_type or -1 */
+    int32_t logical_type;         /* LogicalType union field id or 0 */
+} pf_column_meta;
+
+int pf_file_open(const char* path, pf_file** out);
+int pf_file_close(pf_file* f);
+int pf_file_num_row_groups(pf_file* f, int* out);
+int pf_file_num_columns(pf_file* f, int* out);
+int pf_file_num_rows(pf_file* f, int64_t* out);
+int pf_file_column_meta(pf_file* f, int column, pf_column_meta* out);
+int pf_file_row_group_rows(pf_file* f, int row_group, int64_t* out);
+/* Byte range [start, start+size) of a chunk in the file. */
+int pf_file_chunk_range(pf_file* f, int row_group, int column, uint64_t* start, uint64_t* size);
+/* Parse the chunk's page headers; fills *desc (pages owned by the pf_file) with
+ * chunk_offset = `chunk_offset_in_buffer`. */
+int pf_file_chunk_desc(pf_file* f, int row_group, int column, uint64_t chunk_offset_in_buffer,
+                       pf_chunk_desc* desc);
+/* Read raw bytes of the file (host). */
+int pf_file_read(pf_file* f, uint64_t offset, uint64_t size, void* dst);
+const char* pf_file_created_by(pf_file* f);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PFLOOR_H */
