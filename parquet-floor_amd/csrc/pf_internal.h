@@ -1,0 +1,92 @@
+// pf_internal.h — device-side work descriptors shared by the HIP kernels and the host
+// runtime (pf_runtime.hip). Not part of the C ABI.
+//
+// HBM layout of one decode batch (one pf_decode_row_group call):
+//   in      : the caller's chunk bytes (resident, or one H2D copy of the pinned buffer)
+//   scratch : decompressed page bodies, 16-B aligned, in page order (k_snappy writes,
+//             the page kernels read); per-page BYTE_ARRAY value positions / dict ids
+//   out     : per chunk: values | validity | offsets | chars | list offsets | levels,
+//             each array 256-B aligned inside one arena
+//   meta    : DevChunk[], DevPage[], DevChunkResult[] (small)
+#pragma once
+#include <stdint.h>
+
+namespace pf {
+
+enum : int32_t {
+    PG_V2 = 1,            // DATA_PAGE_V2
+    PG_COMPRESSED = 2,    // body lives in scratch after k_snappy
+    PG_DICT = 4,          // dictionary page
+};
+
+// One decompression job (Snappy raw stream -> dst).
+struct SnappyJob {
+    const uint8_t* src;
+    uint8_t* dst;
+    uint32_t src_len;
+    uint32_t dst_len;
+    int32_t page;         // global page index (for error attribution)
+    int32_t chunk;
+};
+
+struct DevPage {
+    const uint8_t* body;      // v1: [rep][def][values] uncompressed; v2: values section
+    const uint8_t* lvl;       // v2: [rep][def] raw levels (never compressed); v1: null
+    uint32_t body_len;
+    uint32_t rep_len;         // v2 byte lengths
+    uint32_t def_len;
+    int32_t chunk;
+    int32_t flags;
+    int32_t encoding;
+    int32_t def_enc;
+    int32_t rep_enc;
+    int32_t num_values;       // level entries
+    int32_t pad0;
+    int64_t entry_start;      // first level entry of this page within its chunk (host prefix sum)
+    // written by k_count, consumed by k_scan
+    int64_t n_slots;
+    int64_t n_values;
+    int64_t n_rows;
+    int64_t n_chars;
+    // written by k_scan (or host for flat fixed-width chunks)
+    int64_t slot_start;
+    int64_t value_start;
+    int64_t row_start;
+    int64_t char_start;
+    // per-page scratch: BYTE_ARRAY value positions (PLAIN) or dictionary ids
+    uint32_t* aux;
+    int64_t aux_cap;          // entries
+};
+
+struct DevChunk {
+    int32_t ptype, type_length, width, max_def, max_rep, repeated_def, list_null_def, codec;
+    int32_t dict_page;        // global page index of the dictionary page, -1 if none
+    int32_t first_page;       // first data page (global index)
+    int32_t n_pages;          // data pages
+    int32_t needs_count;      // 1: BYTE_ARRAY or nested -> k_count + k_scan
+    int64_t num_entries;
+    // dictionary (k_dict): fixed width -> dict_data is the decoded PLAIN page;
+    // BYTE_ARRAY -> dict_pos[i] = byte offset of entry i's length prefix in dict_data
+    const uint8_t* dict_data;
+    uint32_t* dict_pos;       // n+1 entries: start of chars of entry i (after the prefix), end at [n] sentinel
+    uint32_t* dict_len;
+    int64_t dict_n;
+    // outputs
+    uint8_t* values;
+    uint8_t* validity;
+    int32_t* offsets;
+    uint8_t* chars;
+    int32_t* list_offsets;
+    uint8_t* list_validity;
+    uint8_t* def_levels;
+    uint8_t* rep_levels;
+    int64_t values_cap, chars_cap, slots_cap, rows_cap;   // capacities (bytes / elements)
+};
+
+struct DevChunkResult {
+    int64_t num_slots, num_values, num_rows, num_chars;
+    int32_t status;           // pf_status (first error wins, atomicMin on negative codes)
+    int32_t err_page;
+};
+
+}  // namespace pf

@@ -1,0 +1,583 @@
+// pf_pages.hip — K2..K7: page decode on gfx950.
+//
+// Replaces the per-value work parquet-mr 1.12.2 does behind ColumnReader (called from
+// src/main/java/blue/strategic/parquet/ParquetReader.java:141-168 and :196-203):
+//   K2 RLE/bit-packed hybrid expansion of def/rep levels and dictionary ids
+//      (RunLengthBitPackingHybridDecoder, DictionaryValuesReader)
+//   K3 dictionary gather (PlainValuesDictionary.decodeToX behind getX(), :151-161)
+//   K4 PLAIN decode (Integer/Long/Float/Double/Boolean/Binary/FixedLen PlainValuesReader)
+//   K5 DELTA_BINARY_PACKED (DeltaBinaryPackingValuesReader[ForLong]) — pf_delta.hip
+//   K6 null scatter: def == maxDef test of ParquetReader.java:146 -> validity + slot positions
+//   K7 repetition levels -> list offsets (ParquetReader.java:200's rep stream)
+//
+// Kernels (one 256-thread workgroup per page, entries processed in tiles of TILE):
+//   k_dict_binary : BYTE_ARRAY dictionary page -> entry positions/lengths
+//   k_count       : per data page of BYTE_ARRAY / nested chunks: slots, values, rows, chars
+//                   (+ per-value positions or dictionary ids kept in the page's aux buffer)
+//   k_scan        : per chunk: exclusive scans of the page counts -> output bases
+//   k_decode      : per data page: levels -> validity / list offsets / levels; values -> slots
+#include <hip/hip_runtime.h>
+
+#include "pf_device.h"
+
+namespace pf {
+
+constexpr int NT = 256;
+constexpr int TILE = 1024;
+constexpr int EPT = TILE / NT;   // entries per thread per tile (4 consecutive)
+
+// ---- page section layout ------------------------------------------------------------------
+struct Sections {
+    const uint8_t* rep; uint64_t rep_n;
+    const uint8_t* def; uint64_t def_n;
+    const uint8_t* val; uint64_t val_n;
+    int rep_rle, def_rle;    // 1 = RLE hybrid, 0 = BIT_PACKED (v1 deprecated)
+};
+
+// v1: [rep][def][values], each RLE level section prefixed by its 4-byte LE length;
+//     BIT_PACKED levels take ceil(n*bw/8) bytes, no prefix.
+// v2: levels in pg.lvl (rep_len + def_len bytes, no prefixes), values in pg.body.
+__device__ inline bool page_sections(const DevPage& pg, const DevChunk& ck, Sections& s) {
+    s.rep = s.def = nullptr; s.rep_n = s.def_n = 0; s.rep_rle = s.def_rle = 1;
+    if (pg.flags & PG_V2) {
+        s.rep = pg.lvl; s.rep_n = pg.rep_len;
+        s.def = pg.lvl + pg.rep_len; s.def_n = pg.def_len;
+        s.val = pg.body; s.val_n = pg.body_len;
+        if (ck.max_rep == 0) s.rep_n = 0;
+        if (ck.max_def == 0) s.def_n = 0;
+        return true;
+    }
+    uint64_t pos = 0, n = pg.body_len;
+    const uint8_t* b = pg.body;
+    for (int which = 0; which < 2; which++) {
+        int maxl = which == 0 ? ck.max_rep : ck.max_def;
+        if (maxl == 0) continue;
+        int enc = which == 0 ? pg.rep_enc : pg.def_enc;
+        const uint8_t* p; uint64_t len;
+        if (enc == 3) {
+            if (pos + 4 > n) return false;
+            len = ld32le(b, pos, n);
+            pos += 4;
+            if (len > n - pos) return false;
+            p = b + pos;
+        } else if (enc == 4) {
+            len = (uint64_t(pg.num_values) * bit_width(maxl) + 7) / 8;
+            if (len > n - pos) return false;
+            p = b + pos;
+        } else {
+            return false;
+        }
+        pos += len;
+        if (which == 0) { s.rep = p; s.rep_n = len; s.rep_rle = enc == 3; }
+        else { s.def = p; s.def_n = len; s.def_rle = enc == 3; }
+    }
+    s.val = b + pos; s.val_n = n - pos;
+    return true;
+}
+
+// ---- tile-wise level decoding ---------------------------------------------------------------
+struct LevelLds {
+    Piece prep[TILE];
+    Piece pdef[TILE];
+    uint8_t rep[TILE];
+    uint8_t def[TILE];
+    RleState srep, sdef;
+    int nprep, npdef;
+    uint32_t count;
+    int err;
+};
+
+// BIT_PACKED (deprecated, big-endian bit order: ByteBitPackingValuesReader BE) level at index i
+__device__ __forceinline__ uint32_t bitpacked_be(const uint8_t* p, uint64_t n, uint64_t i, int bw) {
+    uint32_t v = 0;
+    for (int b = 0; b < bw; b++) {
+        uint64_t bit = i * bw + b;
+        v = (v << 1) | ((ld8(p, bit >> 3, n) >> (7 - (bit & 7))) & 1);
+    }
+    return v;
+}
+
+// Decode the levels of entries [e0, e0 + want) into L.rep / L.def; returns count (== want) or
+// sets L.err. Must be called by all threads.
+__device__ inline uint32_t decode_level_tile(LevelLds& L, const Sections& s, const DevChunk& ck,
+                                             uint64_t e0, uint32_t want) {
+    const int bwr = bit_width(ck.max_rep), bwd = bit_width(ck.max_def);
+    if (threadIdx.x == 0) {
+        L.nprep = L.npdef = 0;
+        if (ck.max_rep > 0 && s.rep_rle) {
+            uint32_t got = rle_walk(L.srep, s.rep, s.rep_n, bwr, want, L.prep, TILE, L.nprep);
+            if (got != want || L.srep.err) L.err = 1;
+        }
+        if (ck.max_def > 0 && s.def_rle) {
+            uint32_t got = rle_walk(L.sdef, s.def, s.def_n, bwd, want, L.pdef, TILE, L.npdef);
+            if (got != want || L.sdef.err) L.err = 1;
+        }
+    }
+    __syncthreads();
+    if (L.err) return 0;
+    if (ck.max_rep > 0) {
+        if (s.rep_rle) rle_expand<uint8_t>(L.prep, L.nprep, s.rep, s.rep_n, bwr, L.rep);
+        else for (uint32_t i = threadIdx.x; i < want; i += NT) L.rep[i] = uint8_t(bitpacked_be(s.rep, s.rep_n, e0 + i, bwr));
+    } else {
+        for (uint32_t i = threadIdx.x; i < want; i += NT) L.rep[i] = 0;
+    }
+    if (ck.max_def > 0) {
+        if (s.def_rle) rle_expand<uint8_t>(L.pdef, L.npdef, s.def, s.def_n, bwd, L.def);
+        else for (uint32_t i = threadIdx.x; i < want; i += NT) L.def[i] = uint8_t(bitpacked_be(s.def, s.def_n, e0 + i, bwd));
+    } else {
+        for (uint32_t i = threadIdx.x; i < want; i += NT) L.def[i] = 0;
+    }
+    __syncthreads();
+    // levels above their maximum are corrupt
+    int bad = 0;
+    for (uint32_t i = threadIdx.x; i < want; i += NT)
+        bad |= (L.rep[i] > ck.max_rep) | (L.def[i] > ck.max_def);
+    if (__syncthreads_or(bad)) { if (threadIdx.x == 0) L.err = 1; __syncthreads(); return 0; }
+    return want;
+}
+
+// ---- PLAIN BYTE_ARRAY walk (one lane; v1) --------------------------------------------------
+// BinaryPlainValuesReader: <4-byte LE length><bytes> repeated. Writes the chars start of
+// value k into pos[k]; returns total chars or -1 on overrun.
+__device__ inline int64_t plain_binary_walk(const uint8_t* p, uint64_t n, int64_t count, uint32_t* pos, uint32_t* len) {
+    uint64_t i = 0;
+    int64_t total = 0;
+    for (int64_t k = 0; k < count; k++) {
+        if (i + 4 > n) return -1;
+        uint32_t l = ld32le(p, i, n);
+        i += 4;
+        if (l > n - i) return -1;
+        pos[k] = uint32_t(i);
+        if (len) len[k] = l;
+        i += l;
+        total += l;
+    }
+    return total;
+}
+
+// ---- k_dict_binary --------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_dict_binary(DevChunk* chunks, const DevPage* pages, const int* dict_chunks,
+                                                    DevChunkResult* res) {
+    const int c = dict_chunks[blockIdx.x];
+    DevChunk& ck = chunks[c];
+    const DevPage& pg = pages[ck.dict_page];
+    if (threadIdx.x == 0) {
+        int64_t t = plain_binary_walk(pg.body, pg.body_len, ck.dict_n, ck.dict_pos, ck.dict_len);
+        if (t < 0) set_status(res, c, ST_CORRUPT, ck.dict_page);
+    }
+}
+
+// ---- values helpers ------------------------------------------------------------------------
+__device__ __forceinline__ bool is_dict_enc(int e) { return e == 2 || e == 8; }
+
+// ---- k_count ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                              const int* page_list, DevChunkResult* res) {
+    __shared__ LevelLds L;
+    __shared__ Piece pval[TILE];
+    __shared__ uint32_t ids[TILE];
+    __shared__ uint32_t scan_tmp[NT / 64];
+    __shared__ RleState sval;
+    __shared__ int npval, verr;
+    __shared__ unsigned long long chars_acc;
+
+    const int pi = page_list[blockIdx.x];
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    if (res[pg.chunk].status != 0) return;   // an earlier stage failed this chunk
+    Sections s;
+    const bool ok = page_sections(pg, ck, s);
+    if (threadIdx.x == 0) {
+        rle_init(L.srep); rle_init(L.sdef); rle_init(sval);
+        L.err = ok ? 0 : 1; verr = 0; chars_acc = 0;
+        sval.pos = 1;    // dictionary ids: skip the bit-width byte
+    }
+    __syncthreads();
+    if (L.err) { if (threadIdx.x == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
+
+    const bool dict = is_dict_enc(pg.encoding);
+    const bool binary = ck.ptype == 6;
+    const int id_bw = (dict && s.val_n > 0) ? int(s.val[0]) : 0;
+    uint64_t slots = 0, vals = 0, rows = 0;
+    for (uint64_t e0 = 0; e0 < uint64_t(pg.num_values); e0 += TILE) {
+        uint32_t want = uint32_t(min<uint64_t>(TILE, uint64_t(pg.num_values) - e0));
+        decode_level_tile(L, s, ck, e0, want);
+        if (L.err) break;
+        uint32_t ns = 0, nv = 0, nr = 0;
+        for (uint32_t i = threadIdx.x; i < want; i += NT) {
+            int d = L.def[i];
+            ns += (ck.max_rep == 0 || d >= ck.repeated_def);
+            nv += (d == ck.max_def);
+            nr += (L.rep[i] == 0);
+        }
+        uint32_t t;
+        block_excl_scan<NT>(ns, scan_tmp, t); slots += t;
+        block_excl_scan<NT>(nr, scan_tmp, t); rows += t;
+        block_excl_scan<NT>(nv, scan_tmp, t);
+        // dictionary ids of this tile's present values: decode, keep in aux, sum lengths
+        if (binary && dict && t > 0) {
+            if (threadIdx.x == 0) {
+                if (id_bw > 32 || !ck.dict_len) verr = 1;
+                else {
+                    uint32_t got = rle_walk(sval, s.val, s.val_n, id_bw, t, pval, TILE, npval);
+                    if (got != t || sval.err) verr = 1;
+                }
+            }
+            __syncthreads();
+            if (verr) break;
+            rle_expand<uint32_t>(pval, npval, s.val, s.val_n, id_bw, ids);
+            __syncthreads();
+            uint64_t acc = 0;
+            int bad = 0;
+            for (uint32_t i = threadIdx.x; i < t; i += NT) {
+                uint32_t id = ids[i];
+                if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
+                acc += ck.dict_len[id];
+                pg.aux[vals + i] = id;
+            }
+            if (__syncthreads_or(bad)) { if (threadIdx.x == 0) verr = 1; __syncthreads(); break; }
+            atomicAdd(&chars_acc, (unsigned long long)acc);
+        }
+        vals += t;
+        __syncthreads();
+    }
+    if (L.err || verr) { if (threadIdx.x == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
+    if (binary && !dict) {
+        if (threadIdx.x == 0) {
+            if (pg.encoding != 0) { set_status(res, pg.chunk, ST_ENCODING, pi); verr = 1; }
+            else {
+                int64_t tot = plain_binary_walk(s.val, s.val_n, int64_t(vals), pg.aux, nullptr);
+                if (tot < 0) { set_status(res, pg.chunk, ST_CORRUPT, pi); verr = 1; }
+                else chars_acc = uint64_t(tot);
+            }
+        }
+        __syncthreads();
+        if (verr) return;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        pg.n_slots = int64_t(slots);
+        pg.n_values = int64_t(vals);
+        pg.n_rows = int64_t(rows);
+        pg.n_chars = int64_t(chars_acc);
+    }
+}
+
+// ---- k_scan (one wave per chunk) ------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_scan(DevChunk* chunks, DevPage* pages, const int* chunk_list,
+                                             DevChunkResult* res, uint8_t* chars_arena, uint64_t arena_cap,
+                                             unsigned long long* arena_used) {
+    const int c = chunk_list[blockIdx.x];
+    DevChunk& ck = chunks[c];
+    if (threadIdx.x != 0) return;
+    int64_t s = 0, v = 0, r = 0, ch = 0;
+    for (int i = 0; i < ck.n_pages; i++) {
+        DevPage& pg = pages[ck.first_page + i];
+        pg.slot_start = s; pg.value_start = v; pg.row_start = r; pg.char_start = ch;
+        s += pg.n_slots; v += pg.n_values; r += pg.n_rows; ch += pg.n_chars;
+    }
+    res[c].num_slots = s; res[c].num_values = v; res[c].num_rows = r; res[c].num_chars = ch;
+    if (ck.ptype == 6) {
+        if (ch > int64_t(0x7fffffff)) { set_status(res, c, ST_CAPACITY, -1); ck.chars = nullptr; }
+        else {
+            unsigned long long need = (unsigned long long)((ch + 255) & ~int64_t(255));
+            unsigned long long at = atomicAdd(arena_used, need);
+            if (at + need > arena_cap) { set_status(res, c, ST_CAPACITY, -1); ck.chars = nullptr; }
+            else ck.chars = chars_arena + at;
+        }
+        if (ck.offsets) ck.offsets[0] = 0;
+    }
+    if (ck.max_rep == 1 && ck.list_offsets) ck.list_offsets[r] = int32_t(s);
+}
+
+// ---- k_decode ----------------------------------------------------------------------------------
+struct DecodeLds {
+    LevelLds L;
+    Piece pval[TILE];
+    uint32_t ids[TILE];
+    uint32_t vbits[TILE / 32 + 2];   // validity bits of the tile's slots (relative to aligned base)
+    uint32_t lbits[TILE / 32 + 2];   // list validity bits (rows)
+    uint32_t scan_tmp[NT / 64];
+    RleState sval;
+    int npval, verr;
+};
+
+template <typename T>
+__device__ __forceinline__ void store_w(uint8_t* dst, const uint8_t* src) {
+    T v;
+    __builtin_memcpy(&v, src, sizeof(T));
+    *reinterpret_cast<T*>(dst) = v;
+}
+
+// Copy one value of width w from `src` to `dst` (dst is aligned to w for w in {1,4,8}).
+__device__ __forceinline__ void copy_value(uint8_t* dst, const uint8_t* src, int w) {
+    if (w == 4) { uint32_t v = uint32_t(src[0]) | uint32_t(src[1]) << 8 | uint32_t(src[2]) << 16 | uint32_t(src[3]) << 24; *reinterpret_cast<uint32_t*>(dst) = v; }
+    else if (w == 8) {
+        uint64_t v = 0;
+        #pragma unroll
+        for (int k = 0; k < 8; k++) v |= uint64_t(src[k]) << (8 * k);
+        *reinterpret_cast<uint64_t*>(dst) = v;
+    } else {
+        for (int k = 0; k < w; k++) dst[k] = src[k];
+    }
+}
+
+__device__ __forceinline__ void zero_value(uint8_t* dst, int w) {
+    if (w == 4) *reinterpret_cast<uint32_t*>(dst) = 0;
+    else if (w == 8) *reinterpret_cast<uint64_t*>(dst) = 0;
+    else for (int k = 0; k < w; k++) dst[k] = 0;
+}
+
+// Flush a bit array covering bits [b0, b0+nbits) (bit b0 stored at LDS bit (b0 & 31)) to words of
+// `out` (bitmap, LSB-first). Edge words use atomicOr (neighbouring pages share them; the output
+// bitmap is zeroed before the launch), inner words are plain stores.
+__device__ inline void flush_bits(const uint32_t* bits, uint64_t b0, uint32_t nbits, uint8_t* out_bytes) {
+    if (nbits == 0) return;
+    uint32_t* out = reinterpret_cast<uint32_t*>(out_bytes);
+    uint64_t w0 = b0 >> 5, w1 = (b0 + nbits - 1) >> 5;
+    for (uint64_t w = w0 + threadIdx.x; w <= w1; w += NT) {
+        uint32_t v = bits[w - w0];
+        if (w == w0 || w == w1) { if (v) atomicOr(out + w, v); }
+        else out[w] = v;
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                               const int* page_list, DevChunkResult* res) {
+    __shared__ DecodeLds S;
+    LevelLds& L = S.L;
+    const int pi = page_list[blockIdx.x];
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    const int tid = threadIdx.x;
+    if (res[pg.chunk].status != 0) return;   // an earlier stage failed this chunk
+    Sections s;
+    const bool ok = page_sections(pg, ck, s);
+    if (tid == 0) {
+        rle_init(L.srep); rle_init(L.sdef); rle_init(S.sval);
+        L.err = ok ? 0 : 1; S.verr = 0;
+    }
+    __syncthreads();
+    if (L.err) { if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
+
+    const int enc = pg.encoding;
+    const bool binary = ck.ptype == 6;
+    const bool dict = is_dict_enc(enc);
+    const bool boolean = ck.ptype == 0;
+    const int w = ck.width;
+    const bool counted = ck.needs_count != 0;
+    // value-stream setup
+    int id_bw = 0;
+    if (dict) {
+        id_bw = s.val_n > 0 ? int(s.val[0]) : 0;
+        if (tid == 0) S.sval.pos = 1;
+    } else if (boolean && enc == 3) {
+        // RLE booleans: 4-byte length prefix, then a bit-width-1 hybrid stream
+        if (tid == 0) S.sval.pos = 0;
+    }
+    const uint8_t* rle_bool_p = nullptr; uint64_t rle_bool_n = 0;
+    if (boolean && enc == 3) {
+        uint32_t ln = s.val_n >= 4 ? ld32le(s.val, 0, s.val_n) : 0;
+        if (s.val_n < 4 || ln > s.val_n - 4) { if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
+        rle_bool_p = s.val + 4; rle_bool_n = ln;
+    }
+    // encoding / type support check (PLAIN, dictionary, RLE bool, DELTA_BINARY_PACKED ints, BSS)
+    bool supported = false;
+    if (enc == 0) supported = true;
+    else if (dict) supported = !boolean && (binary ? ck.dict_pos != nullptr : ck.dict_data != nullptr);
+    else if (enc == 3) supported = boolean;
+    else if (enc == 5) supported = (ck.ptype == 1 || ck.ptype == 2) && pg.aux != nullptr;
+    else if (enc == 9) supported = (ck.ptype == 4 || ck.ptype == 5);
+    if (!supported) { if (tid == 0) set_status(res, pg.chunk, dict ? ST_CORRUPT : ST_ENCODING, pi); return; }
+    if (dict && id_bw > 32) { if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
+    if (binary && !ck.chars) return;   // capacity error already recorded by k_scan
+
+    // bases
+    uint64_t slot_base = counted ? uint64_t(pg.slot_start) : uint64_t(pg.entry_start);
+    uint64_t row_base = counted ? uint64_t(pg.row_start) : uint64_t(pg.entry_start);
+    uint64_t char_base = counted ? uint64_t(pg.char_start) : 0;
+    uint64_t vidx = 0;   // page-relative index of the next present value
+    const uint64_t bss_total = (enc == 9 && w > 0) ? s.val_n / uint64_t(w) : 0;
+    if (enc == 9 && pg.num_values > 0 && tid == 0) { /* validated per value below */ }
+
+    for (uint64_t e0 = 0; e0 < uint64_t(pg.num_values); e0 += TILE) {
+        uint32_t want = uint32_t(min<uint64_t>(TILE, uint64_t(pg.num_values) - e0));
+        decode_level_tile(L, s, ck, e0, want);
+        if (L.err) break;
+        // per-thread: EPT consecutive entries
+        const uint32_t eb = uint32_t(tid) * EPT;
+        uint32_t fs = 0, fv = 0, fr = 0;   // bit flags per local entry
+        #pragma unroll
+        for (int k = 0; k < EPT; k++) {
+            uint32_t e = eb + k;
+            if (e < want) {
+                int d = L.def[e];
+                fs |= uint32_t(ck.max_rep == 0 || d >= ck.repeated_def) << k;
+                fv |= uint32_t(d == ck.max_def) << k;
+                fr |= uint32_t(L.rep[e] == 0) << k;
+            }
+        }
+        uint32_t ts, tv, tr;
+        uint32_t so = block_excl_scan<NT>(__popc(fs), S.scan_tmp, ts);
+        uint32_t vo = block_excl_scan<NT>(__popc(fv), S.scan_tmp, tv);
+        uint32_t ro = block_excl_scan<NT>(__popc(fr), S.scan_tmp, tr);
+
+        // dictionary ids / RLE booleans for this tile's present values
+        if ((dict || (boolean && enc == 3)) && tv > 0) {
+            if (tid == 0) {
+                const uint8_t* vp = dict ? s.val : rle_bool_p;
+                uint64_t vn = dict ? s.val_n : rle_bool_n;
+                int bw = dict ? id_bw : 1;
+                if (binary && dict) S.npval = 0;   // ids were kept by k_count
+                else {
+                    uint32_t got = rle_walk(S.sval, vp, vn, bw, tv, S.pval, TILE, S.npval);
+                    if (got != tv || S.sval.err) S.verr = 1;
+                }
+            }
+            __syncthreads();
+            if (S.verr) break;
+            if (binary && dict) {
+                for (uint32_t i = tid; i < tv; i += NT) S.ids[i] = pg.aux[vidx + i];
+            } else {
+                rle_expand<uint32_t>(S.pval, S.npval, dict ? s.val : rle_bool_p, dict ? s.val_n : rle_bool_n,
+                                     dict ? id_bw : 1, S.ids);
+            }
+            __syncthreads();
+        }
+        // BYTE_ARRAY: per-slot lengths -> char offsets (scan over slots in entry order)
+        uint32_t my_len[EPT];
+        uint64_t my_src[EPT];
+        uint32_t lsum = 0;
+        if (binary) {
+            uint32_t v = vo;
+            #pragma unroll
+            for (int k = 0; k < EPT; k++) {
+                my_len[k] = 0; my_src[k] = 0;
+                if ((fv >> k) & 1) {
+                    uint64_t gv = vidx + v;
+                    if (dict) {
+                        uint32_t id = S.ids[v];
+                        if (int64_t(id) < ck.dict_n) { my_src[k] = ck.dict_pos[id]; my_len[k] = ck.dict_len[id]; }
+                        else S.verr = 1;
+                    } else {
+                        uint32_t p = pg.aux[gv];
+                        uint32_t l = (p >= 4 && p <= s.val_n) ? ld32le(s.val, p - 4, s.val_n) : 0xffffffffu;
+                        if (l <= s.val_n - p) { my_src[k] = p; my_len[k] = l; }
+                        else S.verr = 1;
+                    }
+                    v++;
+                }
+                lsum += my_len[k];
+            }
+        }
+        uint32_t tchars = 0;
+        uint32_t lo = binary ? block_excl_scan<NT>(lsum, S.scan_tmp, tchars) : 0;
+        if (binary && (S.verr || char_base + tchars > uint64_t(pg.char_start + pg.n_chars))) {
+            S.verr = 1;   // inconsistent with k_count's sizing: never write past this page's chars
+            break;
+        }
+
+        // validity / list-validity bit staging
+        const uint64_t vb0 = slot_base + 0;      // first slot of this tile
+        for (uint32_t i = tid; i < TILE / 32 + 2; i += NT) { S.vbits[i] = 0; S.lbits[i] = 0; }
+        __syncthreads();
+
+        // per-entry writes
+        {
+            uint32_t sidx = so, vv = vo, ridx = ro;
+            uint64_t cpos = char_base + lo;
+            #pragma unroll
+            for (int k = 0; k < EPT; k++) {
+                uint32_t e = eb + k;
+                if (e >= want) break;
+                const bool is_slot = (fs >> k) & 1, present = (fv >> k) & 1, rstart = (fr >> k) & 1;
+                if (ck.max_rep > 0) {
+                    uint64_t ge = uint64_t(pg.entry_start) + e0 + e;
+                    if (ck.def_levels) ck.def_levels[ge] = L.def[e];
+                    if (ck.rep_levels) ck.rep_levels[ge] = L.rep[e];
+                    if (rstart && ck.max_rep == 1) {
+                        uint64_t row = row_base + ridx;
+                        if (ck.list_offsets) ck.list_offsets[row] = int32_t(slot_base + sidx);
+                        if (L.def[e] >= ck.list_null_def) {
+                            uint64_t rb = row - (row_base & ~uint64_t(31));
+                            atomicOr(&S.lbits[rb >> 5], 1u << (rb & 31));
+                        }
+                    }
+                }
+                if (rstart) ridx++;
+                if (!is_slot) continue;
+                const uint64_t slot = slot_base + sidx;
+                if (present && ck.max_def > 0) {
+                    uint64_t rb = slot - (vb0 & ~uint64_t(31));
+                    atomicOr(&S.vbits[rb >> 5], 1u << (rb & 31));
+                }
+                if (binary) {
+                    if (present) {
+                        const uint8_t* src = dict ? ck.dict_data + my_src[k] : s.val + my_src[k];
+                        for (uint32_t j = 0; j < my_len[k]; j++) ck.chars[cpos + j] = src[j];
+                        cpos += my_len[k];
+                    }
+                    ck.offsets[slot + 1] = int32_t(cpos);
+                } else if (present) {
+                    const uint64_t gv = vidx + vv;
+                    uint8_t* dst = ck.values + slot * uint64_t(w);
+                    if (dict) {
+                        uint32_t id = S.ids[vv];
+                        if (int64_t(id) >= ck.dict_n) { S.verr = 1; }
+                        else copy_value(dst, ck.dict_data + uint64_t(id) * w, w);
+                    } else if (boolean) {
+                        uint32_t b = (enc == 3) ? S.ids[vv] : ((ld8(s.val, gv >> 3, s.val_n) >> (gv & 7)) & 1);
+                        if (enc == 0 && (gv >> 3) >= s.val_n) S.verr = 1;
+                        dst[0] = uint8_t(b);
+                    } else if (enc == 0) {
+                        if ((gv + 1) * uint64_t(w) > s.val_n) S.verr = 1;
+                        else copy_value(dst, s.val + gv * w, w);
+                    } else if (enc == 5) {
+                        const uint64_t* dv = reinterpret_cast<const uint64_t*>(pg.aux);
+                        if (w == 8) *reinterpret_cast<uint64_t*>(dst) = dv[gv];
+                        else *reinterpret_cast<uint32_t*>(dst) = uint32_t(dv[gv]);
+                    } else if (enc == 9) {
+                        if (gv >= bss_total) S.verr = 1;
+                        else for (int b = 0; b < w; b++) dst[b] = s.val[uint64_t(b) * bss_total + gv];
+                    }
+                } else {
+                    zero_value(ck.values + slot * uint64_t(w), w);
+                }
+                if (present) vv++;
+                sidx++;
+            }
+        }
+        __syncthreads();
+        if (S.verr) break;
+        if (ck.max_def > 0 && ck.validity) flush_bits(S.vbits, vb0, ts, ck.validity);
+        if (ck.max_rep == 1 && ck.list_validity) flush_bits(S.lbits, row_base, tr, ck.list_validity);
+        slot_base += ts;
+        row_base += tr;
+        char_base += tchars;
+        vidx += tv;
+        __syncthreads();
+    }
+    if (L.err || S.verr) { if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
+    if (!counted && tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values),
+                                        (unsigned long long)vidx);
+}
+
+// ---- launchers -------------------------------------------------------------------------------
+void launch_dict_binary(DevChunk* d_chunks, const DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
+                        hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(k_dict_binary, dim3(n), dim3(64), 0, st, d_chunks, d_pages, d_list, d_res);
+}
+void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
+                  hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(k_count, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res);
+}
+void launch_scan(DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
+                 uint8_t* arena, uint64_t cap, unsigned long long* used, hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(k_scan, dim3(n), dim3(64), 0, st, d_chunks, d_pages, d_list, d_res, arena, cap, used);
+}
+void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
+                   hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(k_decode, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res);
+}
+
+}  // namespace pf

@@ -1,0 +1,587 @@
+// pf_runtime.hip — context, batch planning and kernel orchestration behind include/pfloor.h.
+//
+// One pf_ctx per GPU (one HIP stream, growable HBM arenas, pinned staging). A decode batch is
+// any set of column chunks (a row group's selected columns, or several row groups): the host
+// turns the descriptors into flat DevChunk / DevPage / SnappyJob tables, uploads them in one
+// copy, and enqueues
+//   k_snappy -> k_dict_binary -> k_delta -> k_count -> k_scan -> k_decode
+// on the context stream. Nothing synchronises until pf_wait.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "pf_device.h"
+#include "pf_host.h"
+#include "pfloor.h"
+
+namespace pf {
+void launch_snappy(const SnappyJob*, int, DevChunkResult*, hipStream_t);
+void launch_dict_binary(DevChunk*, const DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
+void launch_decode(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+}  // namespace pf
+
+using namespace pf;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(pf_ctx* ctx, int code, const std::string& msg);
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        size_t want = std::max<size_t>(n + n / 4, 1 << 20);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
+        size_t want = std::max<size_t>(n + n / 4, 1 << 16);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
+};
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+constexpr int N_EVENTS = 8;   // h2d, snappy, dict, delta, count, scan, decode
+
+}  // namespace
+
+struct pf_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[N_EVENTS] = {};
+    std::string err;
+    DevBuf d_in, d_scratch, d_out, d_bits, d_chars, d_meta;
+    HostBuf h_meta, h_res;
+    // last batch
+    int n_chunks = 0;
+    bool pending = false;
+    bool timing_valid = false;
+    std::vector<DevChunk> chunks;          // host copies (device pointers)
+    std::vector<DevPage> pages;
+    std::vector<SnappyJob> jobs;
+    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_decode;
+    std::vector<int64_t> host_status;      // per chunk host-side planning errors
+    std::vector<pf_column_info> info;
+    size_t bits_bytes = 0;
+    size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
+    uint64_t chars_need = 0;
+    const uint8_t* d_bytes = nullptr;
+    int reruns = 0;
+};
+
+namespace {
+
+int fail(pf_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->err = msg;
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                     \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(ctx, PF_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+int type_width(int ptype, int type_length) {
+    switch (ptype) {
+    case PF_BOOLEAN: return 1;
+    case PF_INT32: case PF_FLOAT: return 4;
+    case PF_INT64: case PF_DOUBLE: return 8;
+    case PF_INT96: return 12;
+    case PF_BYTE_ARRAY: return 0;
+    case PF_FIXED_LEN_BYTE_ARRAY: return type_length > 0 ? type_length : -1;
+    default: return -1;
+    }
+}
+
+// Enqueue the kernels of the planned batch (metadata already on device).
+int enqueue_kernels(pf_ctx* ctx) {
+    hipStream_t st = ctx->stream;
+    uint8_t* meta = static_cast<uint8_t*>(ctx->d_meta.p);
+    DevChunk* d_chunks = reinterpret_cast<DevChunk*>(meta + ctx->off_chunks);
+    DevPage* d_pages = reinterpret_cast<DevPage*>(meta + ctx->off_pages);
+    SnappyJob* d_jobs = reinterpret_cast<SnappyJob*>(meta + ctx->off_jobs);
+    DevChunkResult* d_res = reinterpret_cast<DevChunkResult*>(meta + ctx->off_res);
+    int* lists = reinterpret_cast<int*>(meta + ctx->off_lists);
+    size_t lo = 0;
+    int* d_dictbin = lists + lo; lo += ctx->l_dictbin.size();
+    int* d_delta = lists + lo; lo += ctx->l_delta.size();
+    int* d_count = lists + lo; lo += ctx->l_count.size();
+    int* d_scan = lists + lo; lo += ctx->l_scan.size();
+    int* d_decode = lists + lo; lo += ctx->l_decode.size();
+    unsigned long long* used = reinterpret_cast<unsigned long long*>(meta + ctx->meta_bytes - 256);
+
+    if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
+    HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
+    launch_snappy(d_jobs, int(ctx->jobs.size()), d_res, st);
+    HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
+    launch_dict_binary(d_chunks, d_pages, d_dictbin, int(ctx->l_dictbin.size()), d_res, st);
+    HIPCHK(ctx, hipEventRecord(ctx->ev[3], st));
+    launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), d_res, st);
+    HIPCHK(ctx, hipEventRecord(ctx->ev[4], st));
+    launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, st);
+    HIPCHK(ctx, hipEventRecord(ctx->ev[5], st));
+    launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
+                ctx->d_chars.cap, used, st);
+    HIPCHK(ctx, hipEventRecord(ctx->ev[6], st));
+    launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), d_res, st);
+    HIPCHK(ctx, hipEventRecord(ctx->ev[7], st));
+    HIPCHK(ctx, hipGetLastError());
+    // results + device-written chunk fields (chars base) back to pinned host memory
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_res.p, meta + ctx->off_res, sizeof(DevChunkResult) * ctx->n_chunks,
+                               hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(ctx->h_res.p) + align_up(sizeof(DevChunkResult) * ctx->n_chunks, 256),
+                               d_chunks, sizeof(DevChunk) * ctx->n_chunks, hipMemcpyDeviceToHost, st));
+    return PF_OK;
+}
+
+// Upload metadata tables (results zeroed, arena counter zeroed).
+int upload_meta(pf_ctx* ctx) {
+    uint8_t* h = static_cast<uint8_t*>(ctx->h_meta.p);
+    std::memset(h, 0, ctx->meta_bytes);
+    std::memcpy(h + ctx->off_chunks, ctx->chunks.data(), sizeof(DevChunk) * ctx->chunks.size());
+    std::memcpy(h + ctx->off_pages, ctx->pages.data(), sizeof(DevPage) * ctx->pages.size());
+    std::memcpy(h + ctx->off_jobs, ctx->jobs.data(), sizeof(SnappyJob) * ctx->jobs.size());
+    int* lists = reinterpret_cast<int*>(h + ctx->off_lists);
+    size_t lo = 0;
+    for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_decode}) {
+        std::copy(v->begin(), v->end(), lists + lo);
+        lo += v->size();
+    }
+    DevChunkResult* r = reinterpret_cast<DevChunkResult*>(h + ctx->off_res);
+    for (int c = 0; c < ctx->n_chunks; c++) {
+        r[c].status = int32_t(ctx->host_status[c]);
+        r[c].err_page = -1;
+        const DevChunk& ck = ctx->chunks[c];
+        if (!ck.needs_count) {   // flat fixed width: slots = rows = entries (host-known)
+            r[c].num_slots = ck.num_entries;
+            r[c].num_rows = ck.num_entries;
+        }
+    }
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_meta.p, h, ctx->meta_bytes, hipMemcpyHostToDevice, ctx->stream));
+    return PF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pf_abi_version(void) { return PF_ABI_VERSION; }
+
+const char* pf_last_error(pf_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int pf_device_count(int* count) {
+    if (!count) return fail(nullptr, PF_ERR_INVALID_ARG, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) { *count = 0; return fail(nullptr, PF_ERR_HIP, hipGetErrorString(e)); }
+    *count = n;
+    return PF_OK;
+}
+
+int pf_ctx_create(int device, pf_ctx** out) {
+    if (!out) return fail(nullptr, PF_ERR_INVALID_ARG, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return fail(nullptr, PF_ERR_INVALID_ARG, "no such HIP device");
+    auto ctx = std::make_unique<pf_ctx>();
+    ctx->device = device;
+    HIPCHK(nullptr, hipSetDevice(device));
+    HIPCHK(nullptr, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    for (auto& e : ctx->ev) HIPCHK(nullptr, hipEventCreate(&e));
+    *out = ctx.release();
+    return PF_OK;
+}
+
+int pf_ctx_destroy(pf_ctx* ctx) {
+    if (!ctx) return PF_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (DevBuf* b : {&ctx->d_in, &ctx->d_scratch, &ctx->d_out, &ctx->d_bits, &ctx->d_chars, &ctx->d_meta}) b->release();
+    ctx->h_meta.release();
+    ctx->h_res.release();
+    for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return PF_OK;
+}
+
+int pf_host_alloc(pf_ctx* ctx, size_t bytes, void** out) {
+    if (!out) return fail(ctx, PF_ERR_INVALID_ARG, "null out");
+    if (ctx) (void)hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+    return PF_OK;
+}
+
+int pf_host_free(pf_ctx* ctx, void* ptr) {
+    if (ptr) HIPCHK(ctx, hipHostFree(ptr));
+    return PF_OK;
+}
+
+int pf_device_alloc(pf_ctx* ctx, size_t bytes, void** out) {
+    if (!ctx || !out) return fail(ctx, PF_ERR_INVALID_ARG, "null arg");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipMalloc(out, std::max<size_t>(bytes, 1)));
+    return PF_OK;
+}
+
+int pf_device_free(pf_ctx* ctx, void* ptr) {
+    if (ptr) HIPCHK(ctx, hipFree(ptr));
+    return PF_OK;
+}
+
+int pf_memcpy_h2d(pf_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!ctx) return fail(ctx, PF_ERR_INVALID_ARG, "null ctx");
+    HIPCHK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    return PF_OK;
+}
+
+int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, const uint8_t* bytes, size_t n_bytes,
+                        int bytes_on_device) {
+    if (!ctx) return fail(nullptr, PF_ERR_INVALID_ARG, "null ctx");
+    if (n_chunks < 0 || (n_chunks > 0 && (!cds || !bytes))) return fail(ctx, PF_ERR_INVALID_ARG, "bad arguments");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "previous decode not waited for");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    ctx->n_chunks = n_chunks;
+    ctx->chunks.assign(n_chunks, DevChunk{});
+    ctx->pages.clear(); ctx->jobs.clear();
+    ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_decode.clear();
+    ctx->host_status.assign(n_chunks, 0);
+    ctx->info.assign(n_chunks, pf_column_info{});
+    ctx->reruns = 0;
+    ctx->timing_valid = false;
+
+    // ---- input bytes on device ----
+    HIPCHK(ctx, hipEventRecord(ctx->ev[0], st));
+    const uint8_t* d_bytes = bytes;
+    if (!bytes_on_device && n_bytes) {
+        HIPCHK(ctx, ctx->d_in.ensure(n_bytes));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, bytes, n_bytes, hipMemcpyHostToDevice, st));
+        d_bytes = static_cast<const uint8_t*>(ctx->d_in.p);
+    }
+    ctx->d_bytes = d_bytes;
+
+    // ---- plan: sizes of scratch / outputs ----
+    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; };
+    std::vector<PagePlan> pplan;
+    size_t scratch = 0, out = 0, bits = 0;
+    uint64_t chars_hint = 0;
+    struct OutPlan { size_t values, validity, offsets, list_offsets, list_validity, def, rep; };
+    std::vector<OutPlan> oplan(n_chunks);
+    auto take = [](size_t& cursor, size_t n, size_t a = 256) { size_t o = align_up(cursor, a); cursor = o + n; return o; };
+
+    for (int c = 0; c < n_chunks; c++) {
+        const pf_chunk_desc& cd = cds[c];
+        DevChunk& ck = ctx->chunks[c];
+        ck.ptype = cd.physical_type; ck.type_length = cd.type_length;
+        ck.width = type_width(cd.physical_type, cd.type_length);
+        ck.max_def = cd.max_def; ck.max_rep = cd.max_rep; ck.repeated_def = cd.repeated_def;
+        ck.list_null_def = cd.list_null_def; ck.codec = cd.codec;
+        ck.dict_page = -1;
+        ck.first_page = int(ctx->pages.size());
+        int64_t& hs = ctx->host_status[c];
+        if (ck.width < 0) hs = PF_ERR_UNSUPPORTED_TYPE;
+        else if (cd.codec != PF_CODEC_UNCOMPRESSED && cd.codec != PF_CODEC_SNAPPY) hs = PF_ERR_UNSUPPORTED_CODEC;
+        else if (cd.max_def < 0 || cd.max_def > 255 || cd.max_rep < 0 || cd.max_rep > 255 || cd.n_pages < 0 ||
+                 (cd.n_pages > 0 && !cd.pages) || cd.chunk_offset + cd.chunk_size > n_bytes)
+            hs = PF_ERR_INVALID_ARG;
+        ck.needs_count = (cd.physical_type == PF_BYTE_ARRAY || cd.max_rep > 0) ? 1 : 0;
+        int64_t entries = 0;
+        int dict_global = -1;
+        if (hs == 0) {
+            for (int i = 0; i < cd.n_pages; i++) {
+                const pf_page_desc& pd = cd.pages[i];
+                if (pd.offset + pd.compressed_size > cd.chunk_size) { hs = PF_ERR_CORRUPT_PAGE; break; }
+                if (pd.uncompressed_size > (1u << 29) || pd.compressed_size > (1u << 30)) { hs = PF_ERR_CORRUPT_PAGE; break; }
+                bool is_dict = pd.page_type == PF_PAGE_DICTIONARY;
+                bool v2 = pd.page_type == PF_PAGE_DATA_V2;
+                if (!is_dict && pd.page_type != PF_PAGE_DATA && !v2) continue;   // index pages
+                if (is_dict && (dict_global >= 0 || ck.n_pages > 0)) { hs = PF_ERR_CORRUPT_PAGE; break; }
+                DevPage pg{};
+                pg.chunk = c;
+                pg.encoding = pd.encoding; pg.def_enc = pd.def_encoding; pg.rep_enc = pd.rep_encoding;
+                pg.num_values = pd.num_values;
+                pg.flags = (v2 ? PG_V2 : 0) | (is_dict ? PG_DICT : 0);
+                if (pd.num_values < 0) { hs = PF_ERR_CORRUPT_PAGE; break; }
+                const uint8_t* src = d_bytes + cd.chunk_offset + pd.offset;
+                uint32_t lvl = v2 ? uint32_t(pd.rep_bytes) + uint32_t(pd.def_bytes) : 0;
+                if (v2 && (pd.rep_bytes < 0 || pd.def_bytes < 0 || lvl > pd.compressed_size || lvl > pd.uncompressed_size)) {
+                    hs = PF_ERR_CORRUPT_PAGE; break;
+                }
+                bool compressed = cd.codec == PF_CODEC_SNAPPY && (!v2 || pd.is_compressed);
+                PagePlan pp{0, ~0ull, is_dict};
+                if (v2) { pg.lvl = src; pg.rep_len = uint32_t(pd.rep_bytes); pg.def_len = uint32_t(pd.def_bytes); }
+                if (compressed) {
+                    pp.scratch_off = take(scratch, pd.uncompressed_size - lvl, 16);
+                    pg.flags |= PG_COMPRESSED;
+                    pg.body_len = pd.uncompressed_size - lvl;
+                    SnappyJob j{};
+                    j.src = src + lvl; j.src_len = pd.compressed_size - lvl; j.dst_len = pd.uncompressed_size - lvl;
+                    j.page = int(ctx->pages.size()); j.chunk = c;
+                    ctx->jobs.push_back(j);   // dst patched after scratch allocation
+                } else {
+                    pg.body = src + lvl;
+                    pg.body_len = pd.compressed_size - lvl;
+                }
+                if (is_dict) {
+                    dict_global = int(ctx->pages.size());
+                    ck.dict_page = dict_global;
+                    ck.dict_n = pd.num_values;
+                    if (pd.encoding != PF_ENC_PLAIN && pd.encoding != PF_ENC_PLAIN_DICTIONARY) { hs = PF_ERR_UNSUPPORTED_ENCODING; break; }
+                    if (cd.physical_type == PF_BOOLEAN) { hs = PF_ERR_UNSUPPORTED_ENCODING; break; }
+                    if (cd.physical_type == PF_BYTE_ARRAY) {
+                        pp.aux_off = take(scratch, 8ull * (pd.num_values + 1), 256);
+                        ctx->l_dictbin.push_back(c);
+                    } else if (uint64_t(pd.num_values) * ck.width > pg.body_len) { hs = PF_ERR_CORRUPT_PAGE; break; }
+                } else {
+                    pg.entry_start = entries;
+                    entries += pd.num_values;
+                    ck.n_pages++;
+                    if (cd.physical_type == PF_BYTE_ARRAY) pp.aux_off = take(scratch, 4ull * pd.num_values + 4, 256);
+                    else if (pd.encoding == PF_ENC_DELTA_BINARY_PACKED && (cd.physical_type == PF_INT32 || cd.physical_type == PF_INT64))
+                        pp.aux_off = take(scratch, 8ull * pd.num_values + 8, 256);
+                    if (cd.physical_type == PF_BYTE_ARRAY) chars_hint += pd.uncompressed_size;
+                }
+                pplan.push_back(pp);
+                ctx->pages.push_back(pg);
+            }
+        }
+        if (hs != 0) {   // drop this chunk's pages from every list
+            while (int(ctx->pages.size()) > ck.first_page) { ctx->pages.pop_back(); pplan.pop_back(); }
+            while (!ctx->jobs.empty() && ctx->jobs.back().chunk == c) ctx->jobs.pop_back();
+            if (!ctx->l_dictbin.empty() && ctx->l_dictbin.back() == c) ctx->l_dictbin.pop_back();
+            ck.n_pages = 0; ck.dict_page = -1; entries = 0;
+        }
+        if (ck.dict_page >= 0) ck.first_page = ck.dict_page + 1;
+        ck.num_entries = entries;
+        // outputs
+        OutPlan& op = oplan[c];
+        op = OutPlan{~size_t(0), ~size_t(0), ~size_t(0), ~size_t(0), ~size_t(0), ~size_t(0), ~size_t(0)};
+        if (hs == 0) {
+            if (ck.width > 0) op.values = take(out, size_t(entries) * ck.width);
+            if (cd.max_def > 0) op.validity = take(bits, align_up((entries + 7) / 8, 4), 256);
+            if (cd.physical_type == PF_BYTE_ARRAY) op.offsets = take(out, 4 * size_t(entries + 1));
+            if (cd.max_rep == 1) {
+                op.list_offsets = take(out, 4 * size_t(entries + 1));
+                op.list_validity = take(bits, align_up((entries + 7) / 8, 4), 256);
+            }
+            if (cd.max_rep > 0) { op.def = take(out, entries); op.rep = take(out, entries); }
+        }
+    }
+    // ---- allocate arenas ----
+    HIPCHK(ctx, ctx->d_scratch.ensure(std::max<size_t>(scratch, 1)));
+    HIPCHK(ctx, ctx->d_out.ensure(std::max<size_t>(out, 1)));
+    HIPCHK(ctx, ctx->d_bits.ensure(std::max<size_t>(bits, 1)));
+    size_t chars_cap = std::max<size_t>(size_t(2 * chars_hint) + (16u << 20), ctx->chars_need);
+    HIPCHK(ctx, ctx->d_chars.ensure(chars_cap));
+    ctx->bits_bytes = bits;
+    uint8_t* S = static_cast<uint8_t*>(ctx->d_scratch.p);
+    uint8_t* O = static_cast<uint8_t*>(ctx->d_out.p);
+    uint8_t* B = static_cast<uint8_t*>(ctx->d_bits.p);
+    {
+        size_t ji = 0;
+        for (size_t i = 0; i < ctx->pages.size(); i++) {
+            DevPage& pg = ctx->pages[i];
+            const PagePlan& pp = pplan[i];
+            if (pg.flags & PG_COMPRESSED) {
+                pg.body = S + pp.scratch_off;
+                while (ji < ctx->jobs.size() && ctx->jobs[ji].page != int(i)) ji++;
+                if (ji < ctx->jobs.size()) ctx->jobs[ji].dst = S + pp.scratch_off;
+            }
+            if (pp.aux_off != ~0ull) {
+                pg.aux = reinterpret_cast<uint32_t*>(S + pp.aux_off);
+                pg.aux_cap = pg.num_values;
+            }
+            DevChunk& ck = ctx->chunks[pg.chunk];
+            if (pp.is_dict) {
+                ck.dict_data = pg.body;
+                if (ck.ptype == PF_BYTE_ARRAY) {
+                    ck.dict_pos = reinterpret_cast<uint32_t*>(S + pp.aux_off);
+                    ck.dict_len = ck.dict_pos + (pg.num_values + 1);
+                }
+            }
+        }
+    }
+    for (int c = 0; c < n_chunks; c++) {
+        DevChunk& ck = ctx->chunks[c];
+        const OutPlan& op = oplan[c];
+        auto at = [](uint8_t* base, size_t off) { return off == ~size_t(0) ? nullptr : base + off; };
+        ck.values = at(O, op.values);
+        ck.validity = at(B, op.validity);
+        ck.offsets = reinterpret_cast<int32_t*>(at(O, op.offsets));
+        ck.list_offsets = reinterpret_cast<int32_t*>(at(O, op.list_offsets));
+        ck.list_validity = at(B, op.list_validity);
+        ck.def_levels = at(O, op.def);
+        ck.rep_levels = at(O, op.rep);
+        if (ctx->host_status[c] == 0) {
+            if (ck.needs_count) ctx->l_scan.push_back(c);
+        }
+    }
+    for (size_t i = 0; i < ctx->pages.size(); i++) {
+        const DevPage& pg = ctx->pages[i];
+        if (pg.flags & PG_DICT) continue;
+        const DevChunk& ck = ctx->chunks[pg.chunk];
+        if (pg.encoding == PF_ENC_DELTA_BINARY_PACKED && pg.aux && ck.ptype != PF_BYTE_ARRAY) ctx->l_delta.push_back(int(i));
+        if (ck.needs_count) ctx->l_count.push_back(int(i));
+        ctx->l_decode.push_back(int(i));
+    }
+    // ---- metadata upload ----
+    size_t m = 0;
+    ctx->off_chunks = take(m, sizeof(DevChunk) * n_chunks);
+    ctx->off_pages = take(m, sizeof(DevPage) * ctx->pages.size());
+    ctx->off_jobs = take(m, sizeof(SnappyJob) * ctx->jobs.size());
+    ctx->off_lists = take(m, sizeof(int) * (ctx->l_dictbin.size() + ctx->l_delta.size() + ctx->l_count.size() +
+                                            ctx->l_scan.size() + ctx->l_decode.size()));
+    ctx->off_res = take(m, sizeof(DevChunkResult) * n_chunks);
+    m = take(m, 256) + 256;   // arena counter lives in the last 256 bytes
+    ctx->meta_bytes = m;
+    HIPCHK(ctx, ctx->d_meta.ensure(m));
+    HIPCHK(ctx, ctx->h_meta.ensure(m));
+    HIPCHK(ctx, ctx->h_res.ensure(align_up(sizeof(DevChunkResult) * n_chunks, 256) + sizeof(DevChunk) * n_chunks + 256));
+    int rc = upload_meta(ctx);
+    if (rc) return rc;
+    rc = enqueue_kernels(ctx);
+    if (rc) return rc;
+    ctx->pending = true;
+    return PF_OK;
+}
+
+int pf_wait(pf_ctx* ctx) {
+    if (!ctx) return fail(nullptr, PF_ERR_INVALID_ARG, "null ctx");
+    if (!ctx->pending) return fail(ctx, PF_ERR_STATE, "nothing to wait for");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    for (;;) {
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) { ctx->pending = false; return fail(ctx, PF_ERR_HIP, std::string("decode: ") + hipGetErrorString(e)); }
+        const DevChunkResult* r = static_cast<const DevChunkResult*>(ctx->h_res.p);
+        const DevChunk* dc = reinterpret_cast<const DevChunk*>(static_cast<uint8_t*>(ctx->h_res.p) +
+                                                               align_up(sizeof(DevChunkResult) * ctx->n_chunks, 256));
+        // chars arena overflow: grow to the exact need and run the batch once more
+        uint64_t need = 0;
+        bool overflow = false;
+        for (int c = 0; c < ctx->n_chunks; c++) {
+            if (ctx->chunks[c].ptype == PF_BYTE_ARRAY) need += align_up(uint64_t(std::max<int64_t>(r[c].num_chars, 0)), 256);
+            if (r[c].status == PF_ERR_CAPACITY && ctx->chunks[c].ptype == PF_BYTE_ARRAY && r[c].num_chars <= 0x7fffffff)
+                overflow = true;
+        }
+        if (overflow && ctx->reruns == 0) {
+            ctx->reruns++;
+            ctx->chars_need = size_t(need) + (1u << 20);
+            HIPCHK(ctx, ctx->d_chars.ensure(ctx->chars_need));
+            int rc = upload_meta(ctx);
+            if (rc) { ctx->pending = false; return rc; }
+            rc = enqueue_kernels(ctx);
+            if (rc) { ctx->pending = false; return rc; }
+            continue;
+        }
+        int first_err = PF_OK;
+        for (int c = 0; c < ctx->n_chunks; c++) {
+            pf_column_info& ci = ctx->info[c];
+            const DevChunk& ck = ctx->chunks[c];
+            ci.num_entries = ck.num_entries;
+            ci.num_slots = r[c].num_slots;
+            ci.num_values = r[c].num_values;
+            ci.num_rows = r[c].num_rows;
+            ci.num_chars = ck.ptype == PF_BYTE_ARRAY ? r[c].num_chars : 0;
+            ci.width = ck.width;
+            ci.status = r[c].status;
+            ci.d_values = ck.values;
+            ci.d_validity = ck.validity;
+            ci.d_offsets = ck.offsets;
+            ci.d_chars = dc[c].chars;
+            ci.d_list_offsets = ck.list_offsets;
+            ci.d_list_validity = ck.list_validity;
+            ci.d_def_levels = ck.def_levels;
+            ci.d_rep_levels = ck.rep_levels;
+            if (ci.status != 0 && first_err == PF_OK) {
+                first_err = ci.status;
+                char buf[160];
+                std::snprintf(buf, sizeof buf, "chunk %d: decode failed (status %d, page %d)", c, ci.status, r[c].err_page);
+                fail(ctx, first_err, buf);
+            }
+        }
+        ctx->pending = false;
+        ctx->timing_valid = true;
+        return first_err;
+    }
+}
+
+int pf_column_info_get(pf_ctx* ctx, int chunk, pf_column_info* out) {
+    if (!ctx || !out) return fail(ctx, PF_ERR_INVALID_ARG, "null arg");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
+    if (chunk < 0 || chunk >= ctx->n_chunks) return fail(ctx, PF_ERR_INVALID_ARG, "chunk index out of range");
+    *out = ctx->info[chunk];
+    return PF_OK;
+}
+
+int pf_copy_column(pf_ctx* ctx, int chunk, const pf_column_out* o) {
+    if (!ctx || !o) return fail(ctx, PF_ERR_INVALID_ARG, "null arg");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
+    if (chunk < 0 || chunk >= ctx->n_chunks) return fail(ctx, PF_ERR_INVALID_ARG, "chunk index out of range");
+    const pf_column_info& ci = ctx->info[chunk];
+    if (ci.status != 0) return fail(ctx, ci.status, "chunk failed to decode");
+    struct Item { void* dst; size_t cap; const void* src; size_t n; };
+    Item items[8] = {
+        {o->values, o->values_cap, ci.d_values, size_t(ci.num_slots) * size_t(ci.width)},
+        {o->validity, o->validity_cap, ci.d_validity, size_t((ci.num_slots + 7) / 8)},
+        {o->offsets, o->offsets_cap, ci.d_offsets, ci.d_offsets ? 4 * size_t(ci.num_slots + 1) : 0},
+        {o->chars, o->chars_cap, ci.d_chars, size_t(ci.num_chars)},
+        {o->list_offsets, o->list_offsets_cap, ci.d_list_offsets, ci.d_list_offsets ? 4 * size_t(ci.num_rows + 1) : 0},
+        {o->list_validity, o->list_validity_cap, ci.d_list_validity, size_t((ci.num_rows + 7) / 8)},
+        {o->def_levels, o->def_levels_cap, ci.d_def_levels, size_t(ci.num_entries)},
+        {o->rep_levels, o->rep_levels_cap, ci.d_rep_levels, size_t(ci.num_entries)},
+    };
+    for (const Item& it : items)
+        if (it.dst && it.src && it.n > it.cap) return fail(ctx, PF_ERR_CAPACITY, "output buffer too small");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    for (const Item& it : items)
+        if (it.dst && it.src && it.n) HIPCHK(ctx, hipMemcpyAsync(it.dst, it.src, it.n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return PF_OK;
+}
+
+int pf_last_timing(pf_ctx* ctx, float* stage_ms, int n_stages, int* n_written) {
+    if (!ctx || !stage_ms || n_stages < 0) return fail(ctx, PF_ERR_INVALID_ARG, "bad arg");
+    if (!ctx->timing_valid) return fail(ctx, PF_ERR_STATE, "no finished decode");
+    int k = 0;
+    for (int i = 0; i + 1 < N_EVENTS && k < n_stages; i++, k++) {
+        float ms = 0;
+        HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]));
+        stage_ms[k] = ms;
+    }
+    if (n_written) *n_written = k;
+    return PF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,186 @@
+// pf_snappy.hip — K1: Snappy page decompression on gfx950.
+//
+// Replaces snappy-java's Snappy.uncompress (JNI into Google Snappy), which parquet-mr reaches
+// per page through the Hadoop codec shim (src/main/java/org/apache/hadoop/io/compress/
+// DecompressorStream.java:61-70,101-173; CodecPool.java:6-8; ReflectionUtils.java:10-21).
+//
+// Raw Snappy: varint uncompressed length, then tags
+//   00 literal  (len-1 in tag>>2; 60..63 -> 1..4 LE length bytes follow)
+//   01 copy     (len 4..11 = 4 + (tag>>2 & 7), offset = (tag>>5)<<8 | next byte)
+//   10 copy     (len (tag>>2)+1, 16-bit LE offset)
+//   11 copy     (len (tag>>2)+1, 32-bit LE offset)
+// Copies may overlap their own output (offset < length).
+//
+// Design (one 64-lane wave per page):
+//  * the output window lives in a 64 KiB LDS ring; byte j of a copy reads position
+//    op - off + (j mod off), which always precedes op, so all 64 lanes can copy one token in a
+//    single read-then-write step even when it overlaps itself;
+//  * copies whose offset reaches past the ring read the already-flushed HBM output (a wave's
+//    own stores are ordered before its later loads);
+//  * tokens are parsed in batches into LDS and executed in order; finished output is flushed
+//    ring -> HBM with 16-byte coalesced stores.
+#include <hip/hip_runtime.h>
+
+#include "pf_device.h"
+
+namespace pf {
+
+constexpr uint32_t RING = 65536;
+constexpr uint32_t RMASK = RING - 1;
+constexpr int TOK_BATCH = 256;
+constexpr uint32_t FLUSH_AT = 16384;
+
+struct Token {
+    uint32_t src;    // literal: input byte position; copy: offset
+    uint32_t len;
+    uint32_t out;    // output position
+    uint32_t lit;
+};
+
+__device__ __forceinline__ void flush(const uint8_t* ring, uint8_t* dst, uint32_t from, uint32_t to) {
+    // bytes [from, to) of the output are final in the ring; store them to HBM
+    const int lane = threadIdx.x;
+    // align the bulk to 16 B in the destination
+    uint32_t head = min(to, (from + 15u) & ~15u);
+    for (uint32_t q = from + lane; q < head; q += WAVE) dst[q] = ring[q & RMASK];
+    for (uint32_t q = head + uint32_t(lane) * 16u; q + 16u <= to; q += WAVE * 16u) {
+        uint4 v;
+        uint8_t* b = reinterpret_cast<uint8_t*>(&v);
+        #pragma unroll
+        for (int k = 0; k < 16; k++) b[k] = ring[(q + k) & RMASK];
+        *reinterpret_cast<uint4*>(dst + q) = v;
+    }
+    uint32_t tail_start = head + ((to > head ? to - head : 0) & ~15u);
+    for (uint32_t q = tail_start + lane; q < to; q += WAVE) dst[q] = ring[q & RMASK];
+}
+
+__global__ __launch_bounds__(64) void k_snappy(const SnappyJob* __restrict__ jobs, DevChunkResult* res) {
+    __shared__ uint8_t ring[RING];
+    __shared__ Token toks[TOK_BATCH];
+    __shared__ int ntok_s, err_s;
+    __shared__ uint32_t ip_s;
+
+    const SnappyJob job = jobs[blockIdx.x];
+    const uint8_t* in = job.src;
+    const uint64_t n = job.src_len;
+    uint8_t* dst = job.dst;
+    const int lane = threadIdx.x;
+
+    // preamble: uncompressed length
+    uint64_t pos = 0, ulen = 0;
+    bool ok = uvarint(in, n, pos, ulen) && ulen == job.dst_len;
+    if (!ok) {
+        if (lane == 0) set_status(res, job.chunk, ST_CORRUPT, job.page);
+        return;
+    }
+    if (lane == 0) { ip_s = uint32_t(pos); err_s = 0; }
+    __syncthreads();
+
+    uint32_t op = 0, flushed = 0;
+    for (;;) {
+        // ---- parse a batch of tokens (lane 0, serial) ----
+        if (lane == 0) {
+            uint64_t ip = ip_s;
+            uint32_t o = op;
+            int nt = 0, err = 0;
+            while (nt < TOK_BATCH && ip < n) {
+                uint32_t tag = in[ip++];
+                Token t;
+                t.out = o;
+                if ((tag & 3) == 0) {
+                    uint32_t len = tag >> 2;
+                    if (len >= 60) {
+                        uint32_t nb = len - 59;
+                        if (ip + nb > n) { err = 1; break; }
+                        len = 0;
+                        for (uint32_t k = 0; k < nb; k++) len |= uint32_t(in[ip + k]) << (8 * k);
+                        ip += nb;
+                    }
+                    uint64_t l64 = uint64_t(len) + 1;
+                    if (ip + l64 > n || o + l64 > ulen) { err = 1; break; }
+                    t.src = uint32_t(ip); t.len = uint32_t(l64); t.lit = 1;
+                    ip += l64;
+                } else {
+                    uint32_t len, off;
+                    if ((tag & 3) == 1) {
+                        if (ip + 1 > n) { err = 1; break; }
+                        len = 4 + ((tag >> 2) & 7);
+                        off = ((tag >> 5) << 8) | in[ip];
+                        ip += 1;
+                    } else if ((tag & 3) == 2) {
+                        if (ip + 2 > n) { err = 1; break; }
+                        len = (tag >> 2) + 1;
+                        off = uint32_t(in[ip]) | uint32_t(in[ip + 1]) << 8;
+                        ip += 2;
+                    } else {
+                        if (ip + 4 > n) { err = 1; break; }
+                        len = (tag >> 2) + 1;
+                        off = ld32le(in, ip, n);
+                        ip += 4;
+                    }
+                    if (off == 0 || off > o || uint64_t(o) + len > ulen) { err = 1; break; }
+                    t.src = off; t.len = len; t.lit = 0;
+                }
+                o += t.len;
+                toks[nt++] = t;
+            }
+            ntok_s = nt;
+            ip_s = uint32_t(ip);
+            err_s = err;
+        }
+        __syncthreads();
+        const int nt = ntok_s;
+        if (err_s) break;
+        // ---- execute tokens in order ----
+        for (int i = 0; i < nt; i++) {
+            Token t = toks[i];
+            if (t.lit) {
+                uint32_t done = 0;
+                while (done < t.len) {
+                    uint32_t chunk = min(t.len - done, 8192u);
+                    if (t.out + done + chunk - flushed > RING) {   // keep unflushed bytes in the ring
+                        __syncthreads();
+                        flush(ring, dst, flushed, t.out + done);
+                        flushed = t.out + done;
+                        __syncthreads();
+                    }
+                    for (uint32_t j = lane; j < chunk; j += WAVE)
+                        ring[(t.out + done + j) & RMASK] = in[t.src + done + j];
+                    done += chunk;
+                }
+            } else {
+                uint32_t j = lane;
+                uint8_t v = 0;
+                if (j < t.len) {
+                    uint32_t s = t.out - t.src + (j % t.src);
+                    v = (t.src <= RING - 64) ? ring[s & RMASK] : dst[s];
+                }
+                __syncthreads();   // single wave: orders the reads before the writes
+                if (j < t.len) ring[(t.out + j) & RMASK] = v;
+            }
+            uint32_t end = t.out + t.len;
+            if (end - flushed >= FLUSH_AT) {
+                __syncthreads();
+                flush(ring, dst, flushed, end);
+                flushed = end;
+                __syncthreads();
+            }
+            op = end;
+        }
+        __syncthreads();
+        if (nt < TOK_BATCH) break;   // input exhausted
+    }
+    __syncthreads();
+    if (err_s || op != ulen) {
+        if (lane == 0) set_status(res, job.chunk, ST_CORRUPT, job.page);
+        return;
+    }
+    flush(ring, dst, flushed, op);
+}
+
+void launch_snappy(const SnappyJob* d_jobs, int n_jobs, DevChunkResult* d_res, hipStream_t s) {
+    if (n_jobs <= 0) return;
+    hipLaunchKernelGGL(k_snappy, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_res);
+}
+
+}  // namespace pf
