@@ -187,6 +187,14 @@ int pf_copy_column(pf_ctx* ctx, int chunk, const pf_column_out* out);
 /* Kernel timing of the last decode (sum of per-stage HIP-event times, ms). */
 int pf_last_timing(pf_ctx* ctx, float* stage_ms, int n_stages, int* n_written);
 
+/* Decompress one raw Snappy buffer (snappy-java Snappy.uncompress semantics) with the
+ * page kernels (K1). Host buffers; synchronous. *out_len = uncompressed length.
+ * Invalidates the results of the last pf_decode_row_group on this context. */
+int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
+/* 1 if the last pf_snappy_decompress needed the serial fallback kernel (stream not split into
+ * independent 64 KiB blocks, or corrupt), 0 if the block-parallel kernels decoded it. */
+int pf_snappy_last_fallback(pf_ctx* ctx);
+
 /* ---- host-side metadata parse: the stand-in for the Java side's parquet-mr footer /
  *      PageHeader parse (ParquetFileReader.open + readNextRowGroup,
  *      ParquetReader.java:120, :183). Builds the descriptors above from a file. ---- */
@@ -216,6 +224,7 @@ int pf_file_chunk_desc(pf_file* f, int row_group, int column, uint64_t chunk_off
 /* Read raw bytes of the file (host). */
 int pf_file_read(pf_file* f, uint64_t offset, uint64_t size, void* dst);
 const char* pf_file_created_by(pf_file* f);
+const char* pf_file_last_error(void);            /* thread-local message of the last pf_file_* error */
 
 #ifdef __cplusplus
 }

@@ -417,6 +417,64 @@ int64_t pfo_snappy_uncompress(const uint8_t* in, size_t n, uint8_t* out, size_t 
     return (int64_t)op;
 }
 
+/* Test-vector generator (NOT part of the decode restatement): a greedy Snappy compressor.
+ * mode 0 = Google-style: independent 64 KiB blocks (what snappy-java produces);
+ * mode 1 = one window over the whole input: copies reach back across 64 KiB blocks
+ *          (valid Snappy that exercises the decoder's non-block path). Returns bytes or <0. */
+static size_t put_varint(uint8_t* o, uint64_t v) { size_t i = 0; while (v >= 128) { o[i++] = (uint8_t)(v | 128); v >>= 7; } o[i++] = (uint8_t)v; return i; }
+static size_t emit_literal(uint8_t* o, const uint8_t* s, size_t len) {
+    size_t i = 0, n = len - 1;
+    if (n < 60) o[i++] = (uint8_t)(n << 2);
+    else { int nb = n < 256 ? 1 : n < 65536 ? 2 : n < (1u << 24) ? 3 : 4; o[i++] = (uint8_t)((59 + nb) << 2); for (int k = 0; k < nb; k++) o[i++] = (uint8_t)(n >> (8 * k)); }
+    memcpy(o + i, s, len);
+    return i + len;
+}
+static size_t emit_copy(uint8_t* o, size_t off, size_t len) {
+    size_t i = 0;
+    while (len > 0) {
+        size_t l = len > 64 ? (len - 64 >= 4 ? 64 : len - 4) : len;
+        if (l >= 4 && l <= 11 && off < 2048) { o[i++] = (uint8_t)(1 | ((l - 4) << 2) | ((off >> 8) << 5)); o[i++] = (uint8_t)off; }
+        else if (off < 65536) { o[i++] = (uint8_t)(2 | ((l - 1) << 2)); o[i++] = (uint8_t)off; o[i++] = (uint8_t)(off >> 8); }
+        else { o[i++] = (uint8_t)(3 | ((l - 1) << 2)); for (int k = 0; k < 4; k++) o[i++] = (uint8_t)(off >> (8 * k)); }
+        len -= l;
+    }
+    return i;
+}
+int64_t pfo_snappy_compress(const uint8_t* in, size_t n, uint8_t* out, size_t cap, int mode) {
+    if (cap < 32 + n + n / 6) return E_CAP;
+    size_t o = put_varint(out, n);
+    enum { HB = 14 };
+    int64_t* table = (int64_t*)malloc(sizeof(int64_t) << HB);
+    size_t bstart = 0;
+    for (int i = 0; i < (1 << HB); i++) table[i] = -1;
+    while (bstart < n) {
+        /* mode 0/2: tokens never cross a 64 KiB output boundary; mode 0 also restarts the match
+         * window per block, mode 2 keeps matching into earlier blocks (cross-block copies). */
+        size_t bend = mode == 1 ? n : (n - bstart > 65536 ? bstart + 65536 : n);
+        if (mode == 0) for (int i = 0; i < (1 << HB); i++) table[i] = -1;
+        size_t lo = mode == 0 ? bstart : 0;
+        size_t i = bstart, lit = bstart;
+        while (i + 4 <= bend) {
+            uint32_t v = (uint32_t)in[i] | (uint32_t)in[i + 1] << 8 | (uint32_t)in[i + 2] << 16 | (uint32_t)in[i + 3] << 24;
+            uint32_t h = (v * 0x1e35a7bdu) >> (32 - HB);
+            int64_t cand = table[h];
+            table[h] = (int64_t)i;
+            if (cand >= (int64_t)lo && memcmp(in + cand, in + i, 4) == 0) {
+                size_t len = 4;
+                while (i + len < bend && in[cand + len] == in[i + len]) len++;
+                if (lit < i) o += emit_literal(out + o, in + lit, i - lit);
+                o += emit_copy(out + o, i - (size_t)cand, len);
+                i += len;
+                lit = i;
+            } else i++;
+        }
+        if (lit < bend) o += emit_literal(out + o, in + lit, bend - lit);
+        bstart = bend;
+    }
+    free(table);
+    return (int64_t)o;
+}
+
 /* ------------------------------------------------------------------ bit helpers */
 static int bit_width_of(uint32_t max_level) {  /* BytesUtils.getWidthFromMaxInt */
     int w = 0; while (max_level) { w++; max_level >>= 1; } return w;

@@ -55,6 +55,8 @@ void pfo_free_column(pfo_column* c);
 /* Raw Snappy (snappy-java Snappy.uncompress / Google Snappy format). Returns bytes written or <0. */
 int64_t pfo_snappy_uncompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap);
 int64_t pfo_snappy_uncompressed_length(const uint8_t* in, size_t n);
+/* Test-vector generator: greedy Snappy compressor (mode 0 Google-style 64 KiB blocks, mode 1 cross-block). */
+int64_t pfo_snappy_compress(const uint8_t* in, size_t n, uint8_t* out, size_t cap, int mode);
 
 #ifdef __cplusplus
 }

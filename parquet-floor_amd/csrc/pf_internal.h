@@ -27,6 +27,8 @@ struct SnappyJob {
     uint32_t dst_len;
     int32_t page;         // global page index (for error attribution)
     int32_t chunk;
+    uint32_t split_base;  // first entry of this job's 64 KiB split table
+    uint32_t n_pieces;    // ceil(dst_len / 65536), >= 1
 };
 
 struct DevPage {

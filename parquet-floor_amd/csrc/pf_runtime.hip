@@ -22,7 +22,9 @@
 #include "pfloor.h"
 
 namespace pf {
-void launch_snappy(const SnappyJob*, int, DevChunkResult*, hipStream_t);
+void launch_snappy_index(const SnappyJob*, const int*, int, uint32_t*, int*, hipStream_t);
+void launch_snappy_exec(const SnappyJob*, const int2*, int, const uint32_t*, int*, hipStream_t);
+void launch_snappy_serial(const SnappyJob*, int, const int*, DevChunkResult*, hipStream_t);
 void launch_dict_binary(DevChunk*, const DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
@@ -86,11 +88,14 @@ struct pf_ctx {
     std::vector<DevChunk> chunks;          // host copies (device pointers)
     std::vector<DevPage> pages;
     std::vector<SnappyJob> jobs;
-    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_decode;
+    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_decode, l_index;
+    std::vector<int2> pieces;
+    uint32_t n_splits = 0;
     std::vector<int64_t> host_status;      // per chunk host-side planning errors
     std::vector<pf_column_info> info;
     size_t bits_bytes = 0;
     size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
+    size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_index = 0;
     uint64_t chars_need = 0;
     const uint8_t* d_bytes = nullptr;
     int reruns = 0;
@@ -139,10 +144,16 @@ int enqueue_kernels(pf_ctx* ctx) {
     int* d_scan = lists + lo; lo += ctx->l_scan.size();
     int* d_decode = lists + lo; lo += ctx->l_decode.size();
     unsigned long long* used = reinterpret_cast<unsigned long long*>(meta + ctx->meta_bytes - 256);
+    const int2* d_pieces = reinterpret_cast<const int2*>(meta + ctx->off_pieces);
+    uint32_t* d_splits = reinterpret_cast<uint32_t*>(meta + ctx->off_splits);
+    int* d_fallback = reinterpret_cast<int*>(meta + ctx->off_fallback);
+    const int* d_index = reinterpret_cast<const int*>(meta + ctx->off_index);
 
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
-    launch_snappy(d_jobs, int(ctx->jobs.size()), d_res, st);
+    launch_snappy_index(d_jobs, d_index, int(ctx->l_index.size()), d_splits, d_fallback, st);
+    launch_snappy_exec(d_jobs, d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, st);
+    launch_snappy_serial(d_jobs, int(ctx->jobs.size()), d_fallback, d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
     launch_dict_binary(d_chunks, d_pages, d_dictbin, int(ctx->l_dictbin.size()), d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], st));
@@ -171,6 +182,9 @@ int upload_meta(pf_ctx* ctx) {
     std::memcpy(h + ctx->off_chunks, ctx->chunks.data(), sizeof(DevChunk) * ctx->chunks.size());
     std::memcpy(h + ctx->off_pages, ctx->pages.data(), sizeof(DevPage) * ctx->pages.size());
     std::memcpy(h + ctx->off_jobs, ctx->jobs.data(), sizeof(SnappyJob) * ctx->jobs.size());
+    std::memcpy(h + ctx->off_pieces, ctx->pieces.data(), sizeof(int2) * ctx->pieces.size());
+    std::memset(h + ctx->off_splits, 0xff, sizeof(uint32_t) * ctx->n_splits);
+    std::memcpy(h + ctx->off_index, ctx->l_index.data(), sizeof(int) * ctx->l_index.size());
     int* lists = reinterpret_cast<int*>(h + ctx->off_lists);
     size_t lo = 0;
     for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_decode}) {
@@ -277,6 +291,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->chunks.assign(n_chunks, DevChunk{});
     ctx->pages.clear(); ctx->jobs.clear();
     ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_decode.clear();
+    ctx->l_index.clear(); ctx->pieces.clear(); ctx->n_splits = 0;
     ctx->host_status.assign(n_chunks, 0);
     ctx->info.assign(n_chunks, pf_column_info{});
     ctx->reruns = 0;
@@ -456,6 +471,16 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         if (ck.needs_count) ctx->l_count.push_back(int(i));
         ctx->l_decode.push_back(int(i));
     }
+    // ---- Snappy split tables: one piece per 64 KiB of output; index pages larger than that ----
+    for (size_t j = 0; j < ctx->jobs.size(); j++) {
+        SnappyJob& jb = ctx->jobs[j];
+        uint32_t np = std::max<uint32_t>(1u, (jb.dst_len + 65535u) / 65536u);
+        jb.split_base = ctx->n_splits;
+        jb.n_pieces = np;
+        ctx->n_splits += np;
+        if (np > 1) ctx->l_index.push_back(int(j));
+        for (uint32_t k = 0; k < np; k++) ctx->pieces.push_back(int2{int(j), int(k)});
+    }
     // ---- metadata upload ----
     size_t m = 0;
     ctx->off_chunks = take(m, sizeof(DevChunk) * n_chunks);
@@ -464,6 +489,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_lists = take(m, sizeof(int) * (ctx->l_dictbin.size() + ctx->l_delta.size() + ctx->l_count.size() +
                                             ctx->l_scan.size() + ctx->l_decode.size()));
     ctx->off_res = take(m, sizeof(DevChunkResult) * n_chunks);
+    ctx->off_pieces = take(m, sizeof(int2) * ctx->pieces.size());
+    ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);
+    ctx->off_fallback = take(m, sizeof(int) * ctx->jobs.size());
+    ctx->off_index = take(m, sizeof(int) * ctx->l_index.size());
     m = take(m, 256) + 256;   // arena counter lives in the last 256 bytes
     ctx->meta_bytes = m;
     HIPCHK(ctx, ctx->d_meta.ensure(m));
@@ -569,6 +598,73 @@ int pf_copy_column(pf_ctx* ctx, int chunk, const pf_column_out* o) {
         if (it.dst && it.src && it.n) HIPCHK(ctx, hipMemcpyAsync(it.dst, it.src, it.n, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return PF_OK;
+}
+
+int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    if (!ctx || (!src && n) || !out_len) return fail(ctx, PF_ERR_INVALID_ARG, "null arg");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "previous decode not waited for");
+    uint64_t ulen = 0;
+    size_t p = 0;
+    for (int sh = 0;; sh += 7) {
+        if (p >= n || sh > 28) return fail(ctx, PF_ERR_CORRUPT_PAGE, "snappy: bad length preamble");
+        uint8_t c = src[p++];
+        ulen |= uint64_t(c & 0x7f) << sh;
+        if (!(c & 0x80)) break;
+    }
+    *out_len = size_t(ulen);
+    if (ulen > cap) return fail(ctx, PF_ERR_CAPACITY, "snappy: destination too small");
+    if (n > 0xffffffffull || ulen > 0xffffffffull) return fail(ctx, PF_ERR_INVALID_ARG, "snappy: buffer too large");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    ctx->n_chunks = 0;
+    ctx->info.clear();
+    HIPCHK(ctx, ctx->d_in.ensure(std::max<size_t>(n, 1)));
+    HIPCHK(ctx, ctx->d_scratch.ensure(std::max<size_t>(ulen, 1) + 16));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
+    SnappyJob job{};
+    job.src = static_cast<const uint8_t*>(ctx->d_in.p);
+    job.dst = static_cast<uint8_t*>(ctx->d_scratch.p);
+    job.src_len = uint32_t(n);
+    job.dst_len = uint32_t(ulen);
+    job.n_pieces = std::max<uint32_t>(1u, uint32_t((ulen + 65535) / 65536));
+    std::vector<int2> pieces;
+    for (uint32_t k = 0; k < job.n_pieces; k++) pieces.push_back(int2{0, int(k)});
+    size_t m = 0;
+    auto take = [](size_t& cursor, size_t sz) { size_t o = align_up(cursor, 256); cursor = o + sz; return o; };
+    size_t o_job = take(m, sizeof(SnappyJob)), o_pc = take(m, sizeof(int2) * pieces.size());
+    size_t o_sp = take(m, 4 * pieces.size()), o_fb = take(m, 4), o_ix = take(m, 4), o_res = take(m, sizeof(DevChunkResult));
+    m = align_up(m, 256);
+    HIPCHK(ctx, ctx->d_meta.ensure(m));
+    HIPCHK(ctx, ctx->h_meta.ensure(m));
+    uint8_t* h = static_cast<uint8_t*>(ctx->h_meta.p);
+    std::memset(h, 0, m);
+    std::memcpy(h + o_job, &job, sizeof job);
+    std::memcpy(h + o_pc, pieces.data(), sizeof(int2) * pieces.size());
+    std::memset(h + o_sp, 0xff, 4 * pieces.size());
+    int zero = 0;
+    std::memcpy(h + o_ix, &zero, 4);
+    uint8_t* d = static_cast<uint8_t*>(ctx->d_meta.p);
+    HIPCHK(ctx, hipMemcpyAsync(d, h, m, hipMemcpyHostToDevice, st));
+    const SnappyJob* dj = reinterpret_cast<const SnappyJob*>(d + o_job);
+    launch_snappy_index(dj, reinterpret_cast<const int*>(d + o_ix), job.n_pieces > 1 ? 1 : 0,
+                        reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb), st);
+    launch_snappy_exec(dj, reinterpret_cast<const int2*>(d + o_pc), int(pieces.size()),
+                       reinterpret_cast<const uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb), st);
+    launch_snappy_serial(dj, 1, reinterpret_cast<const int*>(d + o_fb), reinterpret_cast<DevChunkResult*>(d + o_res), st);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, ctx->h_res.ensure(512));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_res.p, d + o_res, sizeof(DevChunkResult), hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(ctx->h_res.p) + 256, d + o_fb, 4, hipMemcpyDeviceToHost, st));
+    if (ulen) HIPCHK(ctx, hipMemcpyAsync(dst, ctx->d_scratch.p, ulen, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    const DevChunkResult* r = static_cast<const DevChunkResult*>(ctx->h_res.p);
+    if (r->status != 0) return fail(ctx, r->status, "snappy: corrupt input");
+    return PF_OK;
+}
+
+// Test hook: which path decoded the last pf_snappy_decompress (1 = serial fallback).
+int pf_snappy_last_fallback(pf_ctx* ctx) {
+    return ctx && ctx->h_res.p ? *reinterpret_cast<const int*>(static_cast<uint8_t*>(ctx->h_res.p) + 256) : -1;
 }
 
 int pf_last_timing(pf_ctx* ctx, float* stage_ms, int n_stages, int* n_written) {

@@ -19,6 +19,9 @@
 //    own stores are ordered before its later loads);
 //  * tokens are parsed in batches into LDS and executed in order; finished output is flushed
 //    ring -> HBM with 16-byte coalesced stores.
+// This serial kernel is the FALLBACK: it only runs for pages the parallel path
+// (pf_snappy_par.hip) flagged — streams whose copies cross 64 KiB block boundaries, or
+// corrupt streams (it produces the precise error status).
 #include <hip/hip_runtime.h>
 
 #include "pf_device.h"
@@ -54,7 +57,9 @@ __device__ __forceinline__ void flush(const uint8_t* ring, uint8_t* dst, uint32_
     for (uint32_t q = tail_start + lane; q < to; q += WAVE) dst[q] = ring[q & RMASK];
 }
 
-__global__ __launch_bounds__(64) void k_snappy(const SnappyJob* __restrict__ jobs, DevChunkResult* res) {
+__global__ __launch_bounds__(64) void k_snappy_serial(const SnappyJob* __restrict__ jobs, const int* __restrict__ fallback,
+                                                      DevChunkResult* res) {
+    if (!fallback[blockIdx.x]) return;   // the parallel path decoded this page
     __shared__ uint8_t ring[RING];
     __shared__ Token toks[TOK_BATCH];
     __shared__ int ntok_s, err_s;
@@ -178,9 +183,11 @@ __global__ __launch_bounds__(64) void k_snappy(const SnappyJob* __restrict__ job
     flush(ring, dst, flushed, op);
 }
 
-void launch_snappy(const SnappyJob* d_jobs, int n_jobs, DevChunkResult* d_res, hipStream_t s) {
-    if (n_jobs <= 0) return;
-    hipLaunchKernelGGL(k_snappy, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_res);
+
+
+void launch_snappy_serial(const SnappyJob* d_jobs, int n_jobs, const int* d_fallback, DevChunkResult* d_res,
+                          hipStream_t s) {
+    if (n_jobs > 0) hipLaunchKernelGGL(k_snappy_serial, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_fallback, d_res);
 }
 
 }  // namespace pf

@@ -94,6 +94,8 @@ def lib():
         "pf_column_info_get": ([vp, i32, C.POINTER(ColumnInfo)], C.c_int),
         "pf_copy_column": ([vp, i32, C.POINTER(ColumnOut)], C.c_int),
         "pf_last_timing": ([vp, C.POINTER(C.c_float), i32, C.POINTER(C.c_int)], C.c_int),
+        "pf_snappy_decompress": ([vp, vp, sz, vp, sz, C.POINTER(C.c_size_t)], C.c_int),
+        "pf_snappy_last_fallback": ([vp], C.c_int),
         "pf_file_open": ([C.c_char_p, C.POINTER(vp)], C.c_int),
         "pf_file_close": ([vp], C.c_int),
         "pf_file_num_row_groups": ([vp, C.POINTER(C.c_int)], C.c_int),

@@ -182,6 +182,18 @@ class GpuDecoder:
         check(lib().pf_column_info_get(self.h, i, C.byref(ci)), self.h, "pf_column_info_get")
         return ci
 
+    def snappy_decompress(self, data: bytes, cap=None):
+        """Raw Snappy buffer -> bytes on the GPU (K1 kernels). Returns (bytes, used_fallback)."""
+        L = lib()
+        src = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, np.uint8)
+        out_len = C.c_size_t()
+        cap = cap if cap is not None else max(1, 64 * len(data) + 64)
+        dst = np.zeros(cap, dtype=np.uint8)
+        rc = L.pf_snappy_decompress(self.h, src.ctypes.data, len(data), dst.ctypes.data, cap, C.byref(out_len))
+        if rc != 0:
+            return rc, None
+        return dst[:out_len.value].tobytes(), L.pf_snappy_last_fallback(self.h)
+
     def timing(self):
         buf = (C.c_float * 8)()
         n = C.c_int()

@@ -44,6 +44,16 @@ class Oracle:
         L.pfo_snappy_uncompress.restype = C.c_int64
         L.pfo_snappy_uncompressed_length.argtypes = [C.c_char_p, C.c_size_t]
         L.pfo_snappy_uncompressed_length.restype = C.c_int64
+        L.pfo_snappy_compress.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int]
+        L.pfo_snappy_compress.restype = C.c_int64
+
+    def snappy_compress(self, data: bytes, mode=0):
+        """Test-vector generator: mode 0 Google-style 64 KiB blocks, mode 1 cross-block copies."""
+        cap = len(data) + len(data) // 6 + 64
+        out = C.create_string_buffer(cap)
+        n = self.lib.pfo_snappy_compress(data, len(data), out, cap, mode)
+        assert n >= 0
+        return out.raw[:n]
 
     def snappy_uncompress(self, data: bytes):
         n = self.lib.pfo_snappy_uncompressed_length(data, len(data))

@@ -1,0 +1,87 @@
+"""K1 (Snappy) on the GPU in isolation: known-answer vectors (pyarrow's Google Snappy), seeded
+multi-block streams from the oracle's test compressor (Google-style 64 KiB blocks -> the
+block-parallel path; cross-block streams -> the serial fallback), and corrupt streams."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dec():
+    from pfloor.decoder import GpuDecoder
+    d = GpuDecoder(0)
+    yield d
+    d.close()
+
+
+def _payloads(rng):
+    words = [b"alpha ", b"beta ", b"gamma ", b"delta ", b"ironic ", b"deposits ", b"packages "]
+    text = b"".join(words[i] for i in rng.integers(0, len(words), 60000))
+    ints = np.cumsum(rng.integers(0, 9, 120000)).astype(np.int64).tobytes()
+    rnd = rng.integers(0, 256, 200000, dtype=np.uint8).tobytes()
+    runs = b"".join(bytes([int(b)]) * int(k) for b, k in zip(rng.integers(0, 4, 4000), rng.integers(1, 300, 4000)))
+    mixed = b"".join((rng.integers(0, 256, int(rng.integers(1, 80)), dtype=np.uint8).tobytes() if rng.random() < 0.3
+                      else words[int(rng.integers(0, 7))] * int(rng.integers(1, 20))) for _ in range(6000))
+    return {"text": text, "ints": ints, "random": rnd, "runs": runs, "mixed": mixed, "tiny": b"ab", "empty": b""}
+
+
+def test_known_answer_vectors(dec, oracle):
+    z = np.load(os.path.join(GOLDEN, "snappy_kat.npz"), allow_pickle=False)
+    for name in sorted({k.rsplit("_", 1)[0] for k in z.files}):
+        raw, comp = z[name + "_raw"].tobytes(), z[name + "_comp"].tobytes()
+        got, fb = dec.snappy_decompress(comp)
+        assert got == raw, name
+        assert fb == 0, f"{name}: Google Snappy stream should take the block-parallel path"
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_block_parallel_path(dec, oracle, seed):
+    rng = np.random.default_rng(seed)
+    for name, data in _payloads(rng).items():
+        comp = oracle.snappy_compress(data, mode=0)
+        got, fb = dec.snappy_decompress(comp)
+        assert got == data, (name, len(data))
+        assert fb == 0, name
+
+
+def test_unaligned_stream_single_piece(dec, oracle):
+    """No token at the 64 KiB marks: the page decodes as one piece (copies may reach far back)."""
+    rng = np.random.default_rng(7)
+    data = _payloads(rng)["text"] * 3
+    got, fb = dec.snappy_decompress(oracle.snappy_compress(data, mode=1))
+    assert got == data and fb == 0
+
+
+def test_cross_block_streams_fall_back(dec, oracle):
+    """Tokens aligned to 64 KiB but copies reaching into earlier blocks: pieces are not
+    independent, so the serial kernel must take over — and still be bit-exact."""
+    rng = np.random.default_rng(7)
+    data = _payloads(rng)["text"] * 3
+    comp = oracle.snappy_compress(data, mode=2)
+    got, fb = dec.snappy_decompress(comp)
+    assert got == data
+    assert fb == 1
+
+
+def test_corrupt_streams_error(dec, oracle):
+    rng = np.random.default_rng(9)
+    data = _payloads(rng)["mixed"]
+    comp = bytearray(oracle.snappy_compress(data, mode=0))
+    for cut in (3, len(comp) // 3, len(comp) - 1):
+        got, _ = dec.snappy_decompress(bytes(comp[:cut]), cap=len(data) + 16)
+        assert isinstance(got, int) and got < 0
+    for _ in range(20):
+        b = bytearray(comp)
+        k = int(rng.integers(4, len(b)))
+        b[k] = int(rng.integers(0, 256))
+        got, _ = dec.snappy_decompress(bytes(b), cap=len(data) + 16)
+        ref = oracle.snappy_uncompress(bytes(b))
+        if isinstance(got, bytes):
+            assert got == ref
+        else:
+            assert ref is None or isinstance(ref, int)
