@@ -29,6 +29,7 @@ struct SnappyJob {
     int32_t chunk;
     uint32_t split_base;  // first entry of this job's 64 KiB split table
     uint32_t n_pieces;    // ceil(dst_len / 65536), >= 1
+    uint32_t* tokmap;     // indexed jobs: bit i = a token starts at input byte i (zeroed per batch)
 };
 
 struct DevPage {

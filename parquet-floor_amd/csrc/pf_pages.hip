@@ -155,16 +155,100 @@ __device__ inline int64_t plain_binary_walk(const uint8_t* p, uint64_t n, int64_
     return total;
 }
 
+// ---- workgroup-parallel PLAIN BYTE_ARRAY walk --------------------------------------------------
+// The <len><bytes> chain is serial, but a 4-byte little-endian length is "plausible" at position q
+// only if q + 4 + len <= n; inside text (or most payloads) only the true prefixes are. Every
+// thread tests 8 positions per 2 KiB tile; plausible positions are emitted in order (block scan)
+// and each must be its predecessor's successor (q_next == q + 4 + len), the first at 0. Any
+// mismatch — a false candidate, overflow, too few candidates — falls back to the exact serial
+// walk, so the result is always the chain parquet-mr's BinaryPlainValuesReader reads.
+constexpr int BW_TILE = NT * 8;          // bytes per tile
+constexpr int BW_CAP = BW_TILE / 4;      // candidates per tile (true prefixes are >= 4 bytes apart)
+
+struct BinWalkLds {
+    uint32_t cand[BW_CAP];
+    uint32_t next[BW_CAP];
+    uint32_t scan[NT / 64];
+    unsigned long long chars;
+    uint32_t found, carry, bad;
+};
+
+__device__ inline int64_t binary_walk_wg(const uint8_t* p, uint64_t n, int64_t count, uint32_t* pos, uint32_t* len,
+                                         BinWalkLds& W) {
+    const int tid = threadIdx.x;
+    if (tid == 0) { W.found = 0; W.carry = 0; W.bad = 0; W.chars = 0; }
+    __syncthreads();
+    if (count == 0) return 0;
+    if (n > 0x7fffffffull) return -1;
+    for (uint64_t t0 = 0; t0 < n; t0 += BW_TILE) {
+        if (W.found >= uint64_t(count) || W.bad) break;
+        const uint64_t b0 = t0 + uint64_t(tid) * 8;
+        uint32_t flags = 0, L[8];
+        #pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint64_t q = b0 + i;
+            L[i] = 0;
+            if (q + 4 <= n) {
+                const uint32_t l = ld32le(p, q, n);
+                if (uint64_t(l) <= n - q - 4) { flags |= 1u << i; L[i] = l; }
+            }
+        }
+        uint32_t tot;
+        uint32_t idx = block_excl_scan<NT>(__popc(flags), W.scan, tot);
+        if (tot > BW_CAP) { if (tid == 0) W.bad = 1; __syncthreads(); break; }
+        const uint32_t base = W.found;
+        uint64_t my_chars = 0;
+        #pragma unroll
+        for (int i = 0; i < 8; i++) {
+            if ((flags >> i) & 1u) {
+                const uint32_t q = uint32_t(b0 + i);
+                W.cand[idx] = q;
+                W.next[idx] = q + 4 + L[i];
+                const uint64_t k = uint64_t(base) + idx;
+                if (k < uint64_t(count)) {
+                    pos[k] = q + 4;
+                    if (len) len[k] = L[i];
+                    my_chars += L[i];
+                }
+                idx++;
+            }
+        }
+        __syncthreads();
+        // chain check: candidate i's successor is candidate i+1 (across tiles via `carry`)
+        int bad = 0;
+        for (uint32_t i = tid; i < tot; i += NT) {
+            const uint64_t k = uint64_t(base) + i;
+            if (k >= uint64_t(count)) continue;
+            const uint32_t expect = i == 0 ? (base == 0 ? 0u : W.carry) : W.next[i - 1];
+            bad |= W.cand[i] != expect;
+        }
+        if (my_chars) atomicAdd(&W.chars, (unsigned long long)my_chars);
+        bad = __syncthreads_or(bad);
+        if (tid == 0) {
+            if (bad) W.bad = 1;
+            if (tot) W.carry = W.next[tot - 1];
+            W.found = base + tot;
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    if (!W.bad && W.found >= uint64_t(count)) return int64_t(W.chars);
+    // exact serial fallback (false candidates in binary payloads, or corrupt pages)
+    __shared__ long long s_res;
+    if (tid == 0) s_res = plain_binary_walk(p, n, count, pos, len);
+    __syncthreads();
+    return s_res;
+}
+
 // ---- k_dict_binary --------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_dict_binary(DevChunk* chunks, const DevPage* pages, const int* dict_chunks,
+__global__ __launch_bounds__(NT) void k_dict_binary(DevChunk* chunks, const DevPage* pages, const int* dict_chunks,
                                                     DevChunkResult* res) {
+    __shared__ BinWalkLds W;
     const int c = dict_chunks[blockIdx.x];
     DevChunk& ck = chunks[c];
     const DevPage& pg = pages[ck.dict_page];
-    if (threadIdx.x == 0) {
-        int64_t t = plain_binary_walk(pg.body, pg.body_len, ck.dict_n, ck.dict_pos, ck.dict_len);
-        if (t < 0) set_status(res, c, ST_CORRUPT, ck.dict_page);
-    }
+    const int64_t t = binary_walk_wg(pg.body, pg.body_len, ck.dict_n, ck.dict_pos, ck.dict_len, W);
+    if (t < 0 && threadIdx.x == 0) set_status(res, c, ST_CORRUPT, ck.dict_page);
 }
 
 // ---- values helpers ------------------------------------------------------------------------
@@ -180,6 +264,7 @@ __global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunk
     __shared__ RleState sval;
     __shared__ int npval, verr;
     __shared__ unsigned long long chars_acc;
+    __shared__ BinWalkLds W;
 
     const int pi = page_list[blockIdx.x];
     DevPage& pg = pages[pi];
@@ -243,16 +328,17 @@ __global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunk
     }
     if (L.err || verr) { if (threadIdx.x == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
     if (binary && !dict) {
-        if (threadIdx.x == 0) {
-            if (pg.encoding != 0) { set_status(res, pg.chunk, ST_ENCODING, pi); verr = 1; }
-            else {
-                int64_t tot = plain_binary_walk(s.val, s.val_n, int64_t(vals), pg.aux, nullptr);
-                if (tot < 0) { set_status(res, pg.chunk, ST_CORRUPT, pi); verr = 1; }
-                else chars_acc = uint64_t(tot);
-            }
+        if (pg.encoding != 0) {
+            if (threadIdx.x == 0) set_status(res, pg.chunk, ST_ENCODING, pi);
+            return;
         }
+        const int64_t tot = binary_walk_wg(s.val, s.val_n, int64_t(vals), pg.aux, nullptr, W);
+        if (tot < 0) {
+            if (threadIdx.x == 0) set_status(res, pg.chunk, ST_CORRUPT, pi);
+            return;
+        }
+        if (threadIdx.x == 0) chars_acc = uint64_t(tot);
         __syncthreads();
-        if (verr) return;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -565,7 +651,7 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
 // ---- launchers -------------------------------------------------------------------------------
 void launch_dict_binary(DevChunk* d_chunks, const DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                         hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_dict_binary, dim3(n), dim3(64), 0, st, d_chunks, d_pages, d_list, d_res);
+    if (n > 0) hipLaunchKernelGGL(k_dict_binary, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res);
 }
 void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                   hipStream_t st) {

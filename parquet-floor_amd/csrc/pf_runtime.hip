@@ -79,7 +79,8 @@ struct pf_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev[N_EVENTS] = {};
     std::string err;
-    DevBuf d_in, d_scratch, d_out, d_bits, d_chars, d_meta;
+    DevBuf d_in, d_scratch, d_out, d_bits, d_chars, d_meta, d_tokmap;
+    size_t tokmap_bytes = 0;
     HostBuf h_meta, h_res;
     // last batch
     int n_chunks = 0;
@@ -150,6 +151,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     const int* d_index = reinterpret_cast<const int*>(meta + ctx->off_index);
 
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
+    if (ctx->tokmap_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_tokmap.p, 0, ctx->tokmap_bytes, st));
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
     launch_snappy_index(d_jobs, d_index, int(ctx->l_index.size()), d_splits, d_fallback, st);
     launch_snappy_exec(d_jobs, d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, st);
@@ -241,7 +243,8 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     if (!ctx) return PF_OK;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (DevBuf* b : {&ctx->d_in, &ctx->d_scratch, &ctx->d_out, &ctx->d_bits, &ctx->d_chars, &ctx->d_meta}) b->release();
+    for (DevBuf* b : {&ctx->d_in, &ctx->d_scratch, &ctx->d_out, &ctx->d_bits, &ctx->d_chars, &ctx->d_meta, &ctx->d_tokmap})
+        b->release();
     ctx->h_meta.release();
     ctx->h_res.release();
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
@@ -471,14 +474,26 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         if (ck.needs_count) ctx->l_count.push_back(int(i));
         ctx->l_decode.push_back(int(i));
     }
-    // ---- Snappy split tables: one piece per 64 KiB of output; index pages larger than that ----
+    // ---- Snappy split tables: one piece per 64 KiB of output; index pages larger than that
+    //      (the index also publishes a token-start bitmap, one bit per input byte) ----
+    size_t tok_words = 0;
+    for (const SnappyJob& jb : ctx->jobs)
+        if (jb.dst_len > 65536u) tok_words += jb.src_len / 32u + 2u;
+    ctx->tokmap_bytes = tok_words * 4;
+    if (tok_words) HIPCHK(ctx, ctx->d_tokmap.ensure(ctx->tokmap_bytes));
+    tok_words = 0;
     for (size_t j = 0; j < ctx->jobs.size(); j++) {
         SnappyJob& jb = ctx->jobs[j];
         uint32_t np = std::max<uint32_t>(1u, (jb.dst_len + 65535u) / 65536u);
         jb.split_base = ctx->n_splits;
         jb.n_pieces = np;
+        jb.tokmap = nullptr;
         ctx->n_splits += np;
-        if (np > 1) ctx->l_index.push_back(int(j));
+        if (np > 1) {
+            ctx->l_index.push_back(int(j));
+            jb.tokmap = static_cast<uint32_t*>(ctx->d_tokmap.p) + tok_words;
+            tok_words += jb.src_len / 32u + 2u;
+        }
         for (uint32_t k = 0; k < np; k++) ctx->pieces.push_back(int2{int(j), int(k)});
     }
     // ---- metadata upload ----
@@ -627,6 +642,13 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     job.src_len = uint32_t(n);
     job.dst_len = uint32_t(ulen);
     job.n_pieces = std::max<uint32_t>(1u, uint32_t((ulen + 65535) / 65536));
+    job.tokmap = nullptr;
+    if (job.n_pieces > 1) {
+        ctx->tokmap_bytes = 4 * (n / 32 + 2);
+        HIPCHK(ctx, ctx->d_tokmap.ensure(ctx->tokmap_bytes));
+        HIPCHK(ctx, hipMemsetAsync(ctx->d_tokmap.p, 0, ctx->tokmap_bytes, st));
+        job.tokmap = static_cast<uint32_t*>(ctx->d_tokmap.p);
+    }
     std::vector<int2> pieces;
     for (uint32_t k = 0; k < job.n_pieces; k++) pieces.push_back(int2{0, int(k)});
     size_t m = 0;

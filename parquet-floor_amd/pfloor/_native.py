@@ -7,7 +7,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpfloor.so")
+# PFLOOR_LIB_PATH: diagnostics only (e.g. the stamp build from `make stamps`).
+LIB_PATH = os.environ.get("PFLOOR_LIB_PATH") or os.path.join(_HERE, "libpfloor.so")
 
 PF_OK = 0
 STATUS = {0: "PF_OK", -1: "PF_ERR_INVALID_ARG", -2: "PF_ERR_CORRUPT_PAGE", -3: "PF_ERR_UNSUPPORTED_ENCODING",
