@@ -29,7 +29,9 @@ struct SnappyJob {
     int32_t chunk;
     uint32_t split_base;  // first entry of this job's 64 KiB split table
     uint32_t n_pieces;    // ceil(dst_len / 65536), >= 1
-    uint32_t* tokmap;     // indexed jobs: bit i = a token starts at input byte i (zeroed per batch)
+    uint32_t* tokmap;     // bit i = a token starts at input byte i (n_win * 256 words, index pass)
+    uint32_t win_base;    // first entry of this job's 8 KiB index windows (SnapWin / lane outs)
+    uint32_t n_win;       // ceil(src_len / 8192), >= 1
 };
 
 struct DevPage {

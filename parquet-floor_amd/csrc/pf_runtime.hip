@@ -17,14 +17,13 @@
 #include <string>
 #include <vector>
 
-#include "pf_device.h"
 #include "pf_host.h"
+#include "pf_snappy_par.h"
 #include "pfloor.h"
 
 namespace pf {
-void launch_snappy_index(const SnappyJob*, const int*, int, uint32_t*, int*, hipStream_t);
-void launch_snappy_exec(const SnappyJob*, const int2*, int, const uint32_t*, int*, hipStream_t);
-void launch_snappy_serial(const SnappyJob*, int, const int*, DevChunkResult*, hipStream_t);
+void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, uint32_t*, const int2*, int, uint32_t*, int*,
+                   DevChunkResult*, hipStream_t);
 void launch_dict_binary(DevChunk*, const DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
@@ -80,7 +79,6 @@ struct pf_ctx {
     hipEvent_t ev[N_EVENTS] = {};
     std::string err;
     DevBuf d_in, d_scratch, d_out, d_bits, d_chars, d_meta, d_tokmap;
-    size_t tokmap_bytes = 0;
     HostBuf h_meta, h_res;
     // last batch
     int n_chunks = 0;
@@ -89,14 +87,17 @@ struct pf_ctx {
     std::vector<DevChunk> chunks;          // host copies (device pointers)
     std::vector<DevPage> pages;
     std::vector<SnappyJob> jobs;
-    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_decode, l_index;
-    std::vector<int2> pieces;
+    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_decode;
+    std::vector<int2> wins, pieces;       // Snappy index windows / 64 KiB pieces (job, index)
     uint32_t n_splits = 0;
+    SnapWin* d_win = nullptr;              // in d_tokmap: bitmap | lane outs | windows
+    const uint32_t* d_last_splits = nullptr;   // diagnostics: last pf_snappy_decompress tables
+    uint32_t* d_lane_out = nullptr;
     std::vector<int64_t> host_status;      // per chunk host-side planning errors
     std::vector<pf_column_info> info;
     size_t bits_bytes = 0;
     size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
-    size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_index = 0;
+    size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0;
     uint64_t chars_need = 0;
     const uint8_t* d_bytes = nullptr;
     int reruns = 0;
@@ -148,14 +149,12 @@ int enqueue_kernels(pf_ctx* ctx) {
     const int2* d_pieces = reinterpret_cast<const int2*>(meta + ctx->off_pieces);
     uint32_t* d_splits = reinterpret_cast<uint32_t*>(meta + ctx->off_splits);
     int* d_fallback = reinterpret_cast<int*>(meta + ctx->off_fallback);
-    const int* d_index = reinterpret_cast<const int*>(meta + ctx->off_index);
+    const int2* d_wins = reinterpret_cast<const int2*>(meta + ctx->off_wins);
 
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
-    if (ctx->tokmap_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_tokmap.p, 0, ctx->tokmap_bytes, st));
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
-    launch_snappy_index(d_jobs, d_index, int(ctx->l_index.size()), d_splits, d_fallback, st);
-    launch_snappy_exec(d_jobs, d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, st);
-    launch_snappy_serial(d_jobs, int(ctx->jobs.size()), d_fallback, d_res, st);
+    launch_snappy(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_lane_out, d_pieces,
+                  int(ctx->pieces.size()), d_splits, d_fallback, d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
     launch_dict_binary(d_chunks, d_pages, d_dictbin, int(ctx->l_dictbin.size()), d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], st));
@@ -177,6 +176,34 @@ int enqueue_kernels(pf_ctx* ctx) {
     return PF_OK;
 }
 
+// Snappy tables of the batch's jobs: 8 KiB index windows and 64 KiB pieces. d_tokmap holds, per
+// window, 1 KiB of token-start bitmap, then 64 lane output counts, then the SnapWin records;
+// the index pass writes every word, so nothing needs clearing.
+int plan_snappy(pf_ctx* ctx) {
+    ctx->wins.clear();
+    ctx->pieces.clear();
+    ctx->n_splits = 0;
+    uint32_t n_win = 0;
+    for (size_t j = 0; j < ctx->jobs.size(); j++) {
+        SnappyJob& jb = ctx->jobs[j];
+        jb.n_win = std::max<uint32_t>(1u, uint32_t((uint64_t(jb.src_len) + SNAP_WIN - 1) / SNAP_WIN));
+        jb.win_base = n_win;
+        for (uint32_t w = 0; w < jb.n_win; w++) ctx->wins.push_back(int2{int(j), int(w)});
+        n_win += jb.n_win;
+        jb.n_pieces = std::max<uint32_t>(1u, uint32_t((uint64_t(jb.dst_len) + SNAP_BLOCK - 1) / SNAP_BLOCK));
+        jb.split_base = ctx->n_splits;
+        ctx->n_splits += jb.n_pieces;
+        for (uint32_t k = 0; k < jb.n_pieces; k++) ctx->pieces.push_back(int2{int(j), int(k)});
+    }
+    const size_t tok_bytes = size_t(n_win) * SNAP_WWORDS * 4, lo_bytes = size_t(n_win) * 64 * 4;
+    HIPCHK(ctx, ctx->d_tokmap.ensure(tok_bytes + lo_bytes + size_t(n_win) * sizeof(SnapWin) + 256));
+    uint8_t* base = static_cast<uint8_t*>(ctx->d_tokmap.p);
+    ctx->d_lane_out = reinterpret_cast<uint32_t*>(base + tok_bytes);
+    ctx->d_win = reinterpret_cast<SnapWin*>(base + tok_bytes + lo_bytes);
+    for (SnappyJob& jb : ctx->jobs) jb.tokmap = reinterpret_cast<uint32_t*>(base) + size_t(jb.win_base) * SNAP_WWORDS;
+    return PF_OK;
+}
+
 // Upload metadata tables (results zeroed, arena counter zeroed).
 int upload_meta(pf_ctx* ctx) {
     uint8_t* h = static_cast<uint8_t*>(ctx->h_meta.p);
@@ -186,7 +213,7 @@ int upload_meta(pf_ctx* ctx) {
     std::memcpy(h + ctx->off_jobs, ctx->jobs.data(), sizeof(SnappyJob) * ctx->jobs.size());
     std::memcpy(h + ctx->off_pieces, ctx->pieces.data(), sizeof(int2) * ctx->pieces.size());
     std::memset(h + ctx->off_splits, 0xff, sizeof(uint32_t) * ctx->n_splits);
-    std::memcpy(h + ctx->off_index, ctx->l_index.data(), sizeof(int) * ctx->l_index.size());
+    std::memcpy(h + ctx->off_wins, ctx->wins.data(), sizeof(int2) * ctx->wins.size());
     int* lists = reinterpret_cast<int*>(h + ctx->off_lists);
     size_t lo = 0;
     for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_decode}) {
@@ -294,7 +321,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->chunks.assign(n_chunks, DevChunk{});
     ctx->pages.clear(); ctx->jobs.clear();
     ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_decode.clear();
-    ctx->l_index.clear(); ctx->pieces.clear(); ctx->n_splits = 0;
+    ctx->wins.clear(); ctx->pieces.clear(); ctx->n_splits = 0;
     ctx->host_status.assign(n_chunks, 0);
     ctx->info.assign(n_chunks, pf_column_info{});
     ctx->reruns = 0;
@@ -474,27 +501,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         if (ck.needs_count) ctx->l_count.push_back(int(i));
         ctx->l_decode.push_back(int(i));
     }
-    // ---- Snappy split tables: one piece per 64 KiB of output; index pages larger than that
-    //      (the index also publishes a token-start bitmap, one bit per input byte) ----
-    size_t tok_words = 0;
-    for (const SnappyJob& jb : ctx->jobs)
-        if (jb.dst_len > 65536u) tok_words += jb.src_len / 32u + 2u;
-    ctx->tokmap_bytes = tok_words * 4;
-    if (tok_words) HIPCHK(ctx, ctx->d_tokmap.ensure(ctx->tokmap_bytes));
-    tok_words = 0;
-    for (size_t j = 0; j < ctx->jobs.size(); j++) {
-        SnappyJob& jb = ctx->jobs[j];
-        uint32_t np = std::max<uint32_t>(1u, (jb.dst_len + 65535u) / 65536u);
-        jb.split_base = ctx->n_splits;
-        jb.n_pieces = np;
-        jb.tokmap = nullptr;
-        ctx->n_splits += np;
-        if (np > 1) {
-            ctx->l_index.push_back(int(j));
-            jb.tokmap = static_cast<uint32_t*>(ctx->d_tokmap.p) + tok_words;
-            tok_words += jb.src_len / 32u + 2u;
-        }
-        for (uint32_t k = 0; k < np; k++) ctx->pieces.push_back(int2{int(j), int(k)});
+    // ---- Snappy tables: 8 KiB index windows, 64 KiB pieces ----
+    {
+        int rc = plan_snappy(ctx);
+        if (rc) return rc;
     }
     // ---- metadata upload ----
     size_t m = 0;
@@ -507,7 +517,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_pieces = take(m, sizeof(int2) * ctx->pieces.size());
     ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);
     ctx->off_fallback = take(m, sizeof(int) * ctx->jobs.size());
-    ctx->off_index = take(m, sizeof(int) * ctx->l_index.size());
+    ctx->off_wins = take(m, sizeof(int2) * ctx->wins.size());
     m = take(m, 256) + 256;   // arena counter lives in the last 256 bytes
     ctx->meta_bytes = m;
     HIPCHK(ctx, ctx->d_meta.ensure(m));
@@ -641,38 +651,32 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     job.dst = static_cast<uint8_t*>(ctx->d_scratch.p);
     job.src_len = uint32_t(n);
     job.dst_len = uint32_t(ulen);
-    job.n_pieces = std::max<uint32_t>(1u, uint32_t((ulen + 65535) / 65536));
-    job.tokmap = nullptr;
-    if (job.n_pieces > 1) {
-        ctx->tokmap_bytes = 4 * (n / 32 + 2);
-        HIPCHK(ctx, ctx->d_tokmap.ensure(ctx->tokmap_bytes));
-        HIPCHK(ctx, hipMemsetAsync(ctx->d_tokmap.p, 0, ctx->tokmap_bytes, st));
-        job.tokmap = static_cast<uint32_t*>(ctx->d_tokmap.p);
-    }
-    std::vector<int2> pieces;
-    for (uint32_t k = 0; k < job.n_pieces; k++) pieces.push_back(int2{0, int(k)});
+    ctx->jobs.assign(1, job);
+    ctx->chunks.clear();
+    ctx->pages.clear();
+    int rc = plan_snappy(ctx);
+    if (rc) return rc;
     size_t m = 0;
     auto take = [](size_t& cursor, size_t sz) { size_t o = align_up(cursor, 256); cursor = o + sz; return o; };
-    size_t o_job = take(m, sizeof(SnappyJob)), o_pc = take(m, sizeof(int2) * pieces.size());
-    size_t o_sp = take(m, 4 * pieces.size()), o_fb = take(m, 4), o_ix = take(m, 4), o_res = take(m, sizeof(DevChunkResult));
+    size_t o_job = take(m, sizeof(SnappyJob)), o_pc = take(m, sizeof(int2) * ctx->pieces.size());
+    size_t o_sp = take(m, 4 * ctx->pieces.size()), o_fb = take(m, 4), o_wn = take(m, sizeof(int2) * ctx->wins.size());
+    size_t o_res = take(m, sizeof(DevChunkResult));
     m = align_up(m, 256);
     HIPCHK(ctx, ctx->d_meta.ensure(m));
     HIPCHK(ctx, ctx->h_meta.ensure(m));
     uint8_t* h = static_cast<uint8_t*>(ctx->h_meta.p);
     std::memset(h, 0, m);
-    std::memcpy(h + o_job, &job, sizeof job);
-    std::memcpy(h + o_pc, pieces.data(), sizeof(int2) * pieces.size());
-    std::memset(h + o_sp, 0xff, 4 * pieces.size());
-    int zero = 0;
-    std::memcpy(h + o_ix, &zero, 4);
+    std::memcpy(h + o_job, ctx->jobs.data(), sizeof(SnappyJob));
+    std::memcpy(h + o_pc, ctx->pieces.data(), sizeof(int2) * ctx->pieces.size());
+    std::memset(h + o_sp, 0xff, 4 * ctx->pieces.size());
+    std::memcpy(h + o_wn, ctx->wins.data(), sizeof(int2) * ctx->wins.size());
     uint8_t* d = static_cast<uint8_t*>(ctx->d_meta.p);
     HIPCHK(ctx, hipMemcpyAsync(d, h, m, hipMemcpyHostToDevice, st));
-    const SnappyJob* dj = reinterpret_cast<const SnappyJob*>(d + o_job);
-    launch_snappy_index(dj, reinterpret_cast<const int*>(d + o_ix), job.n_pieces > 1 ? 1 : 0,
-                        reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb), st);
-    launch_snappy_exec(dj, reinterpret_cast<const int2*>(d + o_pc), int(pieces.size()),
-                       reinterpret_cast<const uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb), st);
-    launch_snappy_serial(dj, 1, reinterpret_cast<const int*>(d + o_fb), reinterpret_cast<DevChunkResult*>(d + o_res), st);
+    ctx->d_last_splits = reinterpret_cast<const uint32_t*>(d + o_sp);
+    launch_snappy(reinterpret_cast<const SnappyJob*>(d + o_job), 1, reinterpret_cast<const int2*>(d + o_wn),
+                  int(ctx->wins.size()), ctx->d_win, ctx->d_lane_out, reinterpret_cast<const int2*>(d + o_pc),
+                  int(ctx->pieces.size()), reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb),
+                  reinterpret_cast<DevChunkResult*>(d + o_res), st);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, ctx->h_res.ensure(512));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_res.p, d + o_res, sizeof(DevChunkResult), hipMemcpyDeviceToHost, st));
@@ -687,6 +691,18 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
 // Test hook: which path decoded the last pf_snappy_decompress (1 = serial fallback).
 int pf_snappy_last_fallback(pf_ctx* ctx) {
     return ctx && ctx->h_res.p ? *reinterpret_cast<const int*>(static_cast<uint8_t*>(ctx->h_res.p) + 256) : -1;
+}
+
+// Diagnostics (not part of pfloor.h): the index tables of the last pf_snappy_decompress.
+int pf_debug_snappy_tables(pf_ctx* ctx, uint32_t* splits, int n_splits, uint32_t* wins, int n_wins, uint32_t* lane_out,
+                           uint32_t* tokmap) {
+    if (!ctx || !ctx->d_last_splits) return fail(ctx, PF_ERR_STATE, "no snappy tables");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (splits) HIPCHK(ctx, hipMemcpy(splits, ctx->d_last_splits, 4 * size_t(n_splits), hipMemcpyDeviceToHost));
+    if (wins) HIPCHK(ctx, hipMemcpy(wins, ctx->d_win, sizeof(SnapWin) * size_t(n_wins), hipMemcpyDeviceToHost));
+    if (lane_out) HIPCHK(ctx, hipMemcpy(lane_out, ctx->d_lane_out, 256 * size_t(n_wins), hipMemcpyDeviceToHost));
+    if (tokmap) HIPCHK(ctx, hipMemcpy(tokmap, ctx->d_tokmap.p, 1024 * size_t(n_wins), hipMemcpyDeviceToHost));
+    return PF_OK;
 }
 
 int pf_last_timing(pf_ctx* ctx, float* stage_ms, int n_stages, int* n_written) {

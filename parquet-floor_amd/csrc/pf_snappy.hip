@@ -19,12 +19,11 @@
 //    own stores are ordered before its later loads);
 //  * tokens are parsed in batches into LDS and executed in order; finished output is flushed
 //    ring -> HBM with 16-byte coalesced stores.
-// This serial kernel is the FALLBACK: it only runs for pages the parallel path
-// (pf_snappy_par.hip) flagged — streams whose copies cross 64 KiB block boundaries, or
-// corrupt streams (it produces the precise error status).
+// This serial kernel is the FALLBACK: it only runs for pages the block-parallel path
+// (pf_snappy_par.hip) could not index (corrupt streams — it produces the precise error status).
 #include <hip/hip_runtime.h>
 
-#include "pf_device.h"
+#include "pf_snappy_par.h"
 
 namespace pf {
 
@@ -59,7 +58,7 @@ __device__ __forceinline__ void flush(const uint8_t* ring, uint8_t* dst, uint32_
 
 __global__ __launch_bounds__(64) void k_snappy_serial(const SnappyJob* __restrict__ jobs, const int* __restrict__ fallback,
                                                       DevChunkResult* res) {
-    if (!fallback[blockIdx.x]) return;   // the parallel path decoded this page
+    if (fallback[blockIdx.x] != FB_SERIAL) return;   // the block-parallel path decoded this page
     __shared__ uint8_t ring[RING];
     __shared__ Token toks[TOK_BATCH];
     __shared__ int ntok_s, err_s;

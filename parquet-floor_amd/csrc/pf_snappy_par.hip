@@ -1,371 +1,632 @@
-// pf_snappy_par.hip — K1 (parallel path): Snappy page decompression split into independent
-// 64 KiB blocks.
+// pf_snappy_par.hip — K1: block-parallel Snappy page decompression.
 //
-// Google Snappy (what snappy-java wraps) compresses its input in independent 64 KiB blocks:
-// no copy reaches back across a block boundary, and a token starts exactly at every multiple of
-// 65536 in the output. Decoding therefore runs as:
-//   k_snappy_index : one wave per page larger than 64 KiB; wave-parallel speculative parse
-//                    (pf_snappy_par.h) of the token stream that records, for each multiple of
-//                    65536, the input position of the token starting there;
-//   k_snappy_exec  : one 256-thread workgroup per 64 KiB piece. Per window (<= 2 KiB of input,
-//                    <= 8 KiB of output): wave 0 parses and emits token records; all threads
-//                    give every output byte a source pointer (an input byte, or an earlier output
-//                    byte: position - offset, taken modulo the offset inside overlapping copies);
-//                    pointer jumping through the window's pointers resolves copy-of-copy chains
-//                    in log(depth) rounds; finally every byte is gathered from its root (the
-//                    staged input, or already-final HBM output) and stored. Literals longer than
-//                    1 KiB end a window and are copied straight to HBM;
-//   k_snappy_serial: (pf_snappy.hip) re-decodes, serially, any page whose stream breaks the
-//                    block assumption or looks corrupt — so arbitrary valid Snappy streams still
-//                    decode bit-exactly and corrupt ones get the precise error.
 // Replaces snappy-java's Snappy.uncompress behind the Hadoop codec shim
 // (src/main/java/org/apache/hadoop/io/compress/DecompressorStream.java:61-70,101-173).
+//
+// Google Snappy (what snappy-java wraps) compresses in independent 64 KiB blocks: no copy reaches
+// back across a block boundary and a token starts exactly at every multiple of 65536 of the output.
+// A page therefore splits into 64 KiB pieces that decode independently, once the token chain is
+// known. Four kernels:
+//
+//   k_snappy_index  one wave per 8 KiB window of compressed input (all pages). Each lane walks the
+//                   token chain of its 128-byte region from the region start (a guess: the true
+//                   chain usually enters a little later). A scalar pass then follows the chain
+//                   lane to lane from the window entry; a lane whose true entry is not on its
+//                   guessed chain re-walks from it, until the chain is consistent (each round
+//                   fixes at least the first wrong lane). Output: the token-start bitmap (1 bit per
+//                   input byte), per-lane output byte counts, the window exit.
+//   k_snappy_fix    one wave per page. Window w's true entry is window w-1's exit; every window
+//                   walks the true chain from there until it meets its own (guessed) chain —
+//                   usually within a few tokens — and patches the bitmap; windows where they never
+//                   meet are re-parsed. Iterates until no exit changes, checks the totals, then
+//                   finds the input position of the token at each 64 KiB output boundary.
+//   k_snappy_exec   one wave per 64 KiB piece: tokens come from the bitmap 1 KiB of input at a
+//                   time (parsed 64 at a time, one per lane), then execute in order — each token
+//                   is one 64-lane read-then-write step in an 8 KiB LDS ring (copies with larger
+//                   offsets read the already-flushed HBM output); full 2 KiB ring slots are
+//                   flushed with 16-byte stores.
+//   k_snappy_serial (pf_snappy.hip) any page whose stream breaks the block structure or is
+//                   corrupt is re-decoded serially — results never depend on the assumption.
 #include <hip/hip_runtime.h>
-
-// Diagnostic build only (make stamps): per-phase s_memtime cycle sums, never in the product .so.
-#ifdef PF_STAMPS
-__device__ unsigned long long pf_stamps[16];
-#define PF_STAMPS_COUNT pf_stamps
-#endif
 
 #include "pf_snappy_par.h"
 
 namespace pf {
 
 #ifdef PF_STAMPS
-#define STAMP_DECL unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
-#define STAMP(i)                                                                   \
-    do {                                                                           \
-        unsigned long long t_ = __builtin_amdgcn_s_memtime();                      \
-        if (threadIdx.x == 0) atomicAdd(&pf_stamps[i], t_ - t_prev_);              \
-        t_prev_ = t_;                                                              \
-    } while (0)
+__device__ unsigned long long pf_stamps[16];
+#define STAMP_ADD(i, v) atomicAdd(&pf_stamps[i], (unsigned long long)(v))
 #else
-#define STAMP_DECL
-#define STAMP(i)
+#define STAMP_ADD(i, v) ((void)0)
 #endif
 
-constexpr uint32_t BLOCK = 65536;
-constexpr int XNT = 256;                     // threads of the executor workgroup
-constexpr uint32_t WOUT = 8192;              // output bytes (pointer slots) per window
-constexpr int PER_T = int(WOUT) / XNT;       // pointer slots per thread (strided by XNT)
-constexpr uint32_t BIGLIT = 1024;            // longer literals end a window, copied straight to HBM
-constexpr uint32_t LPIECE = 64;              // literal records are split into <= 64-byte pieces
-constexpr int REC_CAP = 64 * 16 + int(WOUT / LPIECE) + 64;
-constexpr uint32_t INPUT = 0x80000000u;      // pointer tag: input byte position
+// ======================================================================== index pass
 
-struct SnapRec {
-    uint32_t out;     // output position (page-absolute)
-    uint32_t src;     // literal: input position; copy: offset
-    uint32_t len;     // bit 31: literal
+struct WinLane {
+    uint32_t b0, b1, b2, b3;   // token starts in the lane's region (bit i = input byte rs + i)
+    uint32_t out;              // output bytes of those tokens
+    uint32_t x;                // chain exit (first position >= region end), SNAP_INVALID past the stream
+    uint32_t c;                // chain start
 };
 
-__device__ __forceinline__ bool preamble(const uint8_t* in, uint64_t n, uint64_t& pos, uint64_t& ulen) {
-    pos = 0;
-    return uvarint(in, n, pos, ulen);
+__device__ __forceinline__ void bit_set(WinLane& L, uint32_t i) {
+    const uint32_t m = 1u << (i & 31u), w = i >> 5;
+    L.b0 |= w == 0 ? m : 0u;
+    L.b1 |= w == 1 ? m : 0u;
+    L.b2 |= w == 2 ? m : 0u;
+    L.b3 |= w == 3 ? m : 0u;
+}
+__device__ __forceinline__ void bit_clr(WinLane& L, uint32_t i) {
+    const uint32_t m = 1u << (i & 31u), w = i >> 5;
+    L.b0 &= w == 0 ? ~m : ~0u;
+    L.b1 &= w == 1 ? ~m : ~0u;
+    L.b2 &= w == 2 ? ~m : ~0u;
+    L.b3 &= w == 3 ? ~m : ~0u;
+}
+__device__ __forceinline__ bool bit_get(const WinLane& L, uint32_t i) {
+    const uint32_t w = i >> 5;
+    const uint32_t v = w == 0 ? L.b0 : (w == 1 ? L.b1 : (w == 2 ? L.b2 : L.b3));
+    return (v >> (i & 31u)) & 1u;
 }
 
-__device__ __forceinline__ uint32_t sbyte(const SnapSeg& S, int b) { return (S.w[b >> 2] >> (8 * (b & 3))) & 0xffu; }
-
-// Exact output length of the token at segment position b (static b), from registers.
-__device__ __forceinline__ uint32_t seg_outlen(const SnapSeg& S, int b) {
-    if (pk(S.tl, b) != 255u) return pk(S.ol, b);
-    const uint32_t nb = (sbyte(S, b) >> 2) - 59u;
-    uint32_t v = sbyte(S, b + 1);
-    if (nb > 1) v |= sbyte(S, b + 2) << 8;
-    if (nb > 2) v |= sbyte(S, b + 3) << 16;
-    if (nb > 3) v |= sbyte(S, b + 4) << 24;
-    return v + 1u;
+// Walk the chain from c while positions stay below re (bits relative to rs).
+__device__ void lane_walk(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t rs, uint32_t re,
+                          uint32_t c, WinLane& L) {
+    L.b0 = L.b1 = L.b2 = L.b3 = 0;
+    L.out = 0;
+    L.c = c;
+    uint64_t p = c;
+    bool bad = false;
+    while (p < re) {
+        const SnapTok t = snap_tok(lds_read8(stage, woff + uint32_t(p - W0)));
+        bit_set(L, uint32_t(p) - rs);
+        const uint32_t o = L.out + t.ol;
+        L.out = o < L.out ? 0xffffffffu : o;
+        p += t.tl;
+        if (p > n) { bad = true; break; }
+    }
+    L.x = bad ? SNAP_INVALID : uint32_t(p);
 }
 
-// ---------------------------------------------------------------- k_snappy_index
-__global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict__ jobs, const int* __restrict__ list,
-                                                     uint32_t* splits, int* fallback) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[SNAP_STAGE];
-    const int j = list[blockIdx.x];
-    const SnappyJob job = jobs[j];
+// Parse one window whose chain enters at `entry` (W0 <= entry < min(W0 + SNAP_WIN, n)). All 64
+// lanes. Returns the window exit; flags = WIN_BROKEN if the chain runs past the stream end.
+__device__ uint32_t win_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t entry, WinLane& L,
+                              uint32_t& flags) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t rs = W0 + uint32_t(lane) * SNAP_RB;
+    const uint32_t re = uint32_t(min(uint64_t(rs) + SNAP_RB, n));
+    const int L0 = int((entry - W0) / SNAP_RB);
+    L.b0 = L.b1 = L.b2 = L.b3 = 0;
+    L.out = 0;
+    L.c = rs;
+    L.x = SNAP_INVALID;
+    if (lane >= L0 && uint64_t(rs) < n) lane_walk(stage, woff, W0, n, rs, re, lane == L0 ? entry : rs, L);
+    uint32_t ent = SNAP_INVALID, X = SNAP_INVALID;
+    bool converged = false;
+    flags = 0;
+    for (int round = 0; round <= 64; round++) {
+        // follow the chain lane to lane (uniform scalar loop)
+        ent = SNAP_INVALID;
+        flags = 0;
+        int k = L0;
+        uint32_t e = entry;
+        for (;;) {
+            if (lane == k) ent = e;
+            const uint32_t x = __builtin_amdgcn_readlane(L.x, k);
+            if (x == SNAP_INVALID) { flags = WIN_BROKEN; X = SNAP_INVALID; break; }
+            if (uint64_t(x) >= n || x >= W0 + SNAP_WIN) { X = x; break; }
+            k = int((x - W0) / SNAP_RB);
+            e = x;
+        }
+        const bool need = ent != SNAP_INVALID && ent != L.c && !(ent > L.c && bit_get(L, ent - rs));
+        if (!__any(need)) { converged = true; break; }
+        if (need) lane_walk(stage, woff, W0, n, rs, re, ent, L);
+    }
+    if (!converged) flags = WIN_BROKEN;
+    // lanes off the chain hold no tokens; drop the guessed prefix before a lane's true entry
+    if (ent == SNAP_INVALID) {
+        L.b0 = L.b1 = L.b2 = L.b3 = 0;
+        L.out = 0;
+    } else if (ent > L.c) {
+        uint32_t p = L.c;
+        while (p < ent) {
+            const SnapTok t = snap_tok(lds_read8(stage, woff + (p - W0)));
+            bit_clr(L, p - rs);
+            L.out -= t.ol;
+            p += uint32_t(t.tl);
+        }
+        L.c = ent;
+    }
+    return X;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_sat(uint32_t v) {
+    uint64_t s = v;
+    #pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+    return s > 0xffffffffull ? 0xffffffffu : uint32_t(s);
+}
+
+__device__ __forceinline__ void store_window(uint32_t* tm, uint32_t* lo, const WinLane& L, int lane) {
+    reinterpret_cast<uint4*>(tm)[lane] = make_uint4(L.b0, L.b1, L.b2, L.b3);
+    lo[lane] = L.out;
+}
+
+__global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict__ jobs, const int2* __restrict__ wins,
+                                                     SnapWin* __restrict__ win, uint32_t* __restrict__ lane_out,
+                                                     int* __restrict__ fb) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[SNAP_WSTAGE];
+    const int2 jw = wins[blockIdx.x];
+    const SnappyJob job = jobs[jw.x];
     const int lane = threadIdx.x;
-    uint64_t pos, ulen;
-    if (!preamble(job.src, job.src_len, pos, ulen) || ulen != job.dst_len) {
-        if (lane == 0) fallback[j] = 1;
+    const uint64_t n = job.src_len;
+    const uint32_t W0 = uint32_t(jw.y) * SNAP_WIN;
+    const uint32_t wi = job.win_base + uint32_t(jw.y);
+    uint32_t* tm = job.tokmap + size_t(jw.y) * SNAP_WWORDS;
+    uint32_t* lo = lane_out + size_t(wi) * 64;
+    uint32_t entry = W0;
+    WinLane L{};
+    if (jw.y == 0) {
+        uint64_t pos = 0, ulen = 0;
+        if (!uvarint(job.src, n, pos, ulen) || ulen != job.dst_len) {   // the serial kernel reports it
+            store_window(tm, lo, L, lane);
+            if (lane == 0) { win[wi] = SnapWin{0, SNAP_INVALID, 0, WIN_BROKEN}; fb[jw.x] = FB_SERIAL; }
+            return;
+        }
+        entry = uint32_t(pos);
+    }
+    if (entry >= n) {   // empty body
+        store_window(tm, lo, L, lane);
+        if (lane == 0) win[wi] = SnapWin{entry, entry, 0, 0};
         return;
     }
-    uint32_t* sp = splits + job.split_base;
-    uint64_t out = 0;
-    const uint64_t n = job.src_len;
-    STAMP_DECL
-    while (pos < n) {
-        __syncthreads();
-        const uint32_t woff = snap_stage_window(stage, job.src, n, pos, lane, 64);
-        __syncthreads();
-        STAMP(5);
-        SnapLane L;
-        SnapSeg S;
-        const uint32_t exit = snap_parse_window(stage, woff, n - pos, L, S);
-        STAMP(6);
-        if (job.tokmap && L.valid) {   // publish token starts for the executor
-            const uint64_t gp = pos + uint64_t(lane) * SNAP_SEG;
-            const uint32_t sh = uint32_t(gp & 31u);
-            atomicOr(job.tokmap + (gp >> 5), L.valid << sh);
-            if (sh) atomicOr(job.tokmap + (gp >> 5) + 1, L.valid >> (32u - sh));
-        }
-        uint64_t lsum = 0;
-        #pragma unroll
-        for (int b = 0; b < 32; b++)
-            if ((L.valid >> b) & 1u) lsum += seg_outlen(S, b);
-        uint64_t x = lsum;
-        #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        const uint64_t base = out + x - lsum;
-        if (lsum && ((base + lsum - 1) / BLOCK != base / BLOCK || base % BLOCK == 0)) {
-            uint64_t o = base;
-            #pragma unroll
-            for (int b = 0; b < 32; b++) {
-                if ((L.valid >> b) & 1u) {
-                    if (o % BLOCK == 0 && o > 0 && o < ulen) {
-                        const uint64_t k = o / BLOCK;
-                        if (k < job.n_pieces) sp[k] = uint32_t(pos + uint32_t(lane) * SNAP_SEG + uint32_t(b));
-                    }
-                    o += seg_outlen(S, b);
-                }
-            }
-        }
-        out += __shfl(x, 63, 64);
-        if (exit == SNAP_FAR) { pos = n + 1; break; }
-        pos += exit;
-        STAMP(7);
-    }
-    if (lane == 0 && (out != ulen || pos != n)) fallback[j] = 1;
+    const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
+    __syncthreads();
+    uint32_t flags;
+    const uint32_t X = win_parse(stage, woff, W0, n, entry, L, flags);
+    store_window(tm, lo, L, lane);
+    const uint32_t sum = wave_sum_sat(L.out);
+    if (lane == 0) win[wi] = SnapWin{entry, X, sum, flags};
 }
 
-// ---------------------------------------------------------------- k_snappy_exec
-__global__ __launch_bounds__(XNT) void k_snappy_exec(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
-                                                     const uint32_t* __restrict__ splits, int* fallback) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[SNAP_STAGE];
-    __shared__ uint32_t P[WOUT];
-    __shared__ SnapRec rec[REC_CAP];
-    __shared__ uint32_t s_nrec, s_wout, s_exit, s_bad, s_big_out, s_big_src, s_big_len;
+#ifdef PF_SNAP_TRACE
+__device__ uint32_t pf_trace[8192];
+__device__ uint32_t pf_trace_n;
+#define TRACE(...)                                                                             \
+    do {                                                                                       \
+        if (tr && lane == 0) {                                                                 \
+            const uint32_t v_[] = {__VA_ARGS__};                                               \
+            const uint32_t at_ = atomicAdd(&pf_trace_n, uint32_t(sizeof v_ / 4));              \
+            for (uint32_t q_ = 0; q_ < sizeof v_ / 4 && at_ + q_ < 8192; q_++) pf_trace[at_ + q_] = v_[q_]; \
+        }                                                                                      \
+    } while (0)
+extern "C" int pf_debug_trace(uint32_t* out, int n, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_trace), 4 * size_t(n < 8192 ? n : 8192)) != hipSuccess) return -1;
+    if (reset) {
+        uint32_t z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(pf_trace_n), &z, 4) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#define TRACEF(...)                                                                            \
+    do {                                                                                       \
+        const uint32_t v_[] = {__VA_ARGS__};                                                   \
+        const uint32_t at_ = atomicAdd(&pf_trace_n, uint32_t(sizeof v_ / 4));                  \
+        for (uint32_t q_ = 0; q_ < sizeof v_ / 4 && at_ + q_ < 8192; q_++) pf_trace[at_ + q_] = v_[q_]; \
+    } while (0)
+#else
+#define TRACE(...) ((void)0)
+#define TRACEF(...) ((void)0)
+#endif
 
-    const int2 pc = pieces[blockIdx.x];
-    const int j = pc.x, k = pc.y;
+// ======================================================================== fix pass
+
+constexpr int FIX_MAXW = 1024;       // pages up to 8 MiB compressed (larger: serial fallback)
+constexpr int MERGE_STEPS = 64;      // true-chain steps before a window is re-parsed instead
+constexpr int FIX_ROUNDS = 32;
+
+__device__ __forceinline__ bool tm_get(const uint32_t* tm, uint32_t i) { return (tm[i >> 5] >> (i & 31u)) & 1u; }
+__device__ __forceinline__ void tm_set(uint32_t* tm, uint32_t i) { tm[i >> 5] |= 1u << (i & 31u); }
+__device__ __forceinline__ void tm_clr(uint32_t* tm, uint32_t i) { tm[i >> 5] &= ~(1u << (i & 31u)); }
+
+__global__ __launch_bounds__(64) void k_snappy_fix(const SnappyJob* __restrict__ jobs, SnapWin* __restrict__ win,
+                                                   uint32_t* __restrict__ lane_out, uint32_t* __restrict__ splits,
+                                                   int* __restrict__ fb) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[SNAP_WSTAGE];
+    __shared__ uint32_t s_x[FIX_MAXW], s_ent[FIX_MAXW], s_c[FIX_MAXW], s_pre[FIX_MAXW + 1];
+    __shared__ uint8_t s_rr[FIX_MAXW], s_fl[FIX_MAXW], s_tr[FIX_MAXW];
+    __shared__ uint32_t s_end;
+    const int j = blockIdx.x;
+    const int lane = threadIdx.x;
     const SnappyJob job = jobs[j];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t* sp = splits + job.split_base;
-    if (k > 0 && sp[k] == 0xffffffffu) return;          // merged into an earlier piece
-    uint64_t p0, ulen;
-    if (!preamble(job.src, job.src_len, p0, ulen) || ulen != job.dst_len) { if (tid == 0) fallback[j] = 1; return; }
-    const uint8_t* in = job.src;
-    uint8_t* dst = job.dst;
-    uint64_t in_pos = k == 0 ? p0 : sp[k];
-    const uint32_t out_start = uint32_t(k) * BLOCK;
-    uint64_t in_end = job.src_len;
-    uint32_t out_end = uint32_t(ulen);
-    for (uint32_t k2 = k + 1; k2 < job.n_pieces; k2++)
-        if (sp[k2] != 0xffffffffu) { in_end = sp[k2]; out_end = k2 * BLOCK; break; }
-    if (in_pos > in_end || out_start > out_end) { if (tid == 0) fallback[j] = 1; return; }
-
-    uint32_t op = out_start;
-    bool bad = false;
-    STAMP_DECL
-    while (in_pos < in_end) {
+    if (fb[j] == FB_SERIAL) return;
+    const uint32_t nw = job.n_win;
+    const uint64_t n = job.src_len;
+    SnapWin* Wn = win + job.win_base;
+    uint32_t* LO = lane_out + size_t(job.win_base) * 64;
+    if (nw > uint32_t(FIX_MAXW) || (Wn[0].flags & WIN_BROKEN)) {
+        if (lane == 0) fb[j] = FB_SERIAL;
+        return;
+    }
+    bool ok = false;
+    for (int round = 0; round < FIX_ROUNDS; round++) {
+        for (uint32_t w = lane; w < nw; w += 64) {
+            const SnapWin sw = Wn[w];
+            s_x[w] = sw.exit;
+            s_c[w] = sw.entry;
+            s_fl[w] = uint8_t(sw.flags);
+            s_rr[w] = 0;
+        }
         __syncthreads();
-        const uint32_t woff = snap_stage_window(stage, in, in_end, in_pos, tid, XNT);
+        if (lane == 0) {
+            // True entries along the chain, assuming each window's exit is right. While the entry is
+            // trusted (derived from exact windows only), a window whose first token already leaves
+            // it (a long literal) is resolved right here, so literal-only runs settle in one round.
+            uint32_t e = s_x[0];
+            bool trusted = true;
+            for (uint32_t w = 1; w < nw; w++) {
+                s_ent[w] = e;
+                s_tr[w] = trusted;
+                const uint64_t wend = min(uint64_t(w + 1) * SNAP_WIN, n);
+                if (uint64_t(e) >= wend) continue;
+                if (e == s_c[w] && !(s_fl[w] & (WIN_PASS | WIN_BROKEN))) { e = s_x[w]; continue; }
+                if (trusted) {
+                    const uint64_t x = e + snap_tok(glb_read8(job.src, n, e)).tl;
+                    if (x >= wend && x <= n) { s_rr[w] = 2; e = uint32_t(x); continue; }
+                }
+                trusted = false;
+                e = s_x[w];
+            }
+            for (uint32_t w = 0; w < nw; w++) TRACEF(0xEEEE0000u | uint32_t(round), w, w ? s_ent[w] : 0u, s_c[w], s_x[w], uint32_t(s_fl[w]) | (uint32_t(s_rr[w]) << 8));
+        }
         __syncthreads();
-        STAMP(0);
-        const uint32_t wbase = op;
-        // ---------------- wave 0: parse + records (all from registers) ----------------
-        if (wid == 0) {
-            SnapLane L;
-            SnapSeg S;
-            if (job.tokmap) {
-                // indexed page: token starts come from k_snappy_index's bitmap, no re-parse
-                snap_seg_init(S, stage, woff, lane);
-                const uint64_t limit = in_end - in_pos;
-                const uint32_t ss = uint32_t(lane) * SNAP_SEG;
-                const uint32_t lim = limit >= ss + 32 ? 32u : (limit <= ss ? 0u : uint32_t(limit - ss));
-                const uint64_t gp = in_pos + ss;
-                const uint32_t sh = uint32_t(gp & 31u);
-                uint32_t m = job.tokmap[gp >> 5] >> sh;
-                if (sh) m |= job.tokmap[(gp >> 5) + 1] << (32u - sh);
-                m &= lim >= 32 ? 0xffffffffu : ((1u << lim) - 1u);
-                uint32_t own = 0;
-                #pragma unroll
-                for (int b = 0; b < 32; b++) {
-                    if ((m >> b) & 1u) {
-                        uint32_t il = pk(S.tl, b);
-                        if (il == 255u) { uint32_t olen; snap_long_literal(stage + woff, ss + uint32_t(b), il, olen); }
-                        own = il == SNAP_FAR ? SNAP_FAR : ss + uint32_t(b) + il;
-                    }
+        int changed = 0, serial = 0;
+        for (uint32_t w = 1 + lane; w < nw; w += 64) {
+            const uint32_t e = s_ent[w];
+            const uint32_t W0 = w * SNAP_WIN;
+            const uint64_t wend = min(uint64_t(W0) + SNAP_WIN, n);
+            uint32_t* tm = job.tokmap + size_t(w) * SNAP_WWORDS;
+            uint32_t* lo = LO + size_t(w) * 64;
+            const uint32_t c = s_c[w], x0 = s_x[w], fl = s_fl[w];
+            const bool pass = fl & WIN_PASS;
+            if (e >= wend) {   // jumped over by a literal: no token starts in this window
+                if (!pass || c != e) {
+                    for (int q = 0; q < 64; q++) { reinterpret_cast<uint4*>(tm)[q] = make_uint4(0, 0, 0, 0); lo[q] = 0; }
+                    Wn[w] = SnapWin{e, e, 0, WIN_PASS};
                 }
-                #pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_up(own, d, 64);
-                    if (lane >= d) own = max(own, y);
+                continue;
+            }
+            if (e == c && !pass) continue;   // verified against this entry before
+            uint64_t q = e;
+            uint32_t acc = 0;
+            bool merged = false, bad = false;
+            if (s_rr[w] == 2) {   // a single token spans the rest of the window
+                const SnapTok t = snap_tok(glb_read8(job.src, n, q));
+                acc = t.ol;
+                q += t.tl;
+            } else {   // walk the true chain from e until it meets the window's chain
+                int steps = 0;
+                while (q < wend && steps < MERGE_STEPS) {
+                    if (!pass && tm_get(tm, uint32_t(q) - W0)) { merged = true; break; }
+                    const SnapTok t = snap_tok(glb_read8(job.src, n, q));
+                    acc += t.ol;
+                    q += t.tl;
+                    steps++;
+                    if (q > n) { bad = true; break; }
                 }
-                L.valid = m;
-                L.committed = 1;
-                L.exit = own;
+            }
+            TRACEF(0xFFFF0000u | (bad ? 1u : 0u) | (merged ? 2u : 0u) | (q >= wend ? 4u : 0u), w, e, uint32_t(q), acc);
+            if (bad) {   // the chain from e leaves the stream: corrupt if e is known true, else a bad guess
+                if (s_tr[w]) serial = 1;
+            } else if (merged) {
+                const SnapWin sw = Wn[w];
+                uint32_t rem = 0;
+                for (uint64_t p = c; p < q;) {   // the guessed chain's tokens before the meeting point
+                    const SnapTok t = snap_tok(glb_read8(job.src, n, p));
+                    tm_clr(tm, uint32_t(p) - W0);
+                    lo[(uint32_t(p) - W0) / SNAP_RB] -= t.ol;
+                    rem += t.ol;
+                    p += t.tl;
+                }
+                for (uint64_t p = e; p < q;) {   // the true ones
+                    const SnapTok t = snap_tok(glb_read8(job.src, n, p));
+                    tm_set(tm, uint32_t(p) - W0);
+                    lo[(uint32_t(p) - W0) / SNAP_RB] += t.ol;
+                    p += t.tl;
+                }
+                Wn[w] = SnapWin{e, sw.exit, sw.out - rem + acc, sw.flags};
+            } else if (q >= wend) {   // the true chain crosses the window without meeting it
+                for (int r = 0; r < 64; r++) { reinterpret_cast<uint4*>(tm)[r] = make_uint4(0, 0, 0, 0); lo[r] = 0; }
+                for (uint64_t p = e; p < q;) {
+                    const SnapTok t = snap_tok(glb_read8(job.src, n, p));
+                    tm_set(tm, uint32_t(p) - W0);
+                    lo[(uint32_t(p) - W0) / SNAP_RB] += t.ol;
+                    p += t.tl;
+                }
+                Wn[w] = SnapWin{e, uint32_t(q), acc, 0};
+                if (uint32_t(q) != x0) changed = 1;
             } else {
-                (void)snap_parse_window(stage, woff, in_end - in_pos, L, S);
-            }
-            uint32_t osum = 0, cnt = 0, bigl = 0;
-            #pragma unroll
-            for (int b = 0; b < 32; b++) {
-                if ((L.valid >> b) & 1u) {
-                    const uint32_t ol = seg_outlen(S, b);
-                    const bool lit = (sbyte(S, b) & 3u) == 0;
-                    if (lit && ol > BIGLIT) bigl = ol;
-                    else { osum += ol; cnt += lit ? (ol + LPIECE - 1) / LPIECE : 1u; }
-                }
-            }
-            uint32_t x = osum, xc = cnt;
-            #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(x, d, 64), yc = __shfl_up(xc, d, 64);
-                if (lane >= d) { x += y; xc += yc; }
-            }
-            const unsigned long long comm = __ballot(L.committed);
-            int f2 = 64 - __clzll(comm);
-            const unsigned long long over = __ballot(L.committed && x > WOUT);
-            if (over) f2 = min(f2, __ffsll(over) - 1);
-            const unsigned long long big = __ballot(L.committed && bigl != 0);
-            if (big) f2 = min(f2, __ffsll(big));              // include the big literal's lane
-            bool lbad = false;
-            if (lane < f2) {
-                uint32_t o = wbase + x - osum;
-                uint32_t ri = xc - cnt;
-                const uint64_t lin = in_pos + uint32_t(lane) * SNAP_SEG;
-                #pragma unroll
-                for (int b = 0; b < 32; b++) {
-                    if ((L.valid >> b) & 1u) {
-                        const uint32_t tag = sbyte(S, b);
-                        const uint32_t ol = seg_outlen(S, b);
-                        if ((tag & 3u) == 0) {
-                            const uint32_t hdr = (tag >> 2) < 60 ? 1u : 1u + ((tag >> 2) - 59u);
-                            const uint64_t s = lin + uint32_t(b) + hdr;
-                            if (s + ol > in_end) lbad = true;
-                            if (ol > BIGLIT) {
-                                s_big_out = o; s_big_src = uint32_t(s); s_big_len = ol;
-                            } else {
-                                for (uint32_t q = 0; q < ol; q += LPIECE)
-                                    rec[ri++] = SnapRec{o + q, uint32_t(s + q), min(LPIECE, ol - q) | 0x80000000u};
-                                o += ol;
-                            }
-                        } else {
-                            uint32_t off;
-                            if ((tag & 3u) == 1) off = ((tag >> 5) << 8) | sbyte(S, b + 1);
-                            else if ((tag & 3u) == 2) off = sbyte(S, b + 1) | sbyte(S, b + 2) << 8;
-                            else off = sbyte(S, b + 1) | sbyte(S, b + 2) << 8 | sbyte(S, b + 3) << 16 | sbyte(S, b + 4) << 24;
-                            if (off == 0 || off > o - out_start) lbad = true;   // reaches before the piece
-                            rec[ri++] = SnapRec{o, off, ol};
-                            o += ol;
-                        }
-                    }
-                }
-            }
-            const bool anybad = __any(lbad);
-            const int src_lane = f2 > 0 ? f2 - 1 : 0;
-            const uint32_t t_nrec = __shfl(xc, src_lane, 64);
-            const uint32_t t_wout = __shfl(x, src_lane, 64);
-            const uint32_t t_exit = __shfl(L.exit, src_lane, 64);
-            if (lane == 0) {
-                s_bad = (anybad || f2 <= 0) ? 1u : 0u;
-                s_nrec = t_nrec;
-                s_wout = t_wout;
-                s_exit = t_exit;
-                if (!(big && f2 == __ffsll(big))) s_big_len = 0;
+                s_rr[w] = 1;   // long divergence: re-parse below
             }
         }
+        __threadfence();   // other lanes read these windows' tables next
         __syncthreads();
-        STAMP(1);
-        const uint32_t nrec = s_nrec, wout = s_wout, wexit = s_exit, blen = s_big_len;
-        if (s_bad || uint64_t(wbase) + wout + blen > out_end || wexit == 0 || wexit == SNAP_FAR) { bad = true; break; }
-        // ---------------- pointers: one slot per output byte ----------------
-        for (uint32_t r = tid; r < nrec; r += XNT) {
-            const SnapRec t = rec[r];
-            const uint32_t len = t.len & 0x7fffffffu;
-            uint32_t* pd = P + (t.out - wbase);
-            if (t.len & 0x80000000u) {
-                for (uint32_t q = 0; q < len; q++) pd[q] = INPUT | (t.src + q);
-            } else if (t.src >= len) {
-                const uint32_t s0 = t.out - t.src;
-                for (uint32_t q = 0; q < len; q++) pd[q] = s0 + q;
-            } else {
-                const uint32_t s0 = t.out - t.src;
-                uint32_t jj = 0;
-                for (uint32_t q = 0; q < len; q++) {
-                    pd[q] = s0 + jj;
-                    jj = (jj + 1 == t.src) ? 0u : jj + 1;
-                }
-            }
+        for (uint32_t w = 1; w < nw; w++) {   // re-parse windows from their entry (whole wave)
+            if (s_rr[w] != 1) continue;
+            const uint32_t W0 = w * SNAP_WIN;
+            const uint32_t e = s_ent[w];
+            __syncthreads();
+            const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
+            __syncthreads();
+            WinLane L;
+            uint32_t fl;
+            const uint32_t X = win_parse(stage, woff, W0, n, e, L, fl);
+            store_window(job.tokmap + size_t(w) * SNAP_WWORDS, LO + size_t(w) * 64, L, lane);
+            const uint32_t sum = wave_sum_sat(L.out);
+            if (lane == 0) Wn[w] = SnapWin{e, X, sum, fl};
+            if (lane == 0) TRACEF(0x99990000u, w, e, X, fl);
+            if (X != s_x[w]) changed = 1;
         }
+        if (__any(serial)) {
+            if (lane == 0) fb[j] = FB_SERIAL;
+            return;
+        }
+        const bool any_changed = __any(changed);
+        __threadfence();
         __syncthreads();
-        STAMP(2);
-        // ---------------- pointer jumping (loads batched for ILP) ----------------
-        for (;;) {
-            int pending = 0;
-            #pragma unroll
-            for (int h = 0; h < PER_T; h += 16) {
-                uint32_t v[16];
-                #pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const uint32_t b = uint32_t(tid) + uint32_t(XNT) * uint32_t(h + i);
-                    v[i] = b < wout ? P[b] : INPUT;
-                }
-                uint32_t u[16];
-                #pragma unroll
-                for (int i = 0; i < 16; i++) u[i] = (!(v[i] & INPUT) && v[i] >= wbase) ? P[v[i] - wbase] : v[i];
-                #pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    if (u[i] != v[i]) {
-                        P[uint32_t(tid) + uint32_t(XNT) * uint32_t(h + i)] = u[i];
-                        pending |= !(u[i] & INPUT) && u[i] >= wbase;
-                    }
-                }
-            }
-            if (!__syncthreads_or(pending)) break;
+        if (!any_changed) { ok = true; break; }
+    }
+    if (lane == 0) {   // the converged chain: every window entered where verified, none broken
+        uint32_t e = Wn[0].exit;
+        for (uint32_t w = 1; w < nw && ok; w++) {
+            const SnapWin sw = Wn[w];
+            if (uint64_t(e) >= min(uint64_t(w + 1) * SNAP_WIN, n)) continue;
+            if (sw.entry != e || (sw.flags & (WIN_PASS | WIN_BROKEN))) ok = false;
+            e = sw.exit;
         }
-        STAMP(3);
-        // ---------------- gather + store (loads batched) ----------------
-        const uint64_t stage_first = in_pos - woff;
-        #pragma unroll
-        for (int h = 0; h < PER_T; h += 16) {
-            uint32_t v[16];
-            #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const uint32_t b = uint32_t(tid) + uint32_t(XNT) * uint32_t(h + i);
-                v[i] = b < wout ? P[b] : 0u;
-            }
-            uint8_t by[16];
-            #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const uint32_t b = uint32_t(tid) + uint32_t(XNT) * uint32_t(h + i);
-                by[i] = 0;
-                if (b < wout) {
-                    if (v[i] & INPUT) {
-                        const uint64_t ip = v[i] & ~INPUT;
-                        by[i] = (ip >= stage_first && ip < stage_first + SNAP_STAGE) ? stage[ip - stage_first] : in[ip];
-                    } else {
-                        by[i] = dst[v[i]];
-                    }
-                }
-            }
-            #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const uint32_t b = uint32_t(tid) + uint32_t(XNT) * uint32_t(h + i);
-                if (b < wout) dst[wbase + b] = by[i];
-            }
-        }
-        for (uint32_t q = tid; q < blen; q += XNT) dst[s_big_out + q] = in[s_big_src + q];
-        STAMP(4);
-        op = wbase + wout + blen;
-        in_pos += wexit;
+        s_end = ok ? e : SNAP_INVALID;
     }
     __syncthreads();
-    if ((bad || op != out_end || in_pos != in_end) && tid == 0) fallback[j] = 1;
+    // totals
+    uint32_t run = 0;
+    for (uint32_t w0 = 0; w0 < nw; w0 += 64) {
+        const uint32_t w = w0 + lane;
+        const uint32_t o = w < nw ? Wn[w].out : 0u;
+        uint32_t x = o;
+        #pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (w < nw) s_pre[w] = run + x - o;
+        run += __shfl(x, 63, 64);
+    }
+    if (s_end != n || run != job.dst_len) {
+        if (lane == 0) fb[j] = FB_SERIAL;
+        return;
+    }
+    __syncthreads();
+    // input position of the token starting at each 64 KiB output boundary
+    uint32_t* sp = splits + job.split_base;
+    for (uint32_t k = 1 + lane; k < job.n_pieces; k += 64) {
+        const uint32_t B = k * SNAP_BLOCK;
+        uint32_t a = 0, b = nw;   // last window with s_pre <= B
+        while (b - a > 1) {
+            const uint32_t m = (a + b) / 2;
+            if (s_pre[m] <= B) a = m; else b = m;
+        }
+        const uint32_t w = a;
+        uint32_t cum = s_pre[w];
+        const uint32_t* lo = LO + size_t(w) * 64;
+        int l = 0;
+        for (; l < 63; l++) {
+            const uint32_t v = lo[l];
+            if (B < cum + v) break;
+            cum += v;
+        }
+        const uint32_t rs = w * SNAP_WIN + uint32_t(l) * SNAP_RB;
+        const uint32_t* tm = job.tokmap + size_t(w) * SNAP_WWORDS + l * 4;
+        uint32_t found = SNAP_INVALID;
+        bool done = false;
+        for (int wd = 0; wd < 4 && !done; wd++) {
+            uint32_t m = tm[wd];
+            while (m) {
+                const uint32_t p = rs + uint32_t(wd) * 32 + uint32_t(__ffs(m) - 1);
+                m &= m - 1;
+                if (cum == B) { found = p; done = true; break; }
+                if (cum > B) { done = true; break; }
+                cum += snap_tok(glb_read8(job.src, n, p)).ol;
+            }
+        }
+        sp[k] = found;
+    }
+}
+
+// ======================================================================== executor
+
+
+constexpr uint32_t XRING = 8192;     // output ring (LDS)
+constexpr uint32_t XRMASK = XRING - 1;
+constexpr uint32_t XSLOT = 2048;     // flush granule
+constexpr uint32_t XCHUNK = 1024;    // input bytes whose tokens are enumerated at once
+constexpr uint32_t XSTAGE = XCHUNK + 64 + 16;
+
+__device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
+                                                    const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[XRING];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[XSTAGE];
+    __shared__ uint16_t tokpos[XCHUNK / 2];
+    const int lane = threadIdx.x;
+    int j, k;
+    if (mode == 0) { const int2 pc = pieces[blockIdx.x]; j = pc.x; k = pc.y; }
+    else { j = blockIdx.x; k = 0; }
+    const int f = fb[j];
+    bool whole;
+    if (mode == 0) {
+        if (f >= FB_REDO || (f == FB_WHOLE && k > 0)) return;
+        whole = f == FB_WHOLE;
+    } else {
+        if (f != FB_REDO) return;
+        whole = true;
+    }
+    const SnappyJob job = jobs[j];
+    const uint8_t* in = job.src;
+    uint8_t* dst = job.dst;
+    const uint64_t n = job.src_len;
+    const uint32_t* sp = splits + job.split_base;
+    uint64_t pos0 = 0, ulen = 0;
+    if (!uvarint(in, n, pos0, ulen) || ulen != job.dst_len) {
+        if (lane == 0) atomicMax(&fb[j], FB_SERIAL);
+        return;
+    }
+    uint32_t ip, out_start, out_end = job.dst_len;
+    if (whole) {
+        ip = uint32_t(pos0);
+        out_start = 0;
+    } else {
+        if (k > 0 && sp[k] == SNAP_INVALID) return;   // no token at this boundary: an earlier piece covers it
+        ip = k == 0 ? uint32_t(pos0) : sp[k];
+        out_start = uint32_t(k) * SNAP_BLOCK;
+        for (uint32_t k2 = k + 1; k2 < job.n_pieces; k2++)
+            if (sp[k2] != SNAP_INVALID) { out_end = k2 * SNAP_BLOCK; break; }
+    }
+    const uint16_t* tm16 = reinterpret_cast<const uint16_t*>(job.tokmap);
+    uint32_t op = out_start, F = out_start;
+#ifdef PF_SNAP_TRACE
+    const bool tr = false;
+    TRACE(0xAAAA0000u, uint32_t(k), ip, out_start, out_end);
+#endif
+    bool bad = false;
+    while (op < out_end && !bad) {
+        if (ip >= n) { bad = true; break; }
+        const uint32_t I = ip & ~15u;
+        __syncthreads();
+        const uint32_t woff = snap_stage(stage, in, n, I, XSTAGE, lane);
+        // token starts in [ip, I + XCHUNK): 16 input bytes per lane
+        const uint32_t p16 = I + 16u * uint32_t(lane);
+        uint32_t bits = uint64_t(p16) < n ? uint32_t(tm16[p16 >> 4]) : 0u;
+        if (p16 + 16u <= ip) bits = 0;
+        else if (p16 < ip) bits &= ~((1u << (ip - p16)) - 1u);
+        const uint32_t cnt = __popc(bits);
+        uint32_t ex = cnt;
+        #pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(ex, d, 64);
+            if (lane >= d) ex += y;
+        }
+        const uint32_t T = __shfl(ex, 63, 64);
+        uint32_t q = ex - cnt;
+        while (bits) {
+            const uint32_t b = uint32_t(__ffs(bits) - 1);
+            bits &= bits - 1;
+            tokpos[q++] = uint16_t(16u * uint32_t(lane) + b);
+        }
+        __syncthreads();
+        if (T == 0) { bad = true; break; }
+        bool stop = false;
+        for (uint32_t sb = 0; sb < T && !stop && !bad; sb += 64) {
+            const uint32_t t = sb + uint32_t(lane);
+            const bool v = t < T;
+            const uint32_t pos = v ? uint32_t(tokpos[t]) : 0u;
+            const SnapTok tk = snap_tok(lds_read8(stage, woff + pos));
+            const uint32_t ol = v ? tk.ol : 0u;
+            const uint64_t start = uint64_t(I) + pos;
+            const unsigned long long endp = start + tk.tl;
+            const unsigned long long prev = __shfl_up(endp, 1, 64);
+            uint32_t inc = ol;
+            #pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(inc, d, 64);
+                if (lane >= d) inc += y;
+            }
+            const uint32_t otok = op + inc - ol;
+            const bool take = v && otok < out_end;
+            const unsigned long long tb = __ballot(take);
+            const int nt = __popcll(tb);
+            const bool wrong = take && ((lane == 0 ? start != ip : start != prev) || endp > n || op + inc > out_end);
+            if (__any(wrong)) { bad = true; break; }
+            if (nt == 0) break;   // the previous sub-batch ended exactly at out_end
+            if (uint32_t(nt) < min(T - sb, 64u)) stop = true;
+            TRACE(0xBBBB0000u | uint32_t(k), I, ip, T, sb, uint32_t(nt), op, F);
+            const uint32_t srcv = tk.kind == 0 ? uint32_t(start) + tk.arg : tk.arg;
+            const uint32_t kd = tk.kind;
+            for (int i = 0; i < nt; i++) {
+                const uint32_t k_i = __builtin_amdgcn_readlane(kd, i);
+                const uint32_t l_i = __builtin_amdgcn_readlane(ol, i);
+                const uint32_t s_i = __builtin_amdgcn_readlane(srcv, i);
+                const uint32_t o_i = __builtin_amdgcn_readlane(otok, i);
+                if (o_i + l_i + 64 >= out_end || o_i < out_start + 64) TRACE(0xCCCC0000u | (uint32_t(k) << 8) | k_i, l_i, s_i, o_i, F);
+                if (k_i == 0) {
+                    const bool staged = uint64_t(s_i) + l_i <= uint64_t(I) + XCHUNK + 64;
+                    for (uint32_t d = 0; d < l_i; d += 1024) {
+                        const uint32_t c = min(l_i - d, 1024u);
+                        if (staged) {   // uniform: LDS -> LDS
+                            const uint32_t sb0 = woff + (s_i - I) + d;
+                            for (uint32_t qq = uint32_t(lane); qq < c; qq += 64)
+                                ring[(o_i + d + qq) & XRMASK] = stage[sb0 + qq];
+                        } else {        // long literal straight from HBM
+                            const uint8_t* ib = in + s_i + d;
+                            for (uint32_t qq = uint32_t(lane); qq < c; qq += 64)
+                                ring[(o_i + d + qq) & XRMASK] = __builtin_nontemporal_load(ib + qq);
+                        }
+                        const uint32_t upto = o_i + d + c;
+                        while (upto - F >= XSLOT) {
+                            wait_vmem();   // earlier flushes have landed: far copies may read them
+                            const uint32_t a0 = F + uint32_t(lane) * 32u;
+                            const uint4 v0 = *reinterpret_cast<const uint4*>(ring + (a0 & XRMASK));
+                            const uint4 v1 = *reinterpret_cast<const uint4*>(ring + ((a0 + 16u) & XRMASK));
+                            *reinterpret_cast<uint4*>(dst + a0) = v0;
+                            *reinterpret_cast<uint4*>(dst + a0 + 16) = v1;
+                            F += XSLOT;
+                        }
+                    }
+                } else {
+                    if (s_i == 0 || s_i > o_i - out_start) { bad = true; break; }
+                    uint32_t jj = uint32_t(lane);
+                    if (s_i < l_i) jj = jj % s_i;            // overlapping copy repeats its pattern
+                    const uint32_t sa = o_i - s_i + jj;
+                    uint8_t byte = 0;
+                    if (s_i <= XRING) {
+                        if (uint32_t(lane) < l_i) byte = ring[sa & XRMASK];
+                    } else {
+                        if (uint32_t(lane) < l_i) byte = dst[sa];   // flushed: >= 6 KiB behind F
+                    }
+                    if (uint32_t(lane) < l_i) ring[(o_i + uint32_t(lane)) & XRMASK] = byte;
+#ifdef PF_SNAP_SAFE
+                    __syncthreads();
+#endif
+                    const uint32_t upto = o_i + l_i;
+                    while (upto - F >= XSLOT) {
+                        wait_vmem();
+                        const uint32_t a0 = F + uint32_t(lane) * 32u;
+                        const uint4 v0 = *reinterpret_cast<const uint4*>(ring + (a0 & XRMASK));
+                        const uint4 v1 = *reinterpret_cast<const uint4*>(ring + ((a0 + 16u) & XRMASK));
+                        *reinterpret_cast<uint4*>(dst + a0) = v0;
+                        *reinterpret_cast<uint4*>(dst + a0 + 16) = v1;
+                        F += XSLOT;
+                    }
+                }
+            }
+            if (bad) break;
+#ifdef PF_SNAP_SAFE
+            __syncthreads();
+#endif
+            op += __builtin_amdgcn_readlane(inc, nt - 1);
+            ip = uint32_t(__shfl(endp, nt - 1, 64));
+            if (op >= out_end) stop = true;
+        }
+    }
+    if (bad) {
+        if (lane == 0) atomicMax(&fb[j], whole ? FB_SERIAL : FB_REDO);
+        return;
+    }
+    TRACE(0xDDDD0000u | uint32_t(k), op, F, ip, out_end);
+    // tail: bytes [F, op)
+    for (uint32_t a = F + uint32_t(lane) * 16u; a + 16u <= op; a += 1024u)
+        *reinterpret_cast<uint4*>(dst + a) = *reinterpret_cast<const uint4*>(ring + (a & XRMASK));
+    for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) dst[a] = ring[a & XRMASK];
 }
 
 #ifdef PF_STAMPS
@@ -379,14 +640,18 @@ extern "C" int pf_debug_stamps(unsigned long long* out, int n, int reset) {
 }
 #endif
 
-// ---------------------------------------------------------------- launchers
-void launch_snappy_index(const SnappyJob* d_jobs, const int* d_index_list, int n_index, uint32_t* d_splits,
-                         int* d_fallback, hipStream_t s) {
-    if (n_index > 0) hipLaunchKernelGGL(k_snappy_index, dim3(n_index), dim3(64), 0, s, d_jobs, d_index_list, d_splits, d_fallback);
-}
-void launch_snappy_exec(const SnappyJob* d_jobs, const int2* d_pieces, int n_pieces, const uint32_t* d_splits,
-                        int* d_fallback, hipStream_t s) {
-    if (n_pieces > 0) hipLaunchKernelGGL(k_snappy_exec, dim3(n_pieces), dim3(XNT), 0, s, d_jobs, d_pieces, d_splits, d_fallback);
+void launch_snappy_serial(const SnappyJob*, int, const int*, DevChunkResult*, hipStream_t);
+
+// All Snappy work of one batch, in stream order. fb must be zero on entry.
+void launch_snappy(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
+                   uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, uint32_t* d_splits, int* d_fb,
+                   DevChunkResult* d_res, hipStream_t s) {
+    if (n_jobs <= 0) return;
+    hipLaunchKernelGGL(k_snappy_index, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, d_win, d_lane_out, d_fb);
+    hipLaunchKernelGGL(k_snappy_fix, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_win, d_lane_out, d_splits, d_fb);
+    hipLaunchKernelGGL(k_snappy_exec, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
+    hipLaunchKernelGGL(k_snappy_exec, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
+    launch_snappy_serial(d_jobs, n_jobs, d_fb, d_res, s);
 }
 
 }  // namespace pf

@@ -70,3 +70,30 @@ def test_metadata_matches_oracle(native, oracle, name):
                 total = sum(d.pages[i].num_values for i in range(d.n_pages) if d.pages[i].page_type != 2)
                 exp = next(ch for ch in fm["chunks"] if ch["rg"] == rg and ch["col"] == c)
                 assert total == exp["num_entries"]
+
+
+def test_struct_layouts_match_header(native, tmp_path):
+    """The ctypes mirror (what an FFM/ctypes binding declares) matches the C header's layout:
+    sizeof and every field offset, from a probe compiled against include/pfloor.h."""
+    import subprocess
+    structs = {"pf_page_desc": native.PageDesc, "pf_chunk_desc": native.ChunkDesc,
+               "pf_column_out": native.ColumnOut, "pf_column_info": native.ColumnInfo,
+               "pf_column_meta": native.ColumnMeta}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "pfloor.h"', "int main(void){"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0;}")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for ln in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        s, f, v = ln.split()
+        got[(s, f)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == C.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
