@@ -46,7 +46,7 @@ struct DevPage {
     int32_t def_enc;
     int32_t rep_enc;
     int32_t num_values;       // level entries
-    int32_t pad0;
+    int32_t done;             // set by k_flat when it decoded (or failed) the page; k_decode skips it
     int64_t entry_start;      // first level entry of this page within its chunk (host prefix sum)
     // written by k_count, consumed by k_scan
     int64_t n_slots;

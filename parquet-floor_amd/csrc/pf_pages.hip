@@ -157,21 +157,52 @@ __device__ inline int64_t plain_binary_walk(const uint8_t* p, uint64_t n, int64_
 
 // ---- workgroup-parallel PLAIN BYTE_ARRAY walk --------------------------------------------------
 // The <len><bytes> chain is serial, but a 4-byte little-endian length is "plausible" at position q
-// only if q + 4 + len <= n; inside text (or most payloads) only the true prefixes are. Every
-// thread tests 8 positions per 2 KiB tile; plausible positions are emitted in order (block scan)
-// and each must be its predecessor's successor (q_next == q + 4 + len), the first at 0. Any
-// mismatch — a false candidate, overflow, too few candidates — falls back to the exact serial
-// walk, so the result is always the chain parquet-mr's BinaryPlainValuesReader reads.
-constexpr int BW_TILE = NT * 8;          // bytes per tile
-constexpr int BW_CAP = BW_TILE / 4;      // candidates per tile (true prefixes are >= 4 bytes apart)
+// only if q + 4 + len <= n, and a true prefix is followed by another plausible prefix (or by the
+// stream end). Inside text (or most payloads) only the true prefixes pass both tests: the second
+// one drops the candidates text produces just before each true prefix (the previous value's last
+// byte + the low bytes of the next length). Every thread tests BW_BPT positions of a tile staged
+// in LDS; plausible positions are emitted in order (block scan) and each must be its
+// predecessor's successor (q_next == q + 4 + len), the first at 0. Any mismatch — a false
+// candidate, overflow, too few candidates — falls back to the exact serial walk, so the result is
+// always the chain parquet-mr's BinaryPlainValuesReader reads.
+constexpr int BW_BPT = 16;                          // positions per thread per tile
+constexpr int BW_TILE = NT * BW_BPT;                // bytes per tile
+constexpr int BW_LOOK = 64;                         // staged lookahead for successor tests
+constexpr int BW_STAGE = BW_TILE + BW_LOOK + 16;    // + alignment shift
+constexpr int BW_CAP = BW_TILE / 4;                 // candidates per tile (true prefixes are >= 4 bytes apart)
 
 struct BinWalkLds {
+    __attribute__((aligned(16))) uint8_t stage[BW_STAGE];
     uint32_t cand[BW_CAP];
     uint32_t next[BW_CAP];
     uint32_t scan[NT / 64];
     unsigned long long chars;
     uint32_t found, carry, bad;
 };
+
+// 4 bytes from LDS at byte offset a (a + 8 must be staged when a is not 4-aligned).
+__device__ __forceinline__ uint32_t lds_read4(const uint8_t* s, uint32_t a) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(s + (a & ~3u));
+    const uint32_t sh = 8u * (a & 3u);
+    return sh ? (w[0] >> sh) | (w[1] << (32u - sh)) : w[0];
+}
+
+// Stage p[base - woff, base - woff + bytes) into LDS with 16-byte loads by the whole workgroup;
+// 16-byte chunks wholly at or past n read as zero. Returns woff (base's 16-B misalignment).
+__device__ __forceinline__ uint32_t wg_stage(uint8_t* stage, const uint8_t* p, uint64_t n, uint64_t base,
+                                             uint32_t bytes) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p + base);
+    const uint32_t woff = uint32_t(a & 15u);
+    const uint4* src = reinterpret_cast<const uint4*>(a - woff);
+    const int64_t first = int64_t(base) - int64_t(woff);
+    for (uint32_t c = threadIdx.x; c < bytes / 16; c += blockDim.x) {
+        const int64_t q = first + int64_t(c) * 16;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (q < int64_t(n)) v = src[c];
+        reinterpret_cast<uint4*>(stage)[c] = v;
+    }
+    return woff;
+}
 
 __device__ inline int64_t binary_walk_wg(const uint8_t* p, uint64_t n, int64_t count, uint32_t* pos, uint32_t* len,
                                          BinWalkLds& W) {
@@ -182,15 +213,26 @@ __device__ inline int64_t binary_walk_wg(const uint8_t* p, uint64_t n, int64_t c
     if (n > 0x7fffffffull) return -1;
     for (uint64_t t0 = 0; t0 < n; t0 += BW_TILE) {
         if (W.found >= uint64_t(count) || W.bad) break;
-        const uint64_t b0 = t0 + uint64_t(tid) * 8;
-        uint32_t flags = 0, L[8];
+        const uint32_t woff = wg_stage(W.stage, p, n, t0, BW_STAGE);
+        __syncthreads();
+        const uint64_t b0 = t0 + uint64_t(tid) * BW_BPT;
+        uint32_t flags = 0, L[BW_BPT];
         #pragma unroll
-        for (int i = 0; i < 8; i++) {
+        for (int i = 0; i < BW_BPT; i++) {
             const uint64_t q = b0 + i;
             L[i] = 0;
             if (q + 4 <= n) {
-                const uint32_t l = ld32le(p, q, n);
-                if (uint64_t(l) <= n - q - 4) { flags |= 1u << i; L[i] = l; }
+                const uint32_t l = lds_read4(W.stage, woff + uint32_t(q - t0));
+                if (uint64_t(l) <= n - q - 4) {
+                    const uint64_t s = q + 4 + l;
+                    bool ok = s == n;
+                    if (!ok && s + 4 <= n) {
+                        const uint32_t l2 = s + 8 <= t0 + BW_TILE + BW_LOOK ? lds_read4(W.stage, woff + uint32_t(s - t0))
+                                                                              : ld32le(p, s, n);
+                        ok = uint64_t(l2) <= n - s - 4;
+                    }
+                    if (ok) { flags |= 1u << i; L[i] = l; }
+                }
             }
         }
         uint32_t tot;
@@ -199,7 +241,7 @@ __device__ inline int64_t binary_walk_wg(const uint8_t* p, uint64_t n, int64_t c
         const uint32_t base = W.found;
         uint64_t my_chars = 0;
         #pragma unroll
-        for (int i = 0; i < 8; i++) {
+        for (int i = 0; i < BW_BPT; i++) {
             if ((flags >> i) & 1u) {
                 const uint32_t q = uint32_t(b0 + i);
                 W.cand[idx] = q;
@@ -436,7 +478,7 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
-    if (res[pg.chunk].status != 0) return;   // an earlier stage failed this chunk
+    if (pg.done || res[pg.chunk].status != 0) return;   // k_flat took it / an earlier stage failed this chunk
     Sections s;
     const bool ok = page_sections(pg, ck, s);
     if (tid == 0) {
@@ -648,6 +690,315 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
                                         (unsigned long long)vidx);
 }
 
+// ---- k_flat: data pages of flat columns (max_rep == 0) ------------------------------------------
+// The same per-value work as k_decode, organised for throughput. The definition-level and
+// dictionary-id run headers of the page are walked ONCE (one lane of wave 0 and one of wave 1,
+// concurrently) into LDS run tables; tiles of FT entries then expand them by binary search with no
+// serial section, one workgroup scan for the value index (none when the page has no nulls) and one
+// for BYTE_ARRAY char offsets. BYTE_ARRAY chars are copied cooperatively, one 16-byte output chunk
+// per thread step (coalesced stores), instead of a byte loop per value.
+// Pages it does not take (run tables full, BIT_PACKED levels, RLE booleans, BYTE_STREAM_SPLIT,
+// corrupt section layout) keep done == 0 and are decoded by k_decode.
+constexpr int FT = 2048;             // entries per tile
+constexpr int FEPT = FT / NT;        // consecutive entries per thread
+constexpr int RUN_CAP = 256;
+
+struct Run {
+    uint32_t first;    // index of the first value the run covers (entries for levels)
+    uint32_t count;
+    uint32_t data;     // RLE value, or absolute bit offset of the run's packed values
+    uint32_t packed;
+};
+
+// Walk RLE/bit-packed hybrid run headers of p[0..n) (parquet-mr RunLengthBitPackingHybridDecoder)
+// until `limit` values are covered. Returns 0 covered, 1 stream ended or corrupt first, 2 table full.
+__device__ int walk_runs(const uint8_t* p, uint64_t n, int bw, uint32_t limit, Run* runs, int cap, int& nruns,
+                         uint32_t& covered) {
+    uint64_t pos = 0;
+    nruns = 0;
+    covered = 0;
+    while (covered < limit) {
+        uint64_t h;
+        if (!uvarint(p, n, pos, h)) return 1;
+        Run r;
+        uint64_t cnt;
+        if (h & 1) {
+            cnt = (h >> 1) * 8;
+            const uint64_t nb = (h >> 1) * uint64_t(bw);
+            r.data = uint32_t(pos * 8);
+            r.packed = 1;
+            pos += nb < n - pos ? nb : n - pos;   // truncated to what is left (zero-padded)
+        } else {
+            cnt = h >> 1;
+            const int nbv = (bw + 7) >> 3;
+            if (pos + nbv > n) return 1;
+            uint32_t v = 0;
+            for (int b = 0; b < nbv; b++) v |= uint32_t(p[pos + b]) << (8 * b);
+            pos += nbv;
+            r.data = v;
+            r.packed = 0;
+        }
+        if (cnt == 0) continue;
+        if (nruns == cap) return 2;
+        r.first = covered;
+        r.count = uint32_t(cnt < uint64_t(limit - covered) ? cnt : uint64_t(limit - covered));
+        runs[nruns++] = r;
+        covered += r.count;
+    }
+    return 0;
+}
+
+// Index of the run holding value i (runs sorted by `first`, runs[0].first == 0).
+__device__ __forceinline__ int run_find(const Run* runs, int nr, uint32_t i) {
+    int lo = 0, hi = nr;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (runs[mid].first <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint32_t run_value(const Run& r, const uint8_t* p, uint64_t n, uint32_t i, int bw) {
+    return r.packed ? bits_le(p, n, uint64_t(r.data) + uint64_t(i - r.first) * uint64_t(bw), bw) : r.data;
+}
+
+// Copy the chars of nv values (value v: coff[v] .. next start, from sbase + csrc[v]) to
+// obase[0 .. total): one 16-byte output chunk per thread step; interior chunks are one 16-byte
+// store, the two edge chunks (shared with neighbouring tiles) byte stores.
+__device__ inline void copy_chars(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
+                                  const uint8_t* sbase, uint8_t* obase) {
+    if (total == 0 || nv == 0) return;
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(obase);
+    const uintptr_t aend = a0 + total;
+    for (uintptr_t c = (a0 & ~uintptr_t(15)) + 16u * threadIdx.x; c < aend; c += 16u * blockDim.x) {
+        const int64_t r0 = int64_t(c) - int64_t(a0);
+        const uint32_t first = r0 < 0 ? 0u : uint32_t(r0);
+        int lo = 0, hi = int(nv);
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (coff[mid] <= first) lo = mid; else hi = mid;
+        }
+        uint32_t v = uint32_t(lo);
+        uint32_t vend = v + 1 < nv ? coff[v + 1] : total;
+        const uint8_t* sp = sbase + (int64_t(csrc[v]) - int64_t(coff[v]));
+        uint32_t word[4] = {0, 0, 0, 0};
+        #pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int64_t r = r0 + k;
+            if (r >= 0 && r < int64_t(total)) {
+                while (uint32_t(r) >= vend) {
+                    v++;
+                    vend = v + 1 < nv ? coff[v + 1] : total;
+                    sp = sbase + (int64_t(csrc[v]) - int64_t(coff[v]));
+                }
+                word[k >> 2] |= uint32_t(sp[r]) << (8 * (k & 3));
+            }
+        }
+        uint8_t* dst = reinterpret_cast<uint8_t*>(c);
+        if (r0 >= 0 && r0 + 16 <= int64_t(total)) {
+            *reinterpret_cast<uint4*>(dst) = make_uint4(word[0], word[1], word[2], word[3]);
+        } else {
+            #pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int64_t r = r0 + k;
+                if (r >= 0 && r < int64_t(total)) dst[k] = uint8_t(word[k >> 2] >> (8 * (k & 3)));
+            }
+        }
+    }
+}
+
+struct FlatLds {
+    Run drun[RUN_CAP];
+    Run vrun[RUN_CAP];
+    uint32_t coff[FT];
+    uint32_t csrc[FT];
+    uint32_t vbits[FT / 32 + 2];
+    uint32_t scan_tmp[NT / 64];
+    int ndrun, nvrun, dres, vres;
+    uint32_t dcover, vcover;
+};
+
+__global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                             const int* page_list, DevChunkResult* res) {
+    __shared__ FlatLds S;
+    const int pi = page_list[blockIdx.x];
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    const int tid = threadIdx.x;
+    if (res[pg.chunk].status != 0 || ck.max_rep != 0) return;
+    Sections s;
+    if (!page_sections(pg, ck, s)) return;                 // k_decode reports it
+    const int enc = pg.encoding;
+    const bool binary = ck.ptype == 6, boolean = ck.ptype == 0, dict = is_dict_enc(enc);
+    const int w = ck.width;
+    bool take = ck.max_def == 0 || s.def_rle;
+    if (enc == 0) {
+    } else if (dict) take = take && !boolean;
+    else if (enc == 5) take = take && (ck.ptype == 1 || ck.ptype == 2) && pg.aux != nullptr;
+    else take = false;
+    if (!take) return;
+
+    const int bwd = bit_width(ck.max_def);
+    const uint32_t ne = uint32_t(pg.num_values);
+    const int id_bw = (dict && s.val_n > 0) ? int(s.val[0]) : 0;
+    if (tid == 0) {
+        S.ndrun = 0; S.dcover = ne; S.dres = 0;
+        if (ck.max_def > 0) S.dres = walk_runs(s.def, s.def_n, bwd, ne, S.drun, RUN_CAP, S.ndrun, S.dcover);
+    } else if (tid == 64) {
+        S.nvrun = 0; S.vcover = 0; S.vres = 0;
+        if (dict && s.val_n > 0 && id_bw <= 32)
+            S.vres = walk_runs(s.val + 1, s.val_n - 1, id_bw, ne, S.vrun, RUN_CAP, S.nvrun, S.vcover);
+    }
+    __syncthreads();
+    if (S.dres == 2 || S.vres == 2) return;                // too many runs: k_decode takes the page
+    bool allp = true, lvl_bad = S.dres != 0;
+    for (int r = 0; r < S.ndrun; r++) {
+        const Run& R = S.drun[r];
+        if (R.packed || R.data != uint32_t(ck.max_def)) allp = false;
+        if (!R.packed && R.data > uint32_t(ck.max_def)) lvl_bad = true;
+    }
+    if (lvl_bad) {
+        if (tid == 0) { set_status(res, pg.chunk, ST_CORRUPT, pi); pg.done = 1; }
+        return;
+    }
+    const uint8_t* ids = dict && s.val_n > 0 ? s.val + 1 : s.val;
+    const uint64_t ids_n = dict && s.val_n > 0 ? s.val_n - 1 : 0;
+    const bool counted = ck.needs_count != 0;
+    const uint64_t slot_base = uint64_t(pg.entry_start);   // flat: slot == entry
+    uint64_t char_base = counted ? uint64_t(pg.char_start) : 0;
+    uint64_t vidx = 0;                                      // page-relative index of the next present value
+    int err = 0;
+
+    for (uint32_t e0 = 0; e0 < ne; e0 += FT) {
+        const uint32_t want = min(uint32_t(FT), ne - e0);
+        const uint32_t eb = uint32_t(tid) * FEPT;
+        for (uint32_t i = tid; i < FT / 32 + 2; i += NT) S.vbits[i] = 0;
+        // ---- definition levels -> present bits of this thread's entries
+        uint32_t fv = 0;
+        int bad = 0;
+        if (eb < want) {
+            const uint32_t m = min(uint32_t(FEPT), want - eb);
+            if (allp) {
+                fv = m >= 32 ? 0xffffffffu : (1u << m) - 1u;
+            } else {
+                const uint32_t e = e0 + eb;
+                int r = run_find(S.drun, S.ndrun, e);
+                for (uint32_t k = 0; k < m; k++) {
+                    while (e + k >= S.drun[r].first + S.drun[r].count) r++;
+                    const uint32_t d = run_value(S.drun[r], s.def, s.def_n, e + k, bwd);
+                    bad |= d > uint32_t(ck.max_def);
+                    fv |= uint32_t(d == uint32_t(ck.max_def)) << k;
+                }
+            }
+        }
+        uint32_t tv;
+        uint32_t vo;
+        if (allp) { vo = min(eb, want); tv = want; }
+        else vo = block_excl_scan<NT>(__popc(fv), S.scan_tmp, tv);
+        // ---- dictionary / stream checks that need the value count
+        if (tv > 0 && dict) {
+            if (id_bw > 32 || s.val_n == 0 || (binary ? ck.dict_pos == nullptr : ck.dict_data == nullptr) ||
+                vidx + tv > uint64_t(S.vcover))
+                bad = 1;
+        }
+        if (__syncthreads_or(bad)) { err = 1; break; }
+        // ---- values
+        uint32_t lsum = 0;
+        uint32_t my_src[FEPT], my_len[FEPT];   // indexed by entry k (static after unrolling)
+        {
+            uint32_t j = 0;
+            int vr = -1;
+            #pragma unroll
+            for (uint32_t k = 0; k < FEPT; k++) {
+                my_src[k] = 0;
+                my_len[k] = 0;
+                if (eb + k >= want) continue;
+                const uint64_t slot = slot_base + e0 + eb + k;
+                const bool present = (fv >> k) & 1u;
+                if (!binary) {
+                    uint8_t* dst = ck.values + slot * uint64_t(w);
+                    if (!present) { zero_value(dst, w); continue; }
+                    const uint64_t gv = vidx + vo + j++;
+                    if (dict) {
+                        if (vr < 0) vr = run_find(S.vrun, S.nvrun, uint32_t(gv));
+                        while (gv >= uint64_t(S.vrun[vr].first) + S.vrun[vr].count) vr++;
+                        const uint32_t id = run_value(S.vrun[vr], ids, ids_n, uint32_t(gv), id_bw);
+                        if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
+                        copy_value(dst, ck.dict_data + uint64_t(id) * uint64_t(w), w);
+                    } else if (boolean) {
+                        if ((gv >> 3) >= s.val_n) { bad = 1; continue; }
+                        dst[0] = uint8_t((s.val[gv >> 3] >> (gv & 7)) & 1u);
+                    } else if (enc == 0) {
+                        if ((gv + 1) * uint64_t(w) > s.val_n) { bad = 1; continue; }
+                        copy_value(dst, s.val + gv * uint64_t(w), w);
+                    } else {   // DELTA_BINARY_PACKED, decoded by k_delta into aux
+                        const uint64_t* dv = reinterpret_cast<const uint64_t*>(pg.aux);
+                        if (w == 8) *reinterpret_cast<uint64_t*>(dst) = dv[gv];
+                        else *reinterpret_cast<uint32_t*>(dst) = uint32_t(dv[gv]);
+                    }
+                } else if (present) {
+                    const uint64_t gv = vidx + vo + j;
+                    uint32_t src = 0, l = 0;
+                    if (dict) {
+                        if (vr < 0) vr = run_find(S.vrun, S.nvrun, uint32_t(gv));
+                        while (gv >= uint64_t(S.vrun[vr].first) + S.vrun[vr].count) vr++;
+                        const uint32_t id = run_value(S.vrun[vr], ids, ids_n, uint32_t(gv), id_bw);
+                        if (int64_t(id) >= ck.dict_n) bad = 1;
+                        else { src = ck.dict_pos[id]; l = ck.dict_len[id]; }
+                    } else {   // PLAIN: value positions from k_count's walk
+                        const uint32_t p = pg.aux[gv];
+                        const uint32_t ln = (p >= 4 && p <= s.val_n) ? ld32le(s.val, p - 4, s.val_n) : 0xffffffffu;
+                        if (ln <= s.val_n - p) { src = p; l = ln; }
+                        else bad = 1;
+                    }
+                    my_src[k] = src;
+                    my_len[k] = l;
+                    lsum += l;
+                    j++;
+                }
+            }
+        }
+        uint32_t tchars = 0;
+        const uint32_t lo = binary ? block_excl_scan<NT>(lsum, S.scan_tmp, tchars) : 0;
+        if (binary && char_base + tchars > uint64_t(pg.char_start + pg.n_chars)) bad = 1;   // k_count disagrees
+        if (__syncthreads_or(bad)) { err = 1; break; }
+        if (binary) {
+            uint32_t c = lo, j = 0;
+            #pragma unroll
+            for (uint32_t k = 0; k < FEPT; k++) {
+                if (eb + k >= want) continue;
+                if ((fv >> k) & 1u) {
+                    S.coff[vo + j] = c;
+                    S.csrc[vo + j] = my_src[k];
+                    c += my_len[k];
+                    j++;
+                }
+                ck.offsets[slot_base + e0 + eb + k + 1] = int32_t(char_base + c);
+            }
+        }
+        // validity bits of this thread's entries
+        if (ck.max_def > 0 && fv) {
+            const uint64_t abase = (slot_base + e0) & ~uint64_t(31);
+            const uint64_t rb = slot_base + e0 + eb - abase;
+            const uint32_t sh = uint32_t(rb & 31);
+            atomicOr(&S.vbits[rb >> 5], fv << sh);
+            if (sh + FEPT > 32 && sh) atomicOr(&S.vbits[(rb >> 5) + 1], fv >> (32 - sh));
+        }
+        __syncthreads();
+        if (binary) copy_chars(S.coff, S.csrc, tv, tchars, dict ? ck.dict_data : s.val, ck.chars + char_base);
+        if (ck.max_def > 0 && ck.validity) flush_bits(S.vbits, slot_base + e0, want, ck.validity);
+        vidx += tv;
+        char_base += tchars;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (err) set_status(res, pg.chunk, ST_CORRUPT, pi);
+        else if (!counted) atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values),
+                                     (unsigned long long)vidx);
+        pg.done = 1;
+    }
+}
+
 // ---- launchers -------------------------------------------------------------------------------
 void launch_dict_binary(DevChunk* d_chunks, const DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                         hipStream_t st) {
@@ -660,6 +1011,10 @@ void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list,
 void launch_scan(DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                  uint8_t* arena, uint64_t cap, unsigned long long* used, hipStream_t st) {
     if (n > 0) hipLaunchKernelGGL(k_scan, dim3(n), dim3(64), 0, st, d_chunks, d_pages, d_list, d_res, arena, cap, used);
+}
+void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
+                 hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res);
 }
 void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                    hipStream_t st) {

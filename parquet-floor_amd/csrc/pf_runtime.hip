@@ -28,6 +28,7 @@ void launch_dict_binary(DevChunk*, const DevPage*, const int*, int, DevChunkResu
 void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
+void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 }  // namespace pf
 
@@ -69,7 +70,7 @@ struct HostBuf {
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-constexpr int N_EVENTS = 8;   // h2d, snappy, dict, delta, count, scan, decode
+constexpr int N_EVENTS = 9;   // h2d, snappy, dict, delta, count, scan, flat, decode
 
 }  // namespace
 
@@ -87,7 +88,7 @@ struct pf_ctx {
     std::vector<DevChunk> chunks;          // host copies (device pointers)
     std::vector<DevPage> pages;
     std::vector<SnappyJob> jobs;
-    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_decode;
+    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode;
     std::vector<int2> wins, pieces;       // Snappy index windows / 64 KiB pieces (job, index)
     uint32_t n_splits = 0;
     SnapWin* d_win = nullptr;              // in d_tokmap: bitmap | lane outs | windows
@@ -144,6 +145,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     int* d_delta = lists + lo; lo += ctx->l_delta.size();
     int* d_count = lists + lo; lo += ctx->l_count.size();
     int* d_scan = lists + lo; lo += ctx->l_scan.size();
+    int* d_flat = lists + lo; lo += ctx->l_flat.size();
     int* d_decode = lists + lo; lo += ctx->l_decode.size();
     unsigned long long* used = reinterpret_cast<unsigned long long*>(meta + ctx->meta_bytes - 256);
     const int2* d_pieces = reinterpret_cast<const int2*>(meta + ctx->off_pieces);
@@ -165,8 +167,10 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], st));
-    launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), d_res, st);
+    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size()), d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], st));
+    launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), d_res, st);
+    HIPCHK(ctx, hipEventRecord(ctx->ev[8], st));
     HIPCHK(ctx, hipGetLastError());
     // results + device-written chunk fields (chars base) back to pinned host memory
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_res.p, meta + ctx->off_res, sizeof(DevChunkResult) * ctx->n_chunks,
@@ -216,7 +220,7 @@ int upload_meta(pf_ctx* ctx) {
     std::memcpy(h + ctx->off_wins, ctx->wins.data(), sizeof(int2) * ctx->wins.size());
     int* lists = reinterpret_cast<int*>(h + ctx->off_lists);
     size_t lo = 0;
-    for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_decode}) {
+    for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_flat, &ctx->l_decode}) {
         std::copy(v->begin(), v->end(), lists + lo);
         lo += v->size();
     }
@@ -295,7 +299,7 @@ int pf_host_free(pf_ctx* ctx, void* ptr) {
 int pf_device_alloc(pf_ctx* ctx, size_t bytes, void** out) {
     if (!ctx || !out) return fail(ctx, PF_ERR_INVALID_ARG, "null arg");
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    HIPCHK(ctx, hipMalloc(out, std::max<size_t>(bytes, 1)));
+    HIPCHK(ctx, hipMalloc(out, bytes + 256));   // slack: 16-byte staging loads may read past the end
     return PF_OK;
 }
 
@@ -320,7 +324,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->n_chunks = n_chunks;
     ctx->chunks.assign(n_chunks, DevChunk{});
     ctx->pages.clear(); ctx->jobs.clear();
-    ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_decode.clear();
+    ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_flat.clear(); ctx->l_decode.clear();
     ctx->wins.clear(); ctx->pieces.clear(); ctx->n_splits = 0;
     ctx->host_status.assign(n_chunks, 0);
     ctx->info.assign(n_chunks, pf_column_info{});
@@ -499,6 +503,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         const DevChunk& ck = ctx->chunks[pg.chunk];
         if (pg.encoding == PF_ENC_DELTA_BINARY_PACKED && pg.aux && ck.ptype != PF_BYTE_ARRAY) ctx->l_delta.push_back(int(i));
         if (ck.needs_count) ctx->l_count.push_back(int(i));
+        if (ck.max_rep == 0) ctx->l_flat.push_back(int(i));
         ctx->l_decode.push_back(int(i));
     }
     // ---- Snappy tables: 8 KiB index windows, 64 KiB pieces ----
@@ -512,7 +517,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_pages = take(m, sizeof(DevPage) * ctx->pages.size());
     ctx->off_jobs = take(m, sizeof(SnappyJob) * ctx->jobs.size());
     ctx->off_lists = take(m, sizeof(int) * (ctx->l_dictbin.size() + ctx->l_delta.size() + ctx->l_count.size() +
-                                            ctx->l_scan.size() + ctx->l_decode.size()));
+                                            ctx->l_scan.size() + ctx->l_flat.size() + ctx->l_decode.size()));
     ctx->off_res = take(m, sizeof(DevChunkResult) * n_chunks);
     ctx->off_pieces = take(m, sizeof(int2) * ctx->pieces.size());
     ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);

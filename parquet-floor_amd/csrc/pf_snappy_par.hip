@@ -223,7 +223,7 @@ extern "C" int pf_debug_trace(uint32_t* out, int n, int reset) {
 
 constexpr int FIX_MAXW = 1024;       // pages up to 8 MiB compressed (larger: serial fallback)
 constexpr int MERGE_STEPS = 64;      // true-chain steps before a window is re-parsed instead
-constexpr int FIX_ROUNDS = 32;
+constexpr int FIX_ROUNDS = 256;
 
 __device__ __forceinline__ bool tm_get(const uint32_t* tm, uint32_t i) { return (tm[i >> 5] >> (i & 31u)) & 1u; }
 __device__ __forceinline__ void tm_set(uint32_t* tm, uint32_t i) { tm[i >> 5] |= 1u << (i & 31u); }
@@ -289,6 +289,9 @@ __global__ __launch_bounds__(64) void k_snappy_fix(const SnappyJob* __restrict__
             uint32_t* lo = LO + size_t(w) * 64;
             const uint32_t c = s_c[w], x0 = s_x[w], fl = s_fl[w];
             const bool pass = fl & WIN_PASS;
+            // entry not known yet (an earlier window's exit is being re-derived this round): keep
+            // this window's index results untouched for the next round
+            if (e == SNAP_INVALID) continue;
             if (e >= wend) {   // jumped over by a literal: no token starts in this window
                 if (!pass || c != e) {
                     for (int q = 0; q < 64; q++) { reinterpret_cast<uint4*>(tm)[q] = make_uint4(0, 0, 0, 0); lo[q] = 0; }
@@ -306,8 +309,10 @@ __global__ __launch_bounds__(64) void k_snappy_fix(const SnappyJob* __restrict__
                 q += t.tl;
             } else {   // walk the true chain from e until it meets the window's chain
                 int steps = 0;
+                // a broken guessed chain has no trustworthy exit: never merge into it
+                const bool nomerge = pass || (fl & WIN_BROKEN);
                 while (q < wend && steps < MERGE_STEPS) {
-                    if (!pass && tm_get(tm, uint32_t(q) - W0)) { merged = true; break; }
+                    if (!nomerge && tm_get(tm, uint32_t(q) - W0)) { merged = true; break; }
                     const SnapTok t = snap_tok(glb_read8(job.src, n, q));
                     acc += t.ol;
                     q += t.tl;
@@ -453,6 +458,77 @@ constexpr uint32_t XSTAGE = XCHUNK + 64 + 16;
 
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Batch-parallel executor step limits. A batch writes at most XPAR_OUT bytes into the ring, so
+// with op - F < XSLOT at its start, a copy reaching back <= XNEAR still finds its source in the
+// ring and any longer copy reads output flushed >= 2 KiB earlier.
+constexpr uint32_t XPAR_OUT = 2048;
+constexpr uint32_t XPAR_TOK = 64;
+constexpr uint32_t XNEAR = XRING - XPAR_OUT;
+
+// Number of lanes whose key is < x; keys ascend over the lanes (all 64 lanes must call).
+__device__ __forceinline__ uint32_t lanes_below(uint32_t key, uint32_t x) {
+    uint32_t idx = 0;
+    #pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const uint32_t kv = __shfl(key, int(idx) + s - 1, 64);
+        if (kv < x) idx += uint32_t(s);
+    }
+    const uint32_t k63 = __shfl(key, 63, 64);
+    return (idx == 63 && k63 < x) ? 64u : idx;
+}
+
+__device__ __forceinline__ uint64_t lane_mask_lt(uint32_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }
+
+// One batch-parallel executor step (all 64 lanes; lane t holds token t of the sub-batch: `take`,
+// kind, output length ol, literal source position or copy offset, output position otok).
+// Literals are independent and go first; copies then run in dependency rounds: a copy runs once
+// no pending copy of the batch writes a byte it reads ([a, b); for offset < length only the
+// first `off` bytes before it). Returns false on a copy reaching before the piece.
+__device__ __forceinline__ bool par_step(uint8_t* ring, const uint8_t* stage, uint8_t* dst, uint32_t woff, uint32_t I,
+                                         uint32_t out_start, uint32_t op, uint32_t& F, bool take, uint32_t kd,
+                                         uint32_t ol, uint32_t srcv, uint32_t off, uint32_t otok, uint32_t btot,
+                                         int lane) {
+    wait_vmem();   // flushed output is visible to far copies
+    if (take && kd == 0) {
+        const uint32_t sb = woff + (srcv - I);
+        for (uint32_t j = 0; j < ol; j++) ring[(otok + j) & XRMASK] = stage[sb + j];
+    }
+    __syncthreads();
+    const bool cp = take && kd != 0;
+    if (__any(cp && (off == 0 || off > otok - out_start))) return false;
+    const uint32_t a = otok - off;
+    const uint32_t b = a + min(ol, off);
+    const uint32_t kb = lanes_below(take ? otok : 0xffffffffu, b);            // outputs starting before b
+    const uint32_t ka = lanes_below(take ? otok + ol : 0xffffffffu, a + 1);  // outputs ending by a
+    const uint64_t dep = (cp && kb > ka) ? (lane_mask_lt(kb) & ~lane_mask_lt(ka)) : 0ull;
+    uint64_t pend = __ballot(cp);
+    while (pend) {
+        const bool ready = cp && ((pend >> lane) & 1ull) && (dep & pend) == 0ull;
+        if (ready) {
+            const bool near = off <= XNEAR;
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < ol; j++) {
+                const uint32_t s = a + r;
+                const uint8_t v = near ? ring[s & XRMASK] : dst[s];   // far: flushed >= 2 KiB ago
+                ring[(otok + j) & XRMASK] = v;
+                r = r + 1 == off ? 0u : r + 1;
+            }
+        }
+        pend &= ~__ballot(ready);
+        __syncthreads();
+    }
+    const uint32_t upto = op + btot;
+    while (upto - F >= XSLOT) {
+        const uint32_t a0 = F + uint32_t(lane) * 32u;
+        const uint4 v0 = *reinterpret_cast<const uint4*>(ring + (a0 & XRMASK));
+        const uint4 v1 = *reinterpret_cast<const uint4*>(ring + ((a0 + 16u) & XRMASK));
+        *reinterpret_cast<uint4*>(dst + a0) = v0;
+        *reinterpret_cast<uint4*>(dst + a0 + 16) = v1;
+        F += XSLOT;
+    }
+    return true;
+}
+
 __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
                                                     const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[XRING];
@@ -552,6 +628,20 @@ __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict_
             TRACE(0xBBBB0000u | uint32_t(k), I, ip, T, sb, uint32_t(nt), op, F);
             const uint32_t srcv = tk.kind == 0 ? uint32_t(start) + tk.arg : tk.arg;
             const uint32_t kd = tk.kind;
+            const uint32_t btot = __builtin_amdgcn_readlane(inc, nt - 1);
+            const bool lit = take && kd == 0;
+            // Batch-parallel step: every token of the sub-batch at once, one lane per token. Taken
+            // when the batch is short (no token > XPAR_TOK bytes, <= XPAR_OUT bytes in all) and
+            // every literal is staged; otherwise the token-serial step below.
+            const bool par = btot <= XPAR_OUT &&
+                             !__any(take && (ol > XPAR_TOK ||
+                                             (lit && uint64_t(srcv) + ol > uint64_t(I) + XCHUNK + 64)));
+            if (par) {
+                if (!par_step(ring, stage, dst, woff, I, out_start, op, F, take, kd, ol, srcv, tk.arg, otok, btot, lane)) {
+                    bad = true;
+                    break;
+                }
+            } else
             for (int i = 0; i < nt; i++) {
                 const uint32_t k_i = __builtin_amdgcn_readlane(kd, i);
                 const uint32_t l_i = __builtin_amdgcn_readlane(ol, i);

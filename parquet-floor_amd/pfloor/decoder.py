@@ -195,10 +195,10 @@ class GpuDecoder:
         return dst[:out_len.value].tobytes(), L.pf_snappy_last_fallback(self.h)
 
     def timing(self):
-        buf = (C.c_float * 8)()
+        buf = (C.c_float * 16)()
         n = C.c_int()
-        check(lib().pf_last_timing(self.h, buf, 8, C.byref(n)), self.h, "pf_last_timing")
-        names = ["h2d", "snappy", "dict", "delta", "count", "scan", "decode"]
+        check(lib().pf_last_timing(self.h, buf, 16, C.byref(n)), self.h, "pf_last_timing")
+        names = ["h2d", "snappy", "dict", "delta", "count", "scan", "flat", "decode"]
         return dict(zip(names, list(buf)[:n.value]))
 
     def fetch(self, i, physical_type, max_def, max_rep):

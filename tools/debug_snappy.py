@@ -18,11 +18,30 @@ import test_gpu_snappy as T  # noqa: E402
 def main():
     seed, name = int(sys.argv[1]), sys.argv[2]
     o = Oracle(os.path.join(ROOT, "oracle", "libpf_oracle.so"))
-    if name.startswith("boundary"):
+    comp = None
+    if name.startswith("page:"):   # page:<column>:<page index> of a lineitem-shaped file (seed = rows)
+        import pyarrow.parquet as pq
+        from pfloor import datagen
+        from pfloor.decoder import ParquetFile
+        _, col, pidx = name.split(":")
+        path = f"/tmp/probe_lineitem_{seed}.parquet"
+        if not os.path.exists(path):
+            pq.write_table(datagen.lineitem_table(seed, seed=42), path, compression="snappy", row_group_size=1 << 20)
+        with ParquetFile(path) as pf:
+            c = [i for i, cc in enumerate(pf.columns) if cc.path[0] == col][0]
+            st, nn = pf.chunk_range(0, c)
+            buf = np.zeros(nn, np.uint8)
+            pf.read_into(st, nn, buf.ctypes.data)
+            d = pf.chunk_desc(0, c, 0)
+            pg = d.pages[int(pidx)]
+            comp = buf[pg.offset:pg.offset + pg.compressed_size].tobytes()
+        data = o.snappy_uncompress(comp)
+    elif name.startswith("boundary"):
         data = dict(T._boundary_streams(seed))[int(name.split(":")[1])]
     else:
         data = T._payloads(np.random.default_rng(seed))[name]
-    comp = o.snappy_compress(data, mode=0)
+    if comp is None:
+        comp = o.snappy_compress(data, mode=0)
     dec = GpuDecoder(0)
     L = _native.lib()
     trace = getattr(L, "pf_debug_trace", None) if os.environ.get("PFLOOR_LIB_PATH") else None

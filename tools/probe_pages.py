@@ -29,7 +29,7 @@ if stamps:
     stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
 sbuf = (C.c_ulonglong * 16)()
 sacc = collections.defaultdict(lambda: np.zeros(16))
-stats = collections.defaultdict(lambda: [0, 0, 0.0, 0, 0])
+stats = collections.defaultdict(lambda: [0, collections.Counter(), 0.0, 0, 0, 0])
 with ParquetFile(path) as pf:
     for col in range(pf.num_columns):
         s, n = pf.chunk_range(0, col)
@@ -51,12 +51,13 @@ with ParquetFile(path) as pf:
             ref = o.snappy_uncompress(body)
             st = stats[(pf.columns[col].path[0], kind)]
             st[0] += 1
-            st[1] += int(fb == 1)
+            st[1][fb] += 1
+            st[5] = max(st[5], len(body))
             st[2] += dt
             st[3] += len(body)
             st[4] += int(got != ref)
 for k, v in sorted(stats.items()):
-    line = (f"{k[0]:16s} {k[1]:8s} pages {v[0]:4d} fallback {v[1]:4d} mismatch {v[4]} in {v[3] / 1e6:7.2f} MB "
+    line = (f"{k[0]:16s} {k[1]:8s} pages {v[0]:4d} paths {dict(v[1])} maxpage {v[5]} mismatch {v[4]} in {v[3] / 1e6:7.2f} MB "
             f"avg {v[2] / v[0] * 1e3:7.3f} ms")
     if stamps and v[3] > 200000:
         s = sacc[k]
