@@ -23,6 +23,21 @@
 namespace pf {
 
 constexpr int NT = 256;
+
+#ifdef PF_STAMPS
+__device__ unsigned long long pf_pstamps[16];
+#define PSTAMP(i, v) atomicAdd(&pf_pstamps[i], (unsigned long long)(v))
+extern "C" int pf_debug_pstamps(unsigned long long* out, int n, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_pstamps), sizeof(unsigned long long) * (n < 16 ? n : 16)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(pf_pstamps), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#else
+#define PSTAMP(i, v) ((void)0)
+#endif
 constexpr int TILE = 1024;
 constexpr int EPT = TILE / NT;   // entries per thread per tile (4 consecutive)
 
@@ -161,10 +176,10 @@ __device__ inline int64_t plain_binary_walk(const uint8_t* p, uint64_t n, int64_
 // stream end). Inside text (or most payloads) only the true prefixes pass both tests: the second
 // one drops the candidates text produces just before each true prefix (the previous value's last
 // byte + the low bytes of the next length). Every thread tests BW_BPT positions of a tile staged
-// in LDS; plausible positions are emitted in order (block scan) and each must be its
-// predecessor's successor (q_next == q + 4 + len), the first at 0. Any mismatch — a false
-// candidate, overflow, too few candidates — falls back to the exact serial walk, so the result is
-// always the chain parquet-mr's BinaryPlainValuesReader reads.
+// in LDS; the true chain is then the tile's entry plus the candidates that are another
+// candidate's successor, and it must chain exactly (q_next == q + 4 + len) from the entry. Any
+// mismatch — a false candidate that got linked, overflow, too few values — falls back to the exact
+// serial walk, so the result is always the chain parquet-mr's BinaryPlainValuesReader reads.
 constexpr int BW_BPT = 16;                          // positions per thread per tile
 constexpr int BW_TILE = NT * BW_BPT;                // bytes per tile
 constexpr int BW_LOOK = 64;                         // staged lookahead for successor tests
@@ -175,6 +190,9 @@ struct BinWalkLds {
     __attribute__((aligned(16))) uint8_t stage[BW_STAGE];
     uint32_t cand[BW_CAP];
     uint32_t next[BW_CAP];
+    uint8_t linked[BW_CAP];    // candidate is another candidate's successor
+    uint32_t acand[BW_CAP];    // accepted chain, in order
+    uint32_t anext[BW_CAP];
     uint32_t scan[NT / 64];
     unsigned long long chars;
     uint32_t found, carry, bad;
@@ -204,6 +222,13 @@ __device__ __forceinline__ uint32_t wg_stage(uint8_t* stage, const uint8_t* p, u
     return woff;
 }
 
+// The walk over candidates inside a tile: the true chain is the tile's entry E plus every
+// candidate that is the successor of another candidate (a true value's successor is the next true
+// value; a false candidate's successor is a random far position, so false candidates are almost
+// never linked). The accepted list must still chain exactly from E and leave the tile; a false
+// candidate that does get linked breaks that check and the page takes the serial walk.
+constexpr int BW_CPT = BW_CAP / NT;                 // candidates owned by a thread (contiguous)
+
 __device__ inline int64_t binary_walk_wg(const uint8_t* p, uint64_t n, int64_t count, uint32_t* pos, uint32_t* len,
                                          BinWalkLds& W) {
     const int tid = threadIdx.x;
@@ -211,17 +236,32 @@ __device__ inline int64_t binary_walk_wg(const uint8_t* p, uint64_t n, int64_t c
     __syncthreads();
     if (count == 0) return 0;
     if (n > 0x7fffffffull) return -1;
+#ifdef PF_STAMPS
+    const unsigned long long t_beg = __builtin_amdgcn_s_memtime();
+    if (tid == 0) PSTAMP(0, 1);
+#endif
     for (uint64_t t0 = 0; t0 < n; t0 += BW_TILE) {
         if (W.found >= uint64_t(count) || W.bad) break;
+        const uint32_t E = W.carry;                 // true chain position entering this tile
+        const uint64_t tend = min(t0 + BW_TILE, n);
+        if (E >= tend) continue;                    // one value spans the whole tile
+#ifdef PF_STAMPS
+        unsigned long long t_ph = __builtin_amdgcn_s_memtime();
+#endif
         const uint32_t woff = wg_stage(W.stage, p, n, t0, BW_STAGE);
+        for (uint32_t i = tid; i < BW_CAP / 4; i += NT) reinterpret_cast<uint32_t*>(W.linked)[i] = 0;
         __syncthreads();
+#ifdef PF_STAMPS
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) PSTAMP(9, t_ - t_ph); t_ph = t_; }
+#endif
+
         const uint64_t b0 = t0 + uint64_t(tid) * BW_BPT;
         uint32_t flags = 0, L[BW_BPT];
         #pragma unroll
         for (int i = 0; i < BW_BPT; i++) {
             const uint64_t q = b0 + i;
             L[i] = 0;
-            if (q + 4 <= n) {
+            if (q + 4 <= n && q >= E) {
                 const uint32_t l = lds_read4(W.stage, woff + uint32_t(q - t0));
                 if (uint64_t(l) <= n - q - 4) {
                     const uint64_t s = q + 4 + l;
@@ -237,48 +277,101 @@ __device__ inline int64_t binary_walk_wg(const uint8_t* p, uint64_t n, int64_t c
         }
         uint32_t tot;
         uint32_t idx = block_excl_scan<NT>(__popc(flags), W.scan, tot);
-        if (tot > BW_CAP) { if (tid == 0) W.bad = 1; __syncthreads(); break; }
-        const uint32_t base = W.found;
-        uint64_t my_chars = 0;
+#ifdef PF_STAMPS
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) PSTAMP(10, t_ - t_ph); t_ph = t_; }
+#endif
+
+        if (tot > BW_CAP || tot == 0) { if (tid == 0) { W.bad = 1; PSTAMP(5, 1); } __syncthreads(); break; }
+#ifdef PF_STAMPS
+        if (tid == 0) PSTAMP(1, 1);
+#endif
         #pragma unroll
         for (int i = 0; i < BW_BPT; i++) {
             if ((flags >> i) & 1u) {
                 const uint32_t q = uint32_t(b0 + i);
                 W.cand[idx] = q;
                 W.next[idx] = q + 4 + L[i];
-                const uint64_t k = uint64_t(base) + idx;
-                if (k < uint64_t(count)) {
-                    pos[k] = q + 4;
-                    if (len) len[k] = L[i];
-                    my_chars += L[i];
-                }
                 idx++;
             }
         }
         __syncthreads();
-        // chain check: candidate i's successor is candidate i+1 (across tiles via `carry`)
-        int bad = 0;
+        // link: mark every candidate that is another candidate's successor
         for (uint32_t i = tid; i < tot; i += NT) {
-            const uint64_t k = uint64_t(base) + i;
-            if (k >= uint64_t(count)) continue;
-            const uint32_t expect = i == 0 ? (base == 0 ? 0u : W.carry) : W.next[i - 1];
-            bad |= W.cand[i] != expect;
+            const uint32_t s = W.next[i];
+            if (s >= tend) continue;
+            uint32_t lo = i + 1, hi = tot;   // successors lie at higher indices
+            while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (W.cand[m] < s) lo = m + 1; else hi = m; }
+            if (lo < tot && W.cand[lo] == s) W.linked[lo] = 1;
         }
+        __syncthreads();
+#ifdef PF_STAMPS
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) PSTAMP(11, t_ - t_ph); t_ph = t_; }
+#endif
+
+        // accepted = the entry + linked candidates, ranked in position order over contiguous ranges
+        const uint32_t i0 = uint32_t(tid) * BW_CPT;
+        uint32_t am = 0;
+        #pragma unroll
+        for (int k = 0; k < BW_CPT; k++) {
+            const uint32_t i = i0 + k;
+            am |= uint32_t(i < tot && (W.linked[i] || W.cand[i] == E)) << k;
+        }
+        uint32_t atot;
+        uint32_t r = block_excl_scan<NT>(__popc(am), W.scan, atot);
+        const uint32_t base = W.found;
+        uint64_t my_chars = 0;
+        #pragma unroll
+        for (int k = 0; k < BW_CPT; k++) {
+            if (!((am >> k) & 1u)) continue;
+            const uint32_t q = W.cand[i0 + k], s = W.next[i0 + k];
+            W.acand[r] = q;
+            W.anext[r] = s;
+            const uint64_t kk = uint64_t(base) + r;
+            if (kk < uint64_t(count)) {
+                pos[kk] = q + 4;
+                if (len) len[kk] = s - q - 4;
+                my_chars += s - q - 4;
+            }
+            r++;
+        }
+        __syncthreads();
+#ifdef PF_STAMPS
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) PSTAMP(12, t_ - t_ph); t_ph = t_; }
+#endif
+
+        // the accepted list chains exactly from E and its last value leaves the tile
+        int bad = 0;
+        for (uint32_t a = tid; a < atot; a += NT) {
+            if (uint64_t(base) + a >= uint64_t(count)) continue;
+            bad |= W.acand[a] != (a == 0 ? E : W.anext[a - 1]);
+        }
+        if (tid == 0 && (atot == 0 || (W.anext[atot - 1] < tend && uint64_t(base) + atot < uint64_t(count)))) bad = 1;
         if (my_chars) atomicAdd(&W.chars, (unsigned long long)my_chars);
         bad = __syncthreads_or(bad);
         if (tid == 0) {
-            if (bad) W.bad = 1;
-            if (tot) W.carry = W.next[tot - 1];
-            W.found = base + tot;
+            if (bad) { W.bad = 1; PSTAMP(7, 1); }
+            else W.carry = W.anext[atot - 1];
+            W.found = base + atot;
         }
         __syncthreads();
+#ifdef PF_STAMPS
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) PSTAMP(13, t_ - t_ph); t_ph = t_; }
+#endif
+
     }
     __syncthreads();
+#ifdef PF_STAMPS
+    const unsigned long long t_mid = __builtin_amdgcn_s_memtime();
+    if (tid == 0) PSTAMP(3, t_mid - t_beg);
+#endif
     if (!W.bad && W.found >= uint64_t(count)) return int64_t(W.chars);
-    // exact serial fallback (false candidates in binary payloads, or corrupt pages)
+    // exact serial fallback (candidates the filters could not separate, or corrupt pages)
     __shared__ long long s_res;
     if (tid == 0) s_res = plain_binary_walk(p, n, count, pos, len);
     __syncthreads();
+#ifdef PF_STAMPS
+    if (tid == 0) { PSTAMP(2, 1); PSTAMP(4, __builtin_amdgcn_s_memtime() - t_mid); if (!W.bad) PSTAMP(8, 1); }
+#endif
     return s_res;
 }
 

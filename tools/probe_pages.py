@@ -44,6 +44,7 @@ with ParquetFile(path) as pf:
                 stamps(sbuf, 16, 1)
             t0 = time.perf_counter()
             got, fb = dec.snappy_decompress(body)
+            print('PAGE', pf.columns[col].path[0], kind, len(body), flush=True)
             dt = time.perf_counter() - t0
             if stamps:
                 stamps(sbuf, 16, 1)
@@ -59,10 +60,8 @@ with ParquetFile(path) as pf:
 for k, v in sorted(stats.items()):
     line = (f"{k[0]:16s} {k[1]:8s} pages {v[0]:4d} paths {dict(v[1])} maxpage {v[5]} mismatch {v[4]} in {v[3] / 1e6:7.2f} MB "
             f"avg {v[2] / v[0] * 1e3:7.3f} ms")
-    if stamps and v[3] > 200000:
-        s = sacc[k]
-        w = max(s[8], 1)
-        line += (f" | parse-windows {s[8]:.0f} lanes/win {s[9] / w:.1f} rounds/win {s[10] / w:.1f} "
-                 f"exec cyc p0..4 " + " ".join(f"{s[i] / 1e6:.1f}M" for i in range(5)) +
-                 " idx cyc p5..7 " + " ".join(f"{s[i] / 1e6:.1f}M" for i in range(5, 8)))
+    if stamps:
+        s = sacc[k] / max(v[0], 1)
+        line += " | fix/page: rounds %.1f steps %.0f reparse %.1f cyc total %.0fk lane0 %.0fk par %.0fk rep %.0fk splits %.0fk" % (
+            s[0], s[1], s[2], s[3] / 1e3, s[6] / 1e3, s[7] / 1e3, s[8] / 1e3, s[9] / 1e3)
     print(line, flush=True)
