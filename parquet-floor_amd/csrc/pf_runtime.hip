@@ -22,8 +22,8 @@
 #include "pfloor.h"
 
 namespace pf {
-void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, uint32_t*, const int2*, int, uint32_t*, int*,
-                   DevChunkResult*, hipStream_t);
+void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, const int2*, int, uint32_t*,
+                   int*, DevChunkResult*, hipStream_t);
 void launch_dict_binary(DevChunk*, const DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
@@ -91,7 +91,8 @@ struct pf_ctx {
     std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode;
     std::vector<int2> wins, pieces;       // Snappy index windows / 64 KiB pieces (job, index)
     uint32_t n_splits = 0;
-    SnapWin* d_win = nullptr;              // in d_tokmap: bitmap | lane outs | windows
+    SnapWin* d_win = nullptr;              // in d_tokmap: bitmap | lane outs | windows | entry tables
+    SnapEnt* d_ent = nullptr;
     const uint32_t* d_last_splits = nullptr;   // diagnostics: last pf_snappy_decompress tables
     uint32_t* d_lane_out = nullptr;
     std::vector<int64_t> host_status;      // per chunk host-side planning errors
@@ -155,7 +156,7 @@ int enqueue_kernels(pf_ctx* ctx) {
 
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
-    launch_snappy(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_lane_out, d_pieces,
+    launch_snappy(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent, ctx->d_lane_out, d_pieces,
                   int(ctx->pieces.size()), d_splits, d_fallback, d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
     launch_dict_binary(d_chunks, d_pages, d_dictbin, int(ctx->l_dictbin.size()), d_res, st);
@@ -200,10 +201,12 @@ int plan_snappy(pf_ctx* ctx) {
         for (uint32_t k = 0; k < jb.n_pieces; k++) ctx->pieces.push_back(int2{int(j), int(k)});
     }
     const size_t tok_bytes = size_t(n_win) * SNAP_WWORDS * 4, lo_bytes = size_t(n_win) * 64 * 4;
-    HIPCHK(ctx, ctx->d_tokmap.ensure(tok_bytes + lo_bytes + size_t(n_win) * sizeof(SnapWin) + 256));
+    const size_t win_bytes = align_up(size_t(n_win) * sizeof(SnapWin), 256), ent_bytes = size_t(n_win) * 64 * sizeof(SnapEnt);
+    HIPCHK(ctx, ctx->d_tokmap.ensure(tok_bytes + lo_bytes + win_bytes + ent_bytes + 256));
     uint8_t* base = static_cast<uint8_t*>(ctx->d_tokmap.p);
     ctx->d_lane_out = reinterpret_cast<uint32_t*>(base + tok_bytes);
     ctx->d_win = reinterpret_cast<SnapWin*>(base + tok_bytes + lo_bytes);
+    ctx->d_ent = reinterpret_cast<SnapEnt*>(base + tok_bytes + lo_bytes + win_bytes);
     for (SnappyJob& jb : ctx->jobs) jb.tokmap = reinterpret_cast<uint32_t*>(base) + size_t(jb.win_base) * SNAP_WWORDS;
     return PF_OK;
 }
@@ -679,7 +682,7 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     HIPCHK(ctx, hipMemcpyAsync(d, h, m, hipMemcpyHostToDevice, st));
     ctx->d_last_splits = reinterpret_cast<const uint32_t*>(d + o_sp);
     launch_snappy(reinterpret_cast<const SnappyJob*>(d + o_job), 1, reinterpret_cast<const int2*>(d + o_wn),
-                  int(ctx->wins.size()), ctx->d_win, ctx->d_lane_out, reinterpret_cast<const int2*>(d + o_pc),
+                  int(ctx->wins.size()), ctx->d_win, ctx->d_ent, ctx->d_lane_out, reinterpret_cast<const int2*>(d + o_pc),
                   int(ctx->pieces.size()), reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb),
                   reinterpret_cast<DevChunkResult*>(d + o_res), st);
     HIPCHK(ctx, hipGetLastError());

@@ -12,7 +12,7 @@ namespace pf {
 
 constexpr uint32_t SNAP_RB = 128;                 // input bytes per lane region (index pass)
 constexpr uint32_t SNAP_WIN = 64 * SNAP_RB;       // 8 KiB of input per index window
-constexpr uint32_t SNAP_WSTAGE = SNAP_WIN + 80;   // staged window: + alignment shift (< 16) + header slack
+constexpr uint32_t SNAP_WSTAGE = SNAP_WIN + 96;   // staged window: + alignment shift (< 16) + 64-lane lookahead
 constexpr uint32_t SNAP_WWORDS = SNAP_WIN / 32;   // token-start bitmap words per window
 constexpr uint32_t SNAP_INVALID = 0xffffffffu;
 constexpr uint32_t SNAP_BLOCK = 65536;            // Google Snappy block = executor piece
@@ -20,7 +20,9 @@ constexpr uint32_t SNAP_BLOCK = 65536;            // Google Snappy block = execu
 // per-job decode path (SnappyJob fallback flags, ordered: atomicMax escalates)
 enum : int { FB_OK = 0, FB_WHOLE = 1, FB_REDO = 2, FB_SERIAL = 3 };
 // SnapWin.flags
-enum : uint32_t { WIN_BROKEN = 1, WIN_PASS = 2 };
+enum : uint32_t { WIN_BROKEN = 1, WIN_PASS = 2, WIN_NOCONV = 4 };
+// SnapWin.flags after the chain pass: how the window's bitmap relates to the true chain
+enum : uint32_t { WM_KEEP = 16, WM_SKIP = 17, WM_MERGE = 18, WM_FULL = 19, WM_DONE = 20 };
 
 // Result of the index pass for one 8 KiB input window.
 struct SnapWin {
@@ -28,6 +30,12 @@ struct SnapWin {
     uint32_t exit;    // first chain position at/after the window end (or the stream end)
     uint32_t out;     // output bytes of the tokens in the window (on that chain)
     uint32_t flags;
+};
+
+// Entry-table record (pos carries a 2-bit flag in its top bits).
+struct SnapEnt {
+    uint32_t pos;
+    uint32_t out;
 };
 
 struct SnapTok {

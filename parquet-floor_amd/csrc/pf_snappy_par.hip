@@ -14,12 +14,14 @@
 //                   lane to lane from the window entry; a lane whose true entry is not on its
 //                   guessed chain re-walks from it, until the chain is consistent (each round
 //                   fixes at least the first wrong lane). Output: the token-start bitmap (1 bit per
-//                   input byte), per-lane output byte counts, the window exit.
-//   k_snappy_fix    one wave per page. Window w's true entry is window w-1's exit; every window
-//                   walks the true chain from there until it meets its own (guessed) chain —
-//                   usually within a few tokens — and patches the bitmap; windows where they never
-//                   meet are re-parsed. Iterates until no exit changes, checks the totals, then
-//                   finds the input position of the token at each 64 KiB output boundary.
+//                   input byte), per-lane output byte counts, the window exit, and an entry
+//                   table: for each entry d < 64 bytes into the window, where the chain from
+//                   W0 + d meets the window's chain and the output difference up to there.
+//   k_snappy_chain  one wave per page. Window w's true entry is window w-1's exit: one table
+//                   lookup per window (a walk in HBM for entries deeper than 64 bytes, a whole-
+//                   wave re-parse for unresolved windows). Lanes then repair the bitmap in front
+//                   of the merge points, the totals are checked and the input position of the
+//                   token at each 64 KiB output boundary is found.
 //   k_snappy_exec   one wave per 64 KiB piece: tokens come from the bitmap 1 KiB of input at a
 //                   time (parsed 64 at a time, one per lane), then execute in order — each token
 //                   is one 64-lane read-then-write step in an 8 KiB LDS ring (copies with larger
@@ -36,8 +38,12 @@ namespace pf {
 #ifdef PF_STAMPS
 __device__ unsigned long long pf_stamps[16];
 #define STAMP_ADD(i, v) atomicAdd(&pf_stamps[i], (unsigned long long)(v))
+#define XT_DECL unsigned long long xt_ = __builtin_amdgcn_s_memtime()
+#define XT(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (lane == 0) STAMP_ADD(i, t_ - xt_); xt_ = t_; } while (0)
 #else
 #define STAMP_ADD(i, v) ((void)0)
+#define XT_DECL ((void)0)
+#define XT(i) ((void)0)
 #endif
 
 // ======================================================================== index pass
@@ -68,6 +74,8 @@ __device__ __forceinline__ bool bit_get(const WinLane& L, uint32_t i) {
     const uint32_t v = w == 0 ? L.b0 : (w == 1 ? L.b1 : (w == 2 ? L.b2 : L.b3));
     return (v >> (i & 31u)) & 1u;
 }
+
+constexpr int WIN_ROUNDS = 8;        // lane-region fixed-point rounds before the exact whole-wave parse
 
 // Walk the chain from c while positions stay below re (bits relative to rs).
 __device__ void lane_walk(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t rs, uint32_t re,
@@ -104,7 +112,7 @@ __device__ uint32_t win_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, 
     uint32_t ent = SNAP_INVALID, X = SNAP_INVALID;
     bool converged = false;
     flags = 0;
-    for (int round = 0; round <= 64; round++) {
+    for (int round = 0; round < WIN_ROUNDS; round++) {
         // follow the chain lane to lane (uniform scalar loop)
         ent = SNAP_INVALID;
         flags = 0;
@@ -122,7 +130,7 @@ __device__ uint32_t win_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, 
         if (!__any(need)) { converged = true; break; }
         if (need) lane_walk(stage, woff, W0, n, rs, re, ent, L);
     }
-    if (!converged) flags = WIN_BROKEN;
+    if (!converged) flags = WIN_NOCONV;
     // lanes off the chain hold no tokens; drop the guessed prefix before a lane's true entry
     if (ent == SNAP_INVALID) {
         L.b0 = L.b1 = L.b2 = L.b3 = 0;
@@ -140,11 +148,90 @@ __device__ uint32_t win_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, 
     return X;
 }
 
+// Entry table (index pass -> chain pass): for an entry e = W0 + d, d < 64, where the chain from e
+// meets the window's own chain (bitmap) and the output difference up to that point.
+constexpr int ENT_STEPS = 384;       // longer walks are left to the chain pass (exact parse)
+constexpr uint32_t ENT_POS = 0x3fffffffu;
+enum : uint32_t { ENT_MERGE = 0, ENT_NOMERGE = 1, ENT_SLOW = 2, ENT_BAD = 3 };
+
+__device__ __forceinline__ SnapEnt mk_ent(uint32_t pos, uint32_t flag, uint32_t out) {
+    return SnapEnt{pos | (flag << 30), out};
+}
+
+// MERGE: pos = meeting point m, out = (true chain output in [e, m)) - (window chain output in
+// [W0, m)). NOMERGE: the chain from e leaves the window first: pos = its exit, out = its output.
+// SLOW: not resolved within ENT_STEPS tokens. BAD: the chain from e runs past the stream end.
+template <class BitF, class TokF>
+__device__ SnapEnt ent_walk(uint32_t e, uint32_t W0, uint64_t wend, uint64_t n, BitF bit, TokF tok) {
+    uint64_t q = e;
+    uint32_t acc = 0;
+    int steps = 0;
+    for (;;) {
+        if (q >= wend) return mk_ent(uint32_t(q), ENT_NOMERGE, acc);
+        if (bit(uint32_t(q))) break;
+        if (steps == ENT_STEPS) return mk_ent(e, ENT_SLOW, 0);
+        const SnapTok t = tok(uint32_t(q));
+        acc += t.ol;
+        q += t.tl;
+        steps++;
+        if (q > n) return mk_ent(e, ENT_BAD, 0);
+    }
+    uint64_t p = W0;
+    uint32_t g = 0;
+    steps = 0;
+    while (p < q) {
+        if (steps == ENT_STEPS) return mk_ent(e, ENT_SLOW, 0);
+        const SnapTok t = tok(uint32_t(p));
+        g += t.ol;
+        p += t.tl;
+        steps++;
+    }
+    if (p != q) return mk_ent(e, ENT_SLOW, 0);
+    return mk_ent(uint32_t(q), ENT_MERGE, acc - g);
+}
+
 __device__ __forceinline__ uint32_t wave_sum_sat(uint32_t v) {
     uint64_t s = v;
     #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
     return s > 0xffffffffull ? 0xffffffffu : uint32_t(s);
+}
+
+// Exact whole-wave parse of the chain from e (a token start, W0 <= e < stop) up to the first chain
+// position >= stop, on a staged window. 64 lanes decode the token at cur + lane; the chain through
+// those 64 candidates is followed in scalar registers (readlane), so each 64-byte block costs one
+// LDS read per lane plus one scalar step per token. Token starts are OR-ed into sbits (bit i =
+// W0 + i) and output lengths added to slo[(pos - W0) / SNAP_RB] (both zeroed by the caller).
+// Returns the exit (SNAP_INVALID if the chain runs past n) and the output byte total in `out`.
+__device__ uint32_t seq_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t e, uint64_t stop,
+                              uint32_t* sbits, uint32_t* slo, uint32_t& out) {
+    const int lane = threadIdx.x & 63;
+    uint64_t cur = e;
+    uint32_t acc = 0;
+    out = 0;
+    while (cur < stop) {
+        const uint64_t q = cur + uint64_t(lane);
+        const SnapTok t = snap_tok(lds_read8(stage, woff + uint32_t(q - W0)));
+        const uint32_t tl = t.tl > 0x7fffffffull ? 0x7fffffffu : uint32_t(t.tl);
+        const uint32_t lim = uint32_t(min<uint64_t>(64, stop - cur));
+        uint32_t k = 0;
+        uint64_t mask = 0;
+        while (k < lim) {
+            mask |= 1ull << k;
+            k += __builtin_amdgcn_readlane(tl, k);
+        }
+        if ((mask >> lane) & 1ull) {
+            const uint32_t r = uint32_t(q - W0);
+            atomicOr(&sbits[r >> 5], 1u << (r & 31u));
+            atomicAdd(&slo[r / SNAP_RB], t.ol);
+            const uint32_t a = acc + t.ol;
+            acc = a < acc ? 0xffffffffu : a;
+        }
+        cur += k;
+        if (cur > n) return SNAP_INVALID;
+    }
+    out = wave_sum_sat(acc);
+    return uint32_t(cur);
 }
 
 __device__ __forceinline__ void store_window(uint32_t* tm, uint32_t* lo, const WinLane& L, int lane) {
@@ -153,9 +240,11 @@ __device__ __forceinline__ void store_window(uint32_t* tm, uint32_t* lo, const W
 }
 
 __global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict__ jobs, const int2* __restrict__ wins,
-                                                     SnapWin* __restrict__ win, uint32_t* __restrict__ lane_out,
-                                                     int* __restrict__ fb) {
+                                                     SnapWin* __restrict__ win, SnapEnt* __restrict__ ent,
+                                                     uint32_t* __restrict__ lane_out, int* __restrict__ fb) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[SNAP_WSTAGE];
+    __shared__ __attribute__((aligned(16))) uint32_t sbits[SNAP_WWORDS];
+    __shared__ uint32_t slo[64];
     const int2 jw = wins[blockIdx.x];
     const SnappyJob job = jobs[jw.x];
     const int lane = threadIdx.x;
@@ -180,13 +269,38 @@ __global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict
         if (lane == 0) win[wi] = SnapWin{entry, entry, 0, 0};
         return;
     }
+    const uint64_t wend = min(uint64_t(W0) + SNAP_WIN, n);
     const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
     __syncthreads();
     uint32_t flags;
-    const uint32_t X = win_parse(stage, woff, W0, n, entry, L, flags);
+    uint32_t X = win_parse(stage, woff, W0, n, entry, L, flags);
+    uint32_t sum;
+    if (flags & WIN_NOCONV) {   // chains that do not synchronise: exact whole-wave parse instead
+        reinterpret_cast<uint4*>(sbits)[lane] = make_uint4(0, 0, 0, 0);
+        slo[lane] = 0;
+        __syncthreads();
+        X = seq_parse(stage, woff, W0, n, entry, wend, sbits, slo, sum);
+        flags = X == SNAP_INVALID ? WIN_BROKEN : 0u;
+        __syncthreads();
+        const uint4 v = reinterpret_cast<const uint4*>(sbits)[lane];
+        L.b0 = v.x; L.b1 = v.y; L.b2 = v.z; L.b3 = v.w;
+        L.out = slo[lane];
+    } else {
+        sum = wave_sum_sat(L.out);
+    }
     store_window(tm, lo, L, lane);
-    const uint32_t sum = wave_sum_sat(L.out);
     if (lane == 0) win[wi] = SnapWin{entry, X, sum, flags};
+    if (jw.y == 0) return;   // window 0's entry is exact: no table
+    // entry table: lane d follows the chain from W0 + d until it meets this window's chain
+    __syncthreads();
+    reinterpret_cast<uint4*>(sbits)[lane] = make_uint4(L.b0, L.b1, L.b2, L.b3);
+    __syncthreads();
+    SnapEnt T = mk_ent(0, ENT_SLOW, 0);
+    if (!(flags & WIN_BROKEN) && uint64_t(W0) + lane < wend)
+        T = ent_walk(W0 + uint32_t(lane), W0, wend, n,
+                     [&](uint32_t q) { return (sbits[(q - W0) >> 5] >> ((q - W0) & 31u)) & 1u; },
+                     [&](uint32_t q) { return snap_tok(lds_read8(stage, woff + (q - W0))); });
+    ent[size_t(wi) * 64 + lane] = T;
 }
 
 #ifdef PF_SNAP_TRACE
@@ -219,23 +333,27 @@ extern "C" int pf_debug_trace(uint32_t* out, int n, int reset) {
 #define TRACEF(...) ((void)0)
 #endif
 
-// ======================================================================== fix pass
+// ======================================================================== chain pass
 
 constexpr int FIX_MAXW = 1024;       // pages up to 8 MiB compressed (larger: serial fallback)
-constexpr int MERGE_STEPS = 64;      // true-chain steps before a window is re-parsed instead
-constexpr int FIX_ROUNDS = 256;
+constexpr int CHAIN_BLK = 32;        // windows whose records + tables the chain pass stages at once
 
 __device__ __forceinline__ bool tm_get(const uint32_t* tm, uint32_t i) { return (tm[i >> 5] >> (i & 31u)) & 1u; }
-__device__ __forceinline__ void tm_set(uint32_t* tm, uint32_t i) { tm[i >> 5] |= 1u << (i & 31u); }
-__device__ __forceinline__ void tm_clr(uint32_t* tm, uint32_t i) { tm[i >> 5] &= ~(1u << (i & 31u)); }
 
-__global__ __launch_bounds__(64) void k_snappy_fix(const SnappyJob* __restrict__ jobs, SnapWin* __restrict__ win,
-                                                   uint32_t* __restrict__ lane_out, uint32_t* __restrict__ splits,
-                                                   int* __restrict__ fb) {
+// One wave per page. Window 0's entry is exact (after the varint); window w's true entry is
+// window w-1's true exit. For an entry within the first 64 bytes of a window the index pass
+// already knows where that chain meets the window's own chain (SnapEnt table); deeper entries
+// (after a long literal) walk from the bitmap in HBM; windows the table cannot resolve are parsed
+// exactly from the true entry by the whole wave. One table lookup per window. The result replaces
+// the window's SnapWin: {true entry, merge point / exit, true output bytes, WM_* mode}.
+__global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict__ jobs, SnapWin* __restrict__ win,
+                                                     const SnapEnt* __restrict__ ent, uint32_t* __restrict__ lane_out,
+                                                     int* __restrict__ fb) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[SNAP_WSTAGE];
-    __shared__ uint32_t s_x[FIX_MAXW], s_ent[FIX_MAXW], s_c[FIX_MAXW], s_pre[FIX_MAXW + 1];
-    __shared__ uint8_t s_rr[FIX_MAXW], s_fl[FIX_MAXW], s_tr[FIX_MAXW];
-    __shared__ uint32_t s_end;
+    __shared__ __attribute__((aligned(16))) uint32_t sbits[SNAP_WWORDS];
+    __shared__ uint32_t slo[64];
+    __shared__ SnapWin s_win[CHAIN_BLK];
+    __shared__ __attribute__((aligned(16))) SnapEnt s_tab[CHAIN_BLK * 64];
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
     const SnappyJob job = jobs[j];
@@ -243,175 +361,170 @@ __global__ __launch_bounds__(64) void k_snappy_fix(const SnappyJob* __restrict__
     const uint32_t nw = job.n_win;
     const uint64_t n = job.src_len;
     SnapWin* Wn = win + job.win_base;
+    const SnapEnt* E = ent + size_t(job.win_base) * 64;
     uint32_t* LO = lane_out + size_t(job.win_base) * 64;
     if (nw > uint32_t(FIX_MAXW) || (Wn[0].flags & WIN_BROKEN)) {
         if (lane == 0) fb[j] = FB_SERIAL;
         return;
     }
-    bool ok = false;
-    for (int round = 0; round < FIX_ROUNDS; round++) {
-        for (uint32_t w = lane; w < nw; w += 64) {
-            const SnapWin sw = Wn[w];
-            s_x[w] = sw.exit;
-            s_c[w] = sw.entry;
-            s_fl[w] = uint8_t(sw.flags);
-            s_rr[w] = 0;
-        }
-        __syncthreads();
-        if (lane == 0) {
-            // True entries along the chain, assuming each window's exit is right. While the entry is
-            // trusted (derived from exact windows only), a window whose first token already leaves
-            // it (a long literal) is resolved right here, so literal-only runs settle in one round.
-            uint32_t e = s_x[0];
-            bool trusted = true;
-            for (uint32_t w = 1; w < nw; w++) {
-                s_ent[w] = e;
-                s_tr[w] = trusted;
-                const uint64_t wend = min(uint64_t(w + 1) * SNAP_WIN, n);
-                if (uint64_t(e) >= wend) continue;
-                if (e == s_c[w] && !(s_fl[w] & (WIN_PASS | WIN_BROKEN))) { e = s_x[w]; continue; }
-                if (trusted) {
-                    const uint64_t x = e + snap_tok(glb_read8(job.src, n, e)).tl;
-                    if (x >= wend && x <= n) { s_rr[w] = 2; e = uint32_t(x); continue; }
-                }
-                trusted = false;
-                e = s_x[w];
-            }
-            for (uint32_t w = 0; w < nw; w++) TRACEF(0xEEEE0000u | uint32_t(round), w, w ? s_ent[w] : 0u, s_c[w], s_x[w], uint32_t(s_fl[w]) | (uint32_t(s_rr[w]) << 8));
-        }
-        __syncthreads();
-        int changed = 0, serial = 0;
-        for (uint32_t w = 1 + lane; w < nw; w += 64) {
-            const uint32_t e = s_ent[w];
-            const uint32_t W0 = w * SNAP_WIN;
-            const uint64_t wend = min(uint64_t(W0) + SNAP_WIN, n);
-            uint32_t* tm = job.tokmap + size_t(w) * SNAP_WWORDS;
-            uint32_t* lo = LO + size_t(w) * 64;
-            const uint32_t c = s_c[w], x0 = s_x[w], fl = s_fl[w];
-            const bool pass = fl & WIN_PASS;
-            // entry not known yet (an earlier window's exit is being re-derived this round): keep
-            // this window's index results untouched for the next round
-            if (e == SNAP_INVALID) continue;
-            if (e >= wend) {   // jumped over by a literal: no token starts in this window
-                if (!pass || c != e) {
-                    for (int q = 0; q < 64; q++) { reinterpret_cast<uint4*>(tm)[q] = make_uint4(0, 0, 0, 0); lo[q] = 0; }
-                    Wn[w] = SnapWin{e, e, 0, WIN_PASS};
-                }
-                continue;
-            }
-            if (e == c && !pass) continue;   // verified against this entry before
-            uint64_t q = e;
-            uint32_t acc = 0;
-            bool merged = false, bad = false;
-            if (s_rr[w] == 2) {   // a single token spans the rest of the window
-                const SnapTok t = snap_tok(glb_read8(job.src, n, q));
-                acc = t.ol;
-                q += t.tl;
-            } else {   // walk the true chain from e until it meets the window's chain
-                int steps = 0;
-                // a broken guessed chain has no trustworthy exit: never merge into it
-                const bool nomerge = pass || (fl & WIN_BROKEN);
-                while (q < wend && steps < MERGE_STEPS) {
-                    if (!nomerge && tm_get(tm, uint32_t(q) - W0)) { merged = true; break; }
-                    const SnapTok t = snap_tok(glb_read8(job.src, n, q));
-                    acc += t.ol;
-                    q += t.tl;
-                    steps++;
-                    if (q > n) { bad = true; break; }
-                }
-            }
-            TRACEF(0xFFFF0000u | (bad ? 1u : 0u) | (merged ? 2u : 0u) | (q >= wend ? 4u : 0u), w, e, uint32_t(q), acc);
-            if (bad) {   // the chain from e leaves the stream: corrupt if e is known true, else a bad guess
-                if (s_tr[w]) serial = 1;
-            } else if (merged) {
-                const SnapWin sw = Wn[w];
-                uint32_t rem = 0;
-                for (uint64_t p = c; p < q;) {   // the guessed chain's tokens before the meeting point
-                    const SnapTok t = snap_tok(glb_read8(job.src, n, p));
-                    tm_clr(tm, uint32_t(p) - W0);
-                    lo[(uint32_t(p) - W0) / SNAP_RB] -= t.ol;
-                    rem += t.ol;
-                    p += t.tl;
-                }
-                for (uint64_t p = e; p < q;) {   // the true ones
-                    const SnapTok t = snap_tok(glb_read8(job.src, n, p));
-                    tm_set(tm, uint32_t(p) - W0);
-                    lo[(uint32_t(p) - W0) / SNAP_RB] += t.ol;
-                    p += t.tl;
-                }
-                Wn[w] = SnapWin{e, sw.exit, sw.out - rem + acc, sw.flags};
-            } else if (q >= wend) {   // the true chain crosses the window without meeting it
-                for (int r = 0; r < 64; r++) { reinterpret_cast<uint4*>(tm)[r] = make_uint4(0, 0, 0, 0); lo[r] = 0; }
-                for (uint64_t p = e; p < q;) {
-                    const SnapTok t = snap_tok(glb_read8(job.src, n, p));
-                    tm_set(tm, uint32_t(p) - W0);
-                    lo[(uint32_t(p) - W0) / SNAP_RB] += t.ol;
-                    p += t.tl;
-                }
-                Wn[w] = SnapWin{e, uint32_t(q), acc, 0};
-                if (uint32_t(q) != x0) changed = 1;
-            } else {
-                s_rr[w] = 1;   // long divergence: re-parse below
-            }
-        }
-        __threadfence();   // other lanes read these windows' tables next
-        __syncthreads();
-        for (uint32_t w = 1; w < nw; w++) {   // re-parse windows from their entry (whole wave)
-            if (s_rr[w] != 1) continue;
-            const uint32_t W0 = w * SNAP_WIN;
-            const uint32_t e = s_ent[w];
+    const SnapWin w0 = Wn[0];
+    uint32_t e = w0.exit;
+    if (lane == 0) Wn[0] = SnapWin{w0.entry, w0.exit, w0.out, WM_KEEP};
+    bool bad = false;
+    for (uint32_t w = 1; w < nw; w++) {
+        const uint32_t W0 = w * SNAP_WIN;
+        const uint64_t wend = min(uint64_t(W0) + SNAP_WIN, n);
+        const uint32_t cb = (w - 1) % CHAIN_BLK;
+        if (cb == 0) {   // stage the next block of window records and entry tables
             __syncthreads();
-            const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
+            const uint32_t nb = min(uint32_t(CHAIN_BLK), nw - w);
+            if (uint32_t(lane) < nb) s_win[lane] = Wn[w + lane];
+            const uint4* src = reinterpret_cast<const uint4*>(E + size_t(w) * 64);
+            for (uint32_t i = lane; i < nb * 32; i += 64) reinterpret_cast<uint4*>(s_tab)[i] = src[i];
             __syncthreads();
-            WinLane L;
-            uint32_t fl;
-            const uint32_t X = win_parse(stage, woff, W0, n, e, L, fl);
-            store_window(job.tokmap + size_t(w) * SNAP_WWORDS, LO + size_t(w) * 64, L, lane);
-            const uint32_t sum = wave_sum_sat(L.out);
-            if (lane == 0) Wn[w] = SnapWin{e, X, sum, fl};
-            if (lane == 0) TRACEF(0x99990000u, w, e, X, fl);
-            if (X != s_x[w]) changed = 1;
         }
-        if (__any(serial)) {
-            if (lane == 0) fb[j] = FB_SERIAL;
-            return;
+        if (uint64_t(e) >= wend) {   // inside a literal that started earlier: no token here
+            if (lane == 0) Wn[w] = SnapWin{e, e, 0, WM_SKIP};
+            continue;
         }
-        const bool any_changed = __any(changed);
-        __threadfence();
-        __syncthreads();
-        if (!any_changed) { ok = true; break; }
-    }
-    if (lane == 0) {   // the converged chain: every window entered where verified, none broken
-        uint32_t e = Wn[0].exit;
-        for (uint32_t w = 1; w < nw && ok; w++) {
-            const SnapWin sw = Wn[w];
-            if (uint64_t(e) >= min(uint64_t(w + 1) * SNAP_WIN, n)) continue;
-            if (sw.entry != e || (sw.flags & (WIN_PASS | WIN_BROKEN))) ok = false;
+        const SnapWin sw = s_win[cb];
+        const uint32_t d = e - W0;
+        const uint32_t* tm = job.tokmap + size_t(w) * SNAP_WWORDS;
+        SnapEnt T;
+        if (sw.flags & WIN_BROKEN) T = mk_ent(e, ENT_SLOW, 0);
+        else if (d < 64) T = s_tab[cb * 64 + d];
+        else T = ent_walk(e, W0, wend, n, [&](uint32_t q) { return tm_get(tm, q - W0); },
+                          [&](uint32_t q) { return snap_tok(glb_read8(job.src, n, q)); });
+        const uint32_t fl = T.pos >> 30, pos = T.pos & ENT_POS;
+        if (fl == ENT_BAD) { bad = true; break; }
+        if (fl == ENT_MERGE) {
+            if (lane == 0) Wn[w] = SnapWin{e, pos, sw.out + T.out, WM_MERGE};
             e = sw.exit;
+            continue;
         }
-        s_end = ok ? e : SNAP_INVALID;
+        if (fl == ENT_NOMERGE) {   // the true chain crosses the window without meeting its chain
+            if (lane == 0) Wn[w] = SnapWin{e, pos, T.out, WM_FULL};
+            e = pos;
+            continue;
+        }
+        // unresolved: exact parse of the window from its true entry (whole wave)
+        __syncthreads();
+        const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
+        reinterpret_cast<uint4*>(sbits)[lane] = make_uint4(0, 0, 0, 0);
+        slo[lane] = 0;
+        __syncthreads();
+        uint32_t sum;
+        const uint32_t X = seq_parse(stage, woff, W0, n, e, wend, sbits, slo, sum);
+        if (X == SNAP_INVALID) { bad = true; break; }
+        __syncthreads();
+        reinterpret_cast<uint4*>(job.tokmap + size_t(w) * SNAP_WWORDS)[lane] = reinterpret_cast<const uint4*>(sbits)[lane];
+        LO[size_t(w) * 64 + lane] = slo[lane];
+        if (lane == 0) Wn[w] = SnapWin{e, X, sum, WM_DONE};
+        e = X;
     }
+    if (bad || uint64_t(e) != n) {
+        if (lane == 0) fb[j] = FB_SERIAL;
+    }
+}
+
+// One wave per window: make the bitmap and lane output counts of windows whose true entry is not
+// their own chain's start exact — tokens in [W0, merge point) for WM_MERGE, the whole window for
+// WM_FULL — by parsing from the true entry on the staged window.
+__global__ __launch_bounds__(64) void k_snappy_repair(const SnappyJob* __restrict__ jobs, const int2* __restrict__ wins,
+                                                      const SnapWin* __restrict__ win, uint32_t* __restrict__ lane_out,
+                                                      int* __restrict__ fb) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[SNAP_WSTAGE];
+    __shared__ __attribute__((aligned(16))) uint32_t sbits[SNAP_WWORDS];
+    __shared__ uint32_t slo[64];
+    const int2 jw = wins[blockIdx.x];
+    const SnappyJob job = jobs[jw.x];
+    const int lane = threadIdx.x;
+    if (fb[jw.x] == FB_SERIAL) return;
+    const uint32_t w = uint32_t(jw.y);
+    const SnapWin sw = win[job.win_base + w];
+    const uint32_t W0 = w * SNAP_WIN;
+    if (!((sw.flags == WM_MERGE && sw.entry != W0) || sw.flags == WM_FULL)) return;
+    const uint64_t n = job.src_len;
+    const uint64_t wend = min(uint64_t(W0) + SNAP_WIN, n);
+    const uint64_t stop = sw.flags == WM_FULL ? wend : uint64_t(sw.exit);
+    const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
+    reinterpret_cast<uint4*>(sbits)[lane] = make_uint4(0, 0, 0, 0);
+    slo[lane] = 0;
     __syncthreads();
-    // totals
-    uint32_t run = 0;
-    for (uint32_t w0 = 0; w0 < nw; w0 += 64) {
-        const uint32_t w = w0 + lane;
-        const uint32_t o = w < nw ? Wn[w].out : 0u;
-        uint32_t x = o;
-        #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        if (w < nw) s_pre[w] = run + x - o;
-        run += __shfl(x, 63, 64);
+    uint32_t sum;
+    const uint32_t X = seq_parse(stage, woff, W0, n, sw.entry, stop, sbits, slo, sum);
+    __syncthreads();
+    uint32_t* tm = job.tokmap + size_t(w) * SNAP_WWORDS;
+    uint32_t* lo = lane_out + size_t(job.win_base + w) * 64;
+    if (sw.flags == WM_FULL) {
+        if (X == SNAP_INVALID || uint64_t(X) < wend) { if (lane == 0) atomicMax(&fb[jw.x], FB_SERIAL); return; }
+        reinterpret_cast<uint4*>(tm)[lane] = reinterpret_cast<const uint4*>(sbits)[lane];
+        lo[lane] = slo[lane];
+        return;
     }
-    if (s_end != n || run != job.dst_len) {
+    if (X != sw.exit) { if (lane == 0) atomicMax(&fb[jw.x], FB_SERIAL); return; }
+    // WM_MERGE: bits below the merge point m come from the parse, bits from m on stay
+    const uint32_t rel = sw.exit - W0, rm = rel / SNAP_RB;
+    if (uint32_t(lane) > rm) return;
+    uint32_t nb[4];
+    #pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t wi = uint32_t(lane) * 4 + k, b0 = wi * 32;
+        const uint32_t low = b0 + 32 <= rel ? 0xffffffffu : (b0 >= rel ? 0u : (1u << (rel - b0)) - 1u);
+        nb[k] = low == 0xffffffffu ? sbits[wi] : ((sbits[wi] & low) | (tm[wi] & ~low));
+        tm[wi] = nb[k];
+    }
+    if (uint32_t(lane) < rm) { lo[lane] = slo[lane]; return; }
+    // the merge point's region: parsed tokens below m plus the window's own tokens from m on
+    uint32_t acc = slo[lane];
+    #pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t b0 = (uint32_t(lane) * 4 + k) * 32;
+        uint32_t mm = nb[k] & ~(b0 + 32 <= rel ? 0xffffffffu : (b0 >= rel ? 0u : (1u << (rel - b0)) - 1u));
+        while (mm) {
+            const uint32_t i = b0 + uint32_t(__ffs(mm) - 1);
+            mm &= mm - 1;
+            acc += snap_tok(lds_read8(stage, woff + i)).ol;
+        }
+    }
+    lo[lane] = acc;
+}
+
+// One wave per page: check the output total, then find the input position of the token that
+// starts at each 64 KiB output boundary (window prefix sums -> lane region -> bitmap walk).
+__global__ __launch_bounds__(64) void k_snappy_splits(const SnappyJob* __restrict__ jobs, const SnapWin* __restrict__ win,
+                                                      const uint32_t* __restrict__ lane_out, uint32_t* __restrict__ splits,
+                                                      int* __restrict__ fb) {
+    __shared__ uint32_t s_pre[FIX_MAXW + 1];
+    const int j = blockIdx.x;
+    const int lane = threadIdx.x;
+    const SnappyJob job = jobs[j];
+    if (fb[j] == FB_SERIAL) return;
+    const uint32_t nw = job.n_win;
+    const uint64_t n = job.src_len;
+    const SnapWin* Wn = win + job.win_base;
+    const uint32_t* LO = lane_out + size_t(job.win_base) * 64;
+    uint32_t run = 0;
+    bool ovf = false;
+    for (uint32_t w0i = 0; w0i < nw; w0i += 64) {
+        const uint32_t w = w0i + lane;
+        const uint32_t o = w < nw ? Wn[w].out : 0u;
+        uint64_t x = o;
+        #pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint64_t y = __shfl_up(x, dd, 64);
+            if (lane >= dd) x += y;
+        }
+        if (w < nw) s_pre[w] = uint32_t(run + x - o);
+        const uint64_t t = uint64_t(run) + __shfl(x, 63, 64);
+        ovf |= t > 0xffffffffull;
+        run = uint32_t(t);
+    }
+    if (ovf || run != job.dst_len) {
         if (lane == 0) fb[j] = FB_SERIAL;
         return;
     }
     __syncthreads();
-    // input position of the token starting at each 64 KiB output boundary
     uint32_t* sp = splits + job.split_base;
     for (uint32_t k = 1 + lane; k < job.n_pieces; k += 64) {
         const uint32_t B = k * SNAP_BLOCK;
@@ -434,10 +547,10 @@ __global__ __launch_bounds__(64) void k_snappy_fix(const SnappyJob* __restrict__
         uint32_t found = SNAP_INVALID;
         bool done = false;
         for (int wd = 0; wd < 4 && !done; wd++) {
-            uint32_t m = tm[wd];
-            while (m) {
-                const uint32_t p = rs + uint32_t(wd) * 32 + uint32_t(__ffs(m) - 1);
-                m &= m - 1;
+            uint32_t mm = tm[wd];
+            while (mm) {
+                const uint32_t p = rs + uint32_t(wd) * 32 + uint32_t(__ffs(mm) - 1);
+                mm &= mm - 1;
                 if (cum == B) { found = p; done = true; break; }
                 if (cum > B) { done = true; break; }
                 cum += snap_tok(glb_read8(job.src, n, p)).ol;
@@ -455,15 +568,23 @@ constexpr uint32_t XRMASK = XRING - 1;
 constexpr uint32_t XSLOT = 2048;     // flush granule
 constexpr uint32_t XCHUNK = 1024;    // input bytes whose tokens are enumerated at once
 constexpr uint32_t XSTAGE = XCHUNK + 64 + 16;
+constexpr uint32_t XBATCH = 2048;    // output bytes of one parallel step (ring: XBATCH + XSLOT <= XRING)
+constexpr uint32_t XLIT = 1024;      // long literals are copied in pieces of this many bytes
+constexpr uint32_t FBUF_W = 17;      // dwords per lane of far-copy source (64 bytes + misalignment)
 
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Batch-parallel executor step limits. A batch writes at most XPAR_OUT bytes into the ring, so
-// with op - F < XSLOT at its start, a copy reaching back <= XNEAR still finds its source in the
-// ring and any longer copy reads output flushed >= 2 KiB earlier.
-constexpr uint32_t XPAR_OUT = 2048;
-constexpr uint32_t XPAR_TOK = 64;
-constexpr uint32_t XNEAR = XRING - XPAR_OUT;
+// x mod d for 0 <= x < 64, 1 <= d <= 64 ((x + 0.5) / d is never within 1/128 of an integer).
+__device__ __forceinline__ uint32_t mod_small(uint32_t x, uint32_t d) {
+    const uint32_t q = uint32_t((float(x) + 0.5f) * __builtin_amdgcn_rcpf(float(d)));
+    return x - q * d;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    #pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, uint32_t(__shfl_xor(v, d, 64)));
+    return v;
+}
 
 // Number of lanes whose key is < x; keys ascend over the lanes (all 64 lanes must call).
 __device__ __forceinline__ uint32_t lanes_below(uint32_t key, uint32_t x) {
@@ -479,45 +600,10 @@ __device__ __forceinline__ uint32_t lanes_below(uint32_t key, uint32_t x) {
 
 __device__ __forceinline__ uint64_t lane_mask_lt(uint32_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }
 
-// One batch-parallel executor step (all 64 lanes; lane t holds token t of the sub-batch: `take`,
-// kind, output length ol, literal source position or copy offset, output position otok).
-// Literals are independent and go first; copies then run in dependency rounds: a copy runs once
-// no pending copy of the batch writes a byte it reads ([a, b); for offset < length only the
-// first `off` bytes before it). Returns false on a copy reaching before the piece.
-__device__ __forceinline__ bool par_step(uint8_t* ring, const uint8_t* stage, uint8_t* dst, uint32_t woff, uint32_t I,
-                                         uint32_t out_start, uint32_t op, uint32_t& F, bool take, uint32_t kd,
-                                         uint32_t ol, uint32_t srcv, uint32_t off, uint32_t otok, uint32_t btot,
-                                         int lane) {
-    wait_vmem();   // flushed output is visible to far copies
-    if (take && kd == 0) {
-        const uint32_t sb = woff + (srcv - I);
-        for (uint32_t j = 0; j < ol; j++) ring[(otok + j) & XRMASK] = stage[sb + j];
-    }
-    __syncthreads();
-    const bool cp = take && kd != 0;
-    if (__any(cp && (off == 0 || off > otok - out_start))) return false;
-    const uint32_t a = otok - off;
-    const uint32_t b = a + min(ol, off);
-    const uint32_t kb = lanes_below(take ? otok : 0xffffffffu, b);            // outputs starting before b
-    const uint32_t ka = lanes_below(take ? otok + ol : 0xffffffffu, a + 1);  // outputs ending by a
-    const uint64_t dep = (cp && kb > ka) ? (lane_mask_lt(kb) & ~lane_mask_lt(ka)) : 0ull;
-    uint64_t pend = __ballot(cp);
-    while (pend) {
-        const bool ready = cp && ((pend >> lane) & 1ull) && (dep & pend) == 0ull;
-        if (ready) {
-            const bool near = off <= XNEAR;
-            uint32_t r = 0;
-            for (uint32_t j = 0; j < ol; j++) {
-                const uint32_t s = a + r;
-                const uint8_t v = near ? ring[s & XRMASK] : dst[s];   // far: flushed >= 2 KiB ago
-                ring[(otok + j) & XRMASK] = v;
-                r = r + 1 == off ? 0u : r + 1;
-            }
-        }
-        pend &= ~__ballot(ready);
-        __syncthreads();
-    }
-    const uint32_t upto = op + btot;
+// Store ring bytes [F, upto) in whole XSLOT slots (16-byte stores, 32 B per lane). Returns the
+// number of slots stored (2 store instructions each).
+__device__ __forceinline__ uint32_t flush_slots(const uint8_t* ring, uint8_t* dst, uint32_t& F, uint32_t upto, int lane) {
+    uint32_t nsl = 0;
     while (upto - F >= XSLOT) {
         const uint32_t a0 = F + uint32_t(lane) * 32u;
         const uint4 v0 = *reinterpret_cast<const uint4*>(ring + (a0 & XRMASK));
@@ -525,15 +611,61 @@ __device__ __forceinline__ bool par_step(uint8_t* ring, const uint8_t* stage, ui
         *reinterpret_cast<uint4*>(dst + a0) = v0;
         *reinterpret_cast<uint4*>(dst + a0 + 16) = v1;
         F += XSLOT;
+        nsl++;
     }
-    return true;
+    return nsl;
 }
 
+// ---- wave64 DPP helpers (VALU-speed; __shfl goes through LDS) ----
+__device__ __forceinline__ uint32_t dpp_incl_scan(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {               // lane i <- lane i-1
+    return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xf, 0xf, false);  // wave_shr:1
+}
+
+__device__ __forceinline__ void wait_vmem_but2() { asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
+
+// Executor step descriptor of one token (LDS, indexed by the token's lane).
+enum : uint32_t { XD_LIT = 0, XD_NEAR = 1, XD_FAR = 2, XD_DEP = 3 };
+struct XDesc {
+    uint32_t rel;    // output position relative to the step start
+    uint32_t src;    // LIT: stage offset; NEAR: absolute output position; FAR: fbuf byte offset
+    uint32_t off;    // copy offset (NEAR copies with off < len repeat their source)
+    uint32_t kind;
+};
+
+// One wave per 64 KiB piece (or per page). Token starts come from the bitmap, XCHUNK input bytes
+// at a time; 64 tokens are decoded at once (one per lane) and their output positions scanned
+// (DPP). A step then writes up to XBATCH output bytes into the LDS ring:
+//   far copies (source older than the ring) first issue their HBM loads (flushed output), so the
+//     latency overlaps the next phase;
+//   A. byte-parallel: output byte x of the step is lane x mod 64; its token comes from a
+//      token-start bitmap of the step's output (word prefix counts + popcount), then the byte is
+//      taken from the staged literal or the ring — every literal and every copy whose source
+//      lies wholly before the step;
+//   F. the far copies' bytes, from their prefetched source;
+//   B. copies whose source overlaps this step's output, in token order, one 64-lane
+//      read-then-write each (byte j reads src + j mod offset, always earlier output).
+// Literals longer than 64 bytes (or not staged) are copied alone, XLIT bytes at a time. Full
+// 2 KiB ring slots are flushed with 16-byte stores. A token chain that disagrees with the bitmap,
+// a copy reaching before the piece, or a piece not ending on a token marks the page for the
+// whole-page redo.
 __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
                                                     const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[XRING];
     __shared__ __attribute__((aligned(16))) uint8_t stage[XSTAGE];
     __shared__ uint16_t tokpos[XCHUNK / 2];
+    __shared__ __attribute__((aligned(16))) uint32_t fbuf[64 * FBUF_W];   // far-copy sources, one slot per lane
+    __shared__ __attribute__((aligned(16))) XDesc desc[64];
+    __shared__ uint32_t sbits[XBATCH / 32];                               // token starts of the step's output
+    __shared__ uint32_t wpre[XBATCH / 32];                                // tokens starting in earlier words
     const int lane = threadIdx.x;
     int j, k;
     if (mode == 0) { const int2 pc = pieces[blockIdx.x]; j = pc.x; k = pc.y; }
@@ -570,11 +702,13 @@ __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict_
     }
     const uint16_t* tm16 = reinterpret_cast<const uint16_t*>(job.tokmap);
     uint32_t op = out_start, F = out_start;
-#ifdef PF_SNAP_TRACE
-    const bool tr = false;
-    TRACE(0xAAAA0000u, uint32_t(k), ip, out_start, out_end);
-#endif
+    uint32_t nst = 0;   // store instructions issued by the last flush (still possibly in flight)
     bool bad = false;
+    XT_DECL;
+#ifdef PF_STAMPS
+    const unsigned long long xt0 = xt_;
+    if (lane == 0) STAMP_ADD(13, 1);
+#endif
     while (op < out_end && !bad) {
         if (ip >= n) { bad = true; break; }
         const uint32_t I = ip & ~15u;
@@ -586,133 +720,196 @@ __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict_
         if (p16 + 16u <= ip) bits = 0;
         else if (p16 < ip) bits &= ~((1u << (ip - p16)) - 1u);
         const uint32_t cnt = __popc(bits);
-        uint32_t ex = cnt;
-        #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(ex, d, 64);
-            if (lane >= d) ex += y;
-        }
-        const uint32_t T = __shfl(ex, 63, 64);
+        const uint32_t ex = dpp_incl_scan(cnt);
+        const uint32_t T = __builtin_amdgcn_readlane(ex, 63);
         uint32_t q = ex - cnt;
         while (bits) {
             const uint32_t b = uint32_t(__ffs(bits) - 1);
             bits &= bits - 1;
             tokpos[q++] = uint16_t(16u * uint32_t(lane) + b);
         }
+        nst = 0;   // the bitmap loads above waited for every earlier store
         __syncthreads();
+        XT(7);
         if (T == 0) { bad = true; break; }
-        bool stop = false;
-        for (uint32_t sb = 0; sb < T && !stop && !bad; sb += 64) {
+        uint32_t sb = 0;
+        while (sb < T && op < out_end) {
             const uint32_t t = sb + uint32_t(lane);
             const bool v = t < T;
             const uint32_t pos = v ? uint32_t(tokpos[t]) : 0u;
             const SnapTok tk = snap_tok(lds_read8(stage, woff + pos));
             const uint32_t ol = v ? tk.ol : 0u;
-            const uint64_t start = uint64_t(I) + pos;
-            const unsigned long long endp = start + tk.tl;
-            const unsigned long long prev = __shfl_up(endp, 1, 64);
-            uint32_t inc = ol;
-            #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(inc, d, 64);
-                if (lane >= d) inc += y;
-            }
+            const uint32_t start = I + pos;
+            const uint32_t endp = tk.tl > uint64_t(0xffffffffu - start) ? 0xffffffffu : start + uint32_t(tk.tl);
+            const uint32_t prev = dpp_prev(endp);
+            const uint32_t inc = dpp_incl_scan(ol);
             const uint32_t otok = op + inc - ol;
             const bool take = v && otok < out_end;
-            const unsigned long long tb = __ballot(take);
-            const int nt = __popcll(tb);
-            const bool wrong = take && ((lane == 0 ? start != ip : start != prev) || endp > n || op + inc > out_end);
+            const int nt = __popcll(__ballot(take));
+            const bool wrong = take && ((lane == 0 ? start != ip : start != prev) || endp > n || op + inc > out_end ||
+                                        inc < ol);
             if (__any(wrong)) { bad = true; break; }
-            if (nt == 0) break;   // the previous sub-batch ended exactly at out_end
-            if (uint32_t(nt) < min(T - sb, 64u)) stop = true;
-            TRACE(0xBBBB0000u | uint32_t(k), I, ip, T, sb, uint32_t(nt), op, F);
-            const uint32_t srcv = tk.kind == 0 ? uint32_t(start) + tk.arg : tk.arg;
+            if (nt == 0) break;   // the previous step ended exactly at out_end
             const uint32_t kd = tk.kind;
-            const uint32_t btot = __builtin_amdgcn_readlane(inc, nt - 1);
-            const bool lit = take && kd == 0;
-            // Batch-parallel step: every token of the sub-batch at once, one lane per token. Taken
-            // when the batch is short (no token > XPAR_TOK bytes, <= XPAR_OUT bytes in all) and
-            // every literal is staged; otherwise the token-serial step below.
-            const bool par = btot <= XPAR_OUT &&
-                             !__any(take && (ol > XPAR_TOK ||
-                                             (lit && uint64_t(srcv) + ol > uint64_t(I) + XCHUNK + 64)));
-            if (par) {
-                if (!par_step(ring, stage, dst, woff, I, out_start, op, F, take, kd, ol, srcv, tk.arg, otok, btot, lane)) {
-                    bad = true;
-                    break;
+            const uint32_t off = tk.arg;
+            const uint32_t srcv = start + tk.arg;   // literal data position
+            const bool lstaged = srcv + ol <= I + XCHUNK + 64;
+            XT(1);
+            if (lane == 0) STAMP_ADD(0, 1);
+            // step = tokens before the first long / unstaged literal and within XBATCH output bytes
+            const unsigned long long cutm = __ballot(take && (ol > 64u || inc > XBATCH || (kd == 0 && !lstaged)));
+            const uint32_t cut = cutm ? uint32_t(__ffsll(cutm) - 1) : uint32_t(nt);
+            uint32_t used, btot;
+            if (cut == 0) {
+                // one literal, from HBM (copies are <= 64 bytes, so only a literal gets here)
+                const uint32_t L0 = __builtin_amdgcn_readfirstlane(ol);
+                const uint32_t s0 = __builtin_amdgcn_readfirstlane(srcv);
+                if (__builtin_amdgcn_readfirstlane(kd) != 0) { bad = true; break; }
+                uint32_t fl_slots = 0;
+                for (uint32_t d0 = 0; d0 < L0; d0 += XLIT) {
+                    const uint32_t c = min(L0 - d0, XLIT);
+                    const uint32_t b0 = uint32_t(lane) * 16u;
+                    if (b0 < c) {
+                        uint8_t by[16];
+                        #pragma unroll
+                        for (int u = 0; u < 16; u++) by[u] = b0 + u < c ? in[s0 + d0 + b0 + u] : uint8_t(0);
+                        #pragma unroll
+                        for (int u = 0; u < 16; u++)
+                            if (b0 + u < c) ring[(op + d0 + b0 + u) & XRMASK] = by[u];
+                    }
+                    fl_slots += flush_slots(ring, dst, F, op + d0 + c, lane);
                 }
-            } else
-            for (int i = 0; i < nt; i++) {
-                const uint32_t k_i = __builtin_amdgcn_readlane(kd, i);
-                const uint32_t l_i = __builtin_amdgcn_readlane(ol, i);
-                const uint32_t s_i = __builtin_amdgcn_readlane(srcv, i);
-                const uint32_t o_i = __builtin_amdgcn_readlane(otok, i);
-                if (o_i + l_i + 64 >= out_end || o_i < out_start + 64) TRACE(0xCCCC0000u | (uint32_t(k) << 8) | k_i, l_i, s_i, o_i, F);
-                if (k_i == 0) {
-                    const bool staged = uint64_t(s_i) + l_i <= uint64_t(I) + XCHUNK + 64;
-                    for (uint32_t d = 0; d < l_i; d += 1024) {
-                        const uint32_t c = min(l_i - d, 1024u);
-                        if (staged) {   // uniform: LDS -> LDS
-                            const uint32_t sb0 = woff + (s_i - I) + d;
-                            for (uint32_t qq = uint32_t(lane); qq < c; qq += 64)
-                                ring[(o_i + d + qq) & XRMASK] = stage[sb0 + qq];
-                        } else {        // long literal straight from HBM
-                            const uint8_t* ib = in + s_i + d;
-                            for (uint32_t qq = uint32_t(lane); qq < c; qq += 64)
-                                ring[(o_i + d + qq) & XRMASK] = __builtin_nontemporal_load(ib + qq);
-                        }
-                        const uint32_t upto = o_i + d + c;
-                        while (upto - F >= XSLOT) {
-                            wait_vmem();   // earlier flushes have landed: far copies may read them
-                            const uint32_t a0 = F + uint32_t(lane) * 32u;
-                            const uint4 v0 = *reinterpret_cast<const uint4*>(ring + (a0 & XRMASK));
-                            const uint4 v1 = *reinterpret_cast<const uint4*>(ring + ((a0 + 16u) & XRMASK));
-                            *reinterpret_cast<uint4*>(dst + a0) = v0;
-                            *reinterpret_cast<uint4*>(dst + a0 + 16) = v1;
-                            F += XSLOT;
+                nst = fl_slots * 2;
+                used = 1;
+                btot = L0;
+                XT(11);
+            } else {
+                used = cut;
+                btot = __builtin_amdgcn_readlane(inc, cut - 1);
+                const bool inb = take && uint32_t(lane) < cut;
+                const bool lit = inb && kd == 0;
+                const bool cp = inb && kd != 0;
+                if (__any(cp && (off == 0 || off > otok - out_start))) { bad = true; break; }
+                const uint32_t a = otok - off;                       // copy source start
+                const bool dep = cp && a + min(ol, off) > op;        // reads this step's output
+                const bool far = cp && !dep && int32_t(a - (op + btot - XRING)) < 0;
+                const bool anyfar = __any(far);
+                // far copies: issue the HBM loads of their source now (flushed output)
+                uint32_t fw[FBUF_W];
+                if (anyfar) {
+                    if (nst == 2) wait_vmem_but2();   // all but the last slot's stores have landed
+                    else wait_vmem();
+                    const uint32_t* fsrc = reinterpret_cast<const uint32_t*>(dst + (a & ~3u));
+                    const uint32_t nwd = far ? ((a & 3u) + ol + 3u) >> 2 : 0u;
+                    #pragma unroll
+                    for (int u = 0; u < int(FBUF_W); u++) fw[u] = uint32_t(u) < nwd ? fsrc[u] : 0u;
+                }
+                // step descriptors + token-start bitmap over the step's output
+                const uint32_t rel = otok - op;
+                if (inb) {
+                    XDesc dd;
+                    dd.rel = rel;
+                    dd.off = off;
+                    if (lit) { dd.kind = XD_LIT; dd.src = woff + (srcv - I); }
+                    else if (dep) { dd.kind = XD_DEP; dd.src = a; }
+                    else if (far) { dd.kind = XD_FAR; dd.src = uint32_t(lane) * (FBUF_W * 4) + (a & 3u); }
+                    else { dd.kind = XD_NEAR; dd.src = a; }
+                    desc[lane] = dd;
+                }
+                sbits[lane & (XBATCH / 32 - 1)] = 0;
+                __syncthreads();
+                if (inb) atomicOr(&sbits[rel >> 5], 1u << (rel & 31u));
+                __syncthreads();
+                {
+                    const uint32_t c = __popc(sbits[lane]);
+                    wpre[lane] = dpp_incl_scan(c) - c;
+                }
+                __syncthreads();
+                XT(3);
+                // A: byte-parallel literals + near copies
+                for (uint32_t x0 = 0; x0 < btot; x0 += 128) {
+                    uint8_t by[2];
+                    uint32_t xs[2];
+                    bool wr[2];
+                    #pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        const uint32_t x = x0 + uint32_t(u) * 64 + uint32_t(lane);
+                        xs[u] = x;
+                        wr[u] = false;
+                        by[u] = 0;
+                        if (x < btot) {
+                            const uint32_t wd = x >> 5;
+                            const uint32_t ti = wpre[wd] + __popc(sbits[wd] & ((2u << (x & 31u)) - 1u)) - 1u;
+                            const XDesc dd = desc[ti];
+                            const uint32_t jj = x - dd.rel;
+                            if (dd.kind == XD_LIT) { by[u] = stage[dd.src + jj]; wr[u] = true; }
+                            else if (dd.kind == XD_NEAR) {
+                                const uint32_t r = jj < dd.off ? jj : mod_small(jj, dd.off);
+                                by[u] = ring[(dd.src + r) & XRMASK];
+                                wr[u] = true;
+                            }
                         }
                     }
-                } else {
-                    if (s_i == 0 || s_i > o_i - out_start) { bad = true; break; }
-                    uint32_t jj = uint32_t(lane);
-                    if (s_i < l_i) jj = jj % s_i;            // overlapping copy repeats its pattern
-                    const uint32_t sa = o_i - s_i + jj;
-                    uint8_t byte = 0;
-                    if (s_i <= XRING) {
-                        if (uint32_t(lane) < l_i) byte = ring[sa & XRMASK];
-                    } else {
-                        if (uint32_t(lane) < l_i) byte = dst[sa];   // flushed: >= 6 KiB behind F
-                    }
-                    if (uint32_t(lane) < l_i) ring[(o_i + uint32_t(lane)) & XRMASK] = byte;
-#ifdef PF_SNAP_SAFE
+                    #pragma unroll
+                    for (int u = 0; u < 2; u++)
+                        if (wr[u]) ring[(op + xs[u]) & XRMASK] = by[u];
+                }
+                XT(2);
+                if (anyfar) {   // F: far copies (never self-overlapping: offset > ring > 64)
+                    if (lane == 0) STAMP_ADD(9, 1);
+                    uint32_t* fl = fbuf + lane * FBUF_W;
+                    const uint32_t nwd = far ? ((a & 3u) + ol + 3u) >> 2 : 0u;
+                    #pragma unroll
+                    for (int u = 0; u < int(FBUF_W); u++)
+                        if (uint32_t(u) < nwd) fl[u] = fw[u];
                     __syncthreads();
-#endif
-                    const uint32_t upto = o_i + l_i;
-                    while (upto - F >= XSLOT) {
-                        wait_vmem();
-                        const uint32_t a0 = F + uint32_t(lane) * 32u;
-                        const uint4 v0 = *reinterpret_cast<const uint4*>(ring + (a0 & XRMASK));
-                        const uint4 v1 = *reinterpret_cast<const uint4*>(ring + ((a0 + 16u) & XRMASK));
-                        *reinterpret_cast<uint4*>(dst + a0) = v0;
-                        *reinterpret_cast<uint4*>(dst + a0 + 16) = v1;
-                        F += XSLOT;
+                    const uint8_t* fb8 = reinterpret_cast<const uint8_t*>(fbuf);
+                    for (uint32_t x0 = 0; x0 < btot; x0 += 64) {
+                        const uint32_t x = x0 + uint32_t(lane);
+                        if (x < btot) {
+                            const uint32_t wd = x >> 5;
+                            const uint32_t ti = wpre[wd] + __popc(sbits[wd] & ((2u << (x & 31u)) - 1u)) - 1u;
+                            const XDesc dd = desc[ti];
+                            if (dd.kind == XD_FAR) ring[(op + x) & XRMASK] = fb8[dd.src + (x - dd.rel)];
+                        }
                     }
                 }
-            }
-            if (bad) break;
+                XT(4);
+                // B: dependent copies in token order
+                unsigned long long dm = __ballot(dep);
+                if (lane == 0) STAMP_ADD(8, __popcll(dm));
+                while (dm) {
+                    const int i = __ffsll(dm) - 1;
+                    dm &= dm - 1;
+                    const uint32_t oi = __builtin_amdgcn_readlane(otok, i);
+                    const uint32_t fi = __builtin_amdgcn_readlane(off, i);
+                    const uint32_t li = __builtin_amdgcn_readlane(ol, i);
+                    if (uint32_t(lane) < li) {
+                        const uint32_t r = fi < li ? mod_small(uint32_t(lane), fi) : uint32_t(lane);
+                        const uint8_t byte = ring[(oi - fi + r) & XRMASK];
+                        ring[(oi + uint32_t(lane)) & XRMASK] = byte;
+                    }
+                }
 #ifdef PF_SNAP_SAFE
-            __syncthreads();
+                __syncthreads();
 #endif
-            op += __builtin_amdgcn_readlane(inc, nt - 1);
-            ip = uint32_t(__shfl(endp, nt - 1, 64));
-            if (op >= out_end) stop = true;
+                XT(5);
+                const uint32_t sl = flush_slots(ring, dst, F, op + btot, lane);
+                if (sl) nst = 2 * sl;
+                XT(6);
+            }
+            op += btot;
+            ip = __builtin_amdgcn_readlane(endp, int(used) - 1);
+            sb += used;
         }
     }
     if (bad) {
         if (lane == 0) atomicMax(&fb[j], whole ? FB_SERIAL : FB_REDO);
         return;
     }
-    TRACE(0xDDDD0000u | uint32_t(k), op, F, ip, out_end);
+#ifdef PF_STAMPS
+    if (lane == 0) STAMP_ADD(12, __builtin_amdgcn_s_memtime() - xt0);
+#endif
     // tail: bytes [F, op)
     for (uint32_t a = F + uint32_t(lane) * 16u; a + 16u <= op; a += 1024u)
         *reinterpret_cast<uint4*>(dst + a) = *reinterpret_cast<const uint4*>(ring + (a & XRMASK));
@@ -734,11 +931,14 @@ void launch_snappy_serial(const SnappyJob*, int, const int*, DevChunkResult*, hi
 
 // All Snappy work of one batch, in stream order. fb must be zero on entry.
 void launch_snappy(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
-                   uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, uint32_t* d_splits, int* d_fb,
-                   DevChunkResult* d_res, hipStream_t s) {
+                   SnapEnt* d_ent, uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
+                   int* d_fb, DevChunkResult* d_res, hipStream_t s) {
     if (n_jobs <= 0) return;
-    hipLaunchKernelGGL(k_snappy_index, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, d_win, d_lane_out, d_fb);
-    hipLaunchKernelGGL(k_snappy_fix, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_win, d_lane_out, d_splits, d_fb);
+    hipLaunchKernelGGL(k_snappy_index, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, d_win, d_ent, d_lane_out, d_fb);
+    hipLaunchKernelGGL(k_snappy_chain, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_win, (const SnapEnt*)d_ent, d_lane_out, d_fb);
+    hipLaunchKernelGGL(k_snappy_repair, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, (const SnapWin*)d_win, d_lane_out, d_fb);
+    hipLaunchKernelGGL(k_snappy_splits, dim3(n_jobs), dim3(64), 0, s, d_jobs, (const SnapWin*)d_win,
+                       (const uint32_t*)d_lane_out, d_splits, d_fb);
     hipLaunchKernelGGL(k_snappy_exec, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
     hipLaunchKernelGGL(k_snappy_exec, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
     launch_snappy_serial(d_jobs, n_jobs, d_fb, d_res, s);

@@ -22,9 +22,9 @@ for name, durs in per.items():
         agg[(col, kind)][name].append((d, int(size)))
 for key in sorted(agg):
     parts = []
-    for name in ("k_snappy_index", "k_snappy_fix", "k_snappy_exec", "k_snappy_serial"):
+    for name in ("k_snappy_index", "k_snappy_chain", "k_snappy_exec", "k_snappy_serial"):
         v = agg[key].get(name, [])
         if v:
             ds = [d for d, _ in v]
             parts.append(f"{name[8:]} mean {sum(ds) / len(ds) / 1e3:8.1f} max {max(ds) / 1e3:8.1f}us")
-    print(f"{key[0]:16s} {key[1]:8s} n={len(agg[key]['k_snappy_fix']):3d} " + " | ".join(parts))
+    print(f"{key[0]:16s} {key[1]:8s} n={len(agg[key]['k_snappy_chain']):3d} " + " | ".join(parts))
