@@ -61,6 +61,28 @@ struct DevPage {
     // per-page scratch: BYTE_ARRAY value positions (PLAIN) or dictionary ids
     uint32_t* aux;
     int64_t aux_cap;          // entries
+    int32_t ba_job;           // PLAIN BYTE_ARRAY data page: its BaJob (k_count fills it), else -1
+    int32_t pad_;
+};
+
+// One PLAIN BYTE_ARRAY length walk (a BYTE_ARRAY dictionary page, or the values section of a
+// PLAIN BYTE_ARRAY data page), done tile-parallel by the k_ba_* kernels (pf_pages.hip).
+enum : int32_t { BA_OK = 0, BA_FALLBACK = 1, BA_SKIP = 2 };
+struct BaJob {
+    const uint8_t* p;         // stream (data pages: set by k_count)
+    uint32_t* pos;            // out: chars start of value k
+    uint32_t* len;            // out (optional): length of value k
+    int64_t* chars_out;       // out (optional): total chars
+    uint32_t* cand;           // bitmaps over the stream, n_cap / 32 + 1 words each
+    uint32_t* link1;
+    uint32_t* link2;
+    uint32_t* tile_cnt;       // per tile: accepted positions, then their exclusive scan
+    int64_t count;            // values to read (data pages: set by k_count)
+    uint32_t n;               // stream bytes (data pages: set by k_count; <= n_cap)
+    uint32_t n_cap;           // host bound: tiles and bitmaps are sized for it
+    uint32_t n_tiles;
+    int32_t chunk, page;
+    int32_t state;            // BA_* (data pages: BA_SKIP until k_count fills the job)
 };
 
 struct DevChunk {

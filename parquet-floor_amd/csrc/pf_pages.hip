@@ -11,7 +11,7 @@
 //   K7 repetition levels -> list offsets (ParquetReader.java:200's rep stream)
 //
 // Kernels (one 256-thread workgroup per page, entries processed in tiles of TILE):
-//   k_dict_binary : BYTE_ARRAY dictionary page -> entry positions/lengths
+//   k_ba_*        : PLAIN BYTE_ARRAY length walks (dictionary pages, PLAIN data pages), tile-parallel
 //   k_count       : per data page of BYTE_ARRAY / nested chunks: slots, values, rows, chars
 //                   (+ per-value positions or dictionary ids kept in the page's aux buffer)
 //   k_scan        : per chunk: exclusive scans of the page counts -> output bases
@@ -375,15 +375,197 @@ __device__ inline int64_t binary_walk_wg(const uint8_t* p, uint64_t n, int64_t c
     return s_res;
 }
 
-// ---- k_dict_binary --------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void k_dict_binary(DevChunk* chunks, const DevPage* pages, const int* dict_chunks,
-                                                    DevChunkResult* res) {
+// ---- tile-parallel PLAIN BYTE_ARRAY walk (k_ba_*) ----------------------------------------------
+// BinaryPlainValuesReader reads <4-byte LE length><bytes> values one after another: a serial
+// chain. Spread over the whole GPU instead of one workgroup per page:
+//   k_ba_cand   every stream position q is a candidate if its length fits the stream, the
+//               position after the value is the stream end or again a fitting length, and q + 1
+//               is not plausible too (in text that pair is <char><len><0><0>: q is the char);
+//   k_ba_link   (twice) link1 = successors of candidates, link2 = successors of link1 members
+//               (position 0 is in both): a true value k >= 2 is in link2; a false candidate
+//               needs two false predecessors lined up to get there;
+//   k_ba_count / k_ba_scan  accepted = cand & link2, counted per tile, scanned per job; the total
+//               must be the page's value count;
+//   k_ba_emit   value k's chars start (and length) by rank;
+//   k_ba_verify every accepted value's end must be the next accepted value's start, value 0 at 0;
+//   k_ba_fallback  jobs that failed any check take the workgroup walk (binary_walk_wg, which ends
+//               in the exact serial walk), so results never depend on the filters.
+constexpr uint32_t BA_TILE = NT * 32;          // 8 KiB of stream per tile: one bitmap word per thread
+constexpr uint32_t BA_STAGE = BA_TILE + 32;    // + alignment shift and the lookahead of a length
+
+__device__ __forceinline__ uint32_t ba_stage(uint8_t* stg, const uint8_t* p, uint64_t n, uint64_t base) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p + base);
+    const uint32_t woff = uint32_t(a & 15u);
+    const uint4* src = reinterpret_cast<const uint4*>(a - woff);
+    const int64_t first = int64_t(base) - int64_t(woff);
+    for (uint32_t c = threadIdx.x; c < BA_STAGE / 16; c += NT) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (first + int64_t(c) * 16 < int64_t(n)) v = src[c];
+        reinterpret_cast<uint4*>(stg)[c] = v;
+    }
+    return woff;
+}
+
+__device__ __forceinline__ uint32_t lds_le32(const uint8_t* s, uint32_t a) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(s + (a & ~3u));
+    const uint32_t sh = 8u * (a & 3u);
+    return sh ? ((w[0] >> sh) | (w[1] << (32u - sh))) : w[0];
+}
+
+__global__ __launch_bounds__(NT) void k_ba_cand(BaJob* __restrict__ jobs, const int2* __restrict__ tiles) {
+    __shared__ __attribute__((aligned(16))) uint8_t stg[BA_STAGE];
+    const int2 jt = tiles[blockIdx.x];
+    const BaJob& J = jobs[jt.x];
+    if (J.state != BA_OK) return;
+    const uint32_t n = J.n;
+    const uint32_t t0 = uint32_t(jt.y) * BA_TILE;
+    if (t0 >= n) return;
+    const uint8_t* p = J.p;
+    const uint32_t woff = ba_stage(stg, p, n, t0);
+    __syncthreads();
+    const uint32_t wi = t0 / 32 + threadIdx.x;
+    const uint32_t q0 = t0 + threadIdx.x * 32u;
+    uint64_t m = 0;   // plausible positions q0 .. q0 + 32
+    for (int b = 0; b <= 32; b++) {
+        const uint32_t q = q0 + uint32_t(b);
+        if (uint64_t(q) + 4 > n) break;
+        const uint32_t l = lds_le32(stg, woff + (q - t0));
+        if (l > n - q - 4) continue;
+        const uint32_t sv = q + 4 + l;
+        bool ok = sv == n;
+        if (!ok && uint64_t(sv) + 4 <= n) {
+            const uint32_t ls = sv - t0 + 4 <= BA_TILE + 8 ? lds_le32(stg, woff + (sv - t0)) : ld32le(p, sv, n);
+            ok = ls <= n - sv - 4;
+        }
+        m |= uint64_t(ok) << b;
+    }
+    // a plausible position followed by another is the byte before a true length prefix in text
+    // (<char><len><0><0>): drop it (a true value that this drops fails the count check and takes
+    // the exact fallback walk)
+    J.cand[wi] = uint32_t(m & ~(m >> 1));
+    J.link1[wi] = wi == 0 ? 1u : 0u;
+    J.link2[wi] = wi == 0 ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(NT) void k_ba_link(BaJob* __restrict__ jobs, const int2* __restrict__ tiles, int level) {
+    __shared__ __attribute__((aligned(16))) uint8_t stg[BA_STAGE];
+    const int2 jt = tiles[blockIdx.x];
+    const BaJob& J = jobs[jt.x];
+    if (J.state != BA_OK) return;
+    const uint32_t n = J.n;
+    const uint32_t t0 = uint32_t(jt.y) * BA_TILE;
+    if (t0 >= n) return;
+    const uint32_t woff = ba_stage(stg, J.p, n, t0);
+    __syncthreads();
+    const uint32_t wi = t0 / 32 + threadIdx.x;
+    const uint32_t* cand = J.cand;
+    uint32_t* to = level == 1 ? J.link1 : J.link2;
+    uint32_t m = cand[wi];
+    if (level == 2) m &= J.link1[wi];
+    while (m) {
+        const uint32_t q = wi * 32u + uint32_t(__ffs(m) - 1);
+        m &= m - 1;
+        const uint32_t sv = q + 4 + lds_le32(stg, woff + (q - t0));
+        if (sv < n && ((cand[sv >> 5] >> (sv & 31u)) & 1u)) atomicOr(&to[sv >> 5], 1u << (sv & 31u));
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_ba_count(BaJob* __restrict__ jobs, const int2* __restrict__ tiles) {
+    __shared__ uint32_t tmp[NT / 64];
+    const int2 jt = tiles[blockIdx.x];
+    const BaJob& J = jobs[jt.x];
+    if (J.state != BA_OK) return;
+    const uint32_t t0 = uint32_t(jt.y) * BA_TILE;
+    if (t0 >= J.n) {
+        if (threadIdx.x == 0) J.tile_cnt[jt.y] = 0;
+        return;
+    }
+    const uint32_t wi = t0 / 32 + threadIdx.x;
+    uint32_t tot;
+    block_excl_scan<NT>(__popc(J.cand[wi] & J.link2[wi]), tmp, tot);
+    if (threadIdx.x == 0) J.tile_cnt[jt.y] = tot;
+}
+
+__global__ __launch_bounds__(NT) void k_ba_scan(BaJob* __restrict__ jobs) {
+    __shared__ uint32_t tmp[NT / 64];
+    BaJob& J = jobs[blockIdx.x];
+    if (J.state != BA_OK) return;
+    uint64_t run = 0;
+    for (uint32_t b = 0; b < J.n_tiles; b += NT) {
+        const uint32_t i = b + threadIdx.x;
+        const uint32_t v = i < J.n_tiles ? J.tile_cnt[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<NT>(v, tmp, tot);
+        if (i < J.n_tiles) J.tile_cnt[i] = uint32_t(run) + ex;
+        run += tot;
+    }
+    if (threadIdx.x == 0 && int64_t(run) != J.count) {
+        J.state = BA_FALLBACK;
+        PSTAMP(14, 1);
+        PSTAMP(15, run > uint64_t(J.count) ? run - uint64_t(J.count) : 0);
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_ba_emit(BaJob* __restrict__ jobs, const int2* __restrict__ tiles) {
+    __shared__ uint32_t tmp[NT / 64];
+    const int2 jt = tiles[blockIdx.x];
+    const BaJob& J = jobs[jt.x];
+    if (J.state != BA_OK) return;
+    const uint32_t n = J.n;
+    const uint32_t t0 = uint32_t(jt.y) * BA_TILE;
+    if (t0 >= n) return;
+    const uint32_t wi = t0 / 32 + threadIdx.x;
+    uint32_t m = J.cand[wi] & J.link2[wi];
+    uint32_t tot;
+    uint64_t k = uint64_t(J.tile_cnt[jt.y]) + block_excl_scan<NT>(__popc(m), tmp, tot);
+    const uint64_t count = uint64_t(J.count);
+    while (m) {
+        const uint32_t q = wi * 32u + uint32_t(__ffs(m) - 1);
+        m &= m - 1;
+        if (k < count) {
+            J.pos[k] = q + 4;
+            if (J.len) J.len[k] = ld32le(J.p, q, n);
+        }
+        k++;
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_ba_verify(BaJob* __restrict__ jobs, const int2* __restrict__ tiles) {
+    __shared__ uint32_t tmp[NT / 64];
+    const int2 jt = tiles[blockIdx.x];
+    BaJob& J = jobs[jt.x];
+    if (J.state != BA_OK) return;
+    const uint32_t n = J.n;
+    const uint32_t t0 = uint32_t(jt.y) * BA_TILE;
+    if (t0 >= n) return;
+    const uint32_t wi = t0 / 32 + threadIdx.x;
+    uint32_t m = J.cand[wi] & J.link2[wi];
+    uint32_t tot;
+    uint64_t k = uint64_t(J.tile_cnt[jt.y]) + block_excl_scan<NT>(__popc(m), tmp, tot);
+    const uint64_t count = uint64_t(J.count);
+    int bad = 0;
+    while (m) {
+        const uint32_t q = wi * 32u + uint32_t(__ffs(m) - 1);
+        m &= m - 1;
+        const uint32_t nq = q + 4 + ld32le(J.p, q, n);
+        if (k == 0 && q != 0) bad = 1;
+        if (k + 1 < count) bad |= J.pos[k + 1] != nq + 4;
+        else if (k + 1 == count) { if (J.chars_out) *J.chars_out = int64_t(nq) - 4 * int64_t(count); }
+        else bad = 1;
+        k++;
+    }
+    if (__syncthreads_or(bad) && threadIdx.x == 0) { atomicExch(&J.state, int32_t(BA_FALLBACK)); PSTAMP(6, 1); }
+}
+
+__global__ __launch_bounds__(NT) void k_ba_fallback(BaJob* __restrict__ jobs, DevChunkResult* res) {
     __shared__ BinWalkLds W;
-    const int c = dict_chunks[blockIdx.x];
-    DevChunk& ck = chunks[c];
-    const DevPage& pg = pages[ck.dict_page];
-    const int64_t t = binary_walk_wg(pg.body, pg.body_len, ck.dict_n, ck.dict_pos, ck.dict_len, W);
-    if (t < 0 && threadIdx.x == 0) set_status(res, c, ST_CORRUPT, ck.dict_page);
+    BaJob& J = jobs[blockIdx.x];
+    if (J.state != BA_FALLBACK) return;
+    const int64_t t = binary_walk_wg(J.p, J.n, J.count, J.pos, J.len, W);
+    if (threadIdx.x == 0) {
+        if (t < 0) set_status(res, J.chunk, ST_CORRUPT, J.page);
+        else if (J.chars_out) *J.chars_out = t;
+    }
 }
 
 // ---- values helpers ------------------------------------------------------------------------
@@ -391,7 +573,7 @@ __device__ __forceinline__ bool is_dict_enc(int e) { return e == 2 || e == 8; }
 
 // ---- k_count ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                              const int* page_list, DevChunkResult* res) {
+                                              const int* page_list, DevChunkResult* res, BaJob* bajobs) {
     __shared__ LevelLds L;
     __shared__ Piece pval[TILE];
     __shared__ uint32_t ids[TILE];
@@ -399,7 +581,6 @@ __global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunk
     __shared__ RleState sval;
     __shared__ int npval, verr;
     __shared__ unsigned long long chars_acc;
-    __shared__ BinWalkLds W;
 
     const int pi = page_list[blockIdx.x];
     DevPage& pg = pages[pi];
@@ -463,16 +644,18 @@ __global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunk
     }
     if (L.err || verr) { if (threadIdx.x == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
     if (binary && !dict) {
-        if (pg.encoding != 0) {
+        if (pg.encoding != 0 || pg.ba_job < 0) {
             if (threadIdx.x == 0) set_status(res, pg.chunk, ST_ENCODING, pi);
             return;
         }
-        const int64_t tot = binary_walk_wg(s.val, s.val_n, int64_t(vals), pg.aux, nullptr, W);
-        if (tot < 0) {
-            if (threadIdx.x == 0) set_status(res, pg.chunk, ST_CORRUPT, pi);
-            return;
+        if (threadIdx.x == 0) {   // the value chain is walked by the k_ba_* kernels
+            BaJob& J = bajobs[pg.ba_job];
+            J.p = s.val;
+            J.n = uint32_t(min<uint64_t>(s.val_n, J.n_cap));
+            J.count = int64_t(vals);
+            J.state = vals > 0 ? BA_OK : BA_SKIP;
+            chars_acc = 0;
         }
-        if (threadIdx.x == 0) chars_acc = uint64_t(tot);
         __syncthreads();
     }
     __syncthreads();
@@ -1093,13 +1276,21 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
 }
 
 // ---- launchers -------------------------------------------------------------------------------
-void launch_dict_binary(DevChunk* d_chunks, const DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
-                        hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_dict_binary, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res);
-}
 void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
-                  hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_count, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res);
+                  BaJob* d_bajobs, hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(k_count, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res, d_bajobs);
+}
+// PLAIN BYTE_ARRAY walks of jobs [0, n_jobs) over tiles [0, n_tiles).
+void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevChunkResult* d_res, hipStream_t st) {
+    if (n_jobs <= 0 || n_tiles <= 0) return;
+    hipLaunchKernelGGL(k_ba_cand, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
+    hipLaunchKernelGGL(k_ba_link, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles, 1);
+    hipLaunchKernelGGL(k_ba_link, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles, 2);
+    hipLaunchKernelGGL(k_ba_count, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
+    hipLaunchKernelGGL(k_ba_scan, dim3(n_jobs), dim3(NT), 0, st, d_jobs);
+    hipLaunchKernelGGL(k_ba_emit, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
+    hipLaunchKernelGGL(k_ba_verify, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
+    hipLaunchKernelGGL(k_ba_fallback, dim3(n_jobs), dim3(NT), 0, st, d_jobs, d_res);
 }
 void launch_scan(DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                  uint8_t* arena, uint64_t cap, unsigned long long* used, hipStream_t st) {

@@ -4,7 +4,7 @@
 // any set of column chunks (a row group's selected columns, or several row groups): the host
 // turns the descriptors into flat DevChunk / DevPage / SnappyJob tables, uploads them in one
 // copy, and enqueues
-//   k_snappy -> k_dict_binary -> k_delta -> k_count -> k_scan -> k_decode
+//   k_snappy -> k_ba (dictionaries) -> k_delta -> k_count -> k_ba (PLAIN pages) -> k_scan -> k_flat -> k_decode
 // on the context stream. Nothing synchronises until pf_wait.
 #include <hip/hip_runtime.h>
 
@@ -24,9 +24,9 @@
 namespace pf {
 void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, const int2*, int, uint32_t*,
                    int*, DevChunkResult*, hipStream_t);
-void launch_dict_binary(DevChunk*, const DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
-void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, BaJob*, hipStream_t);
 void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
 void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
@@ -70,7 +70,8 @@ struct HostBuf {
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-constexpr int N_EVENTS = 9;   // h2d, snappy, dict, delta, count, scan, flat, decode
+constexpr int N_EVENTS = 9;
+constexpr uint32_t BA_TILE_BYTES = 8192;   // pf_pages.hip BA_TILE   // h2d, snappy, dict, delta, count, scan, flat, decode
 
 }  // namespace
 
@@ -90,6 +91,9 @@ struct pf_ctx {
     std::vector<SnappyJob> jobs;
     std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode;
     std::vector<int2> wins, pieces;       // Snappy index windows / 64 KiB pieces (job, index)
+    std::vector<BaJob> bajobs;             // PLAIN BYTE_ARRAY walks: dictionary pages, then data pages
+    std::vector<int2> ba_tiles;            // (job relative to its batch, tile)
+    int n_ba_dict = 0, n_ba_dict_tiles = 0;
     uint32_t n_splits = 0;
     SnapWin* d_win = nullptr;              // in d_tokmap: bitmap | lane outs | windows | entry tables
     SnapEnt* d_ent = nullptr;
@@ -99,7 +103,7 @@ struct pf_ctx {
     std::vector<pf_column_info> info;
     size_t bits_bytes = 0;
     size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
-    size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0;
+    size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0, off_bajobs = 0, off_batiles = 0;
     uint64_t chars_need = 0;
     const uint8_t* d_bytes = nullptr;
     int reruns = 0;
@@ -159,11 +163,17 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_snappy(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent, ctx->d_lane_out, d_pieces,
                   int(ctx->pieces.size()), d_splits, d_fallback, d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
-    launch_dict_binary(d_chunks, d_pages, d_dictbin, int(ctx->l_dictbin.size()), d_res, st);
+    BaJob* d_bajobs = reinterpret_cast<BaJob*>(meta + ctx->off_bajobs);
+    const int2* d_batiles = reinterpret_cast<const int2*>(meta + ctx->off_batiles);
+    const int n_ba = int(ctx->bajobs.size()), n_bt = int(ctx->ba_tiles.size());
+    (void)d_dictbin;
+    launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], st));
     launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], st));
-    launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, st);
+    launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st);
+    launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
+              d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[5], st));
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
@@ -221,6 +231,14 @@ int upload_meta(pf_ctx* ctx) {
     std::memcpy(h + ctx->off_pieces, ctx->pieces.data(), sizeof(int2) * ctx->pieces.size());
     std::memset(h + ctx->off_splits, 0xff, sizeof(uint32_t) * ctx->n_splits);
     std::memcpy(h + ctx->off_wins, ctx->wins.data(), sizeof(int2) * ctx->wins.size());
+    {   // data-page walks report their chars into the page record
+        BaJob* bj = reinterpret_cast<BaJob*>(h + ctx->off_bajobs);
+        std::memcpy(bj, ctx->bajobs.data(), sizeof(BaJob) * ctx->bajobs.size());
+        uint8_t* dpages = static_cast<uint8_t*>(ctx->d_meta.p) + ctx->off_pages;
+        for (size_t i = size_t(ctx->n_ba_dict); i < ctx->bajobs.size(); i++)
+            bj[i].chars_out = reinterpret_cast<int64_t*>(dpages + sizeof(DevPage) * size_t(bj[i].page) + offsetof(DevPage, n_chars));
+        std::memcpy(h + ctx->off_batiles, ctx->ba_tiles.data(), sizeof(int2) * ctx->ba_tiles.size());
+    }
     int* lists = reinterpret_cast<int*>(h + ctx->off_lists);
     size_t lo = 0;
     for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_flat, &ctx->l_decode}) {
@@ -382,6 +400,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                 if (is_dict && (dict_global >= 0 || ck.n_pages > 0)) { hs = PF_ERR_CORRUPT_PAGE; break; }
                 DevPage pg{};
                 pg.chunk = c;
+                pg.ba_job = -1;
                 pg.encoding = pd.encoding; pg.def_enc = pd.def_encoding; pg.rep_enc = pd.rep_encoding;
                 pg.num_values = pd.num_values;
                 pg.flags = (v2 ? PG_V2 : 0) | (is_dict ? PG_DICT : 0);
@@ -451,6 +470,32 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             if (cd.max_rep > 0) { op.def = take(out, entries); op.rep = take(out, entries); }
         }
     }
+    // ---- PLAIN BYTE_ARRAY walk jobs: dictionary pages first, then PLAIN data pages ----
+    ctx->bajobs.clear();
+    ctx->ba_tiles.clear();
+    std::vector<size_t> ba_bm;
+    for (int pass = 0; pass < 2; pass++) {
+        for (size_t i = 0; i < ctx->pages.size(); i++) {
+            DevPage& pg = ctx->pages[i];
+            const DevChunk& ck = ctx->chunks[pg.chunk];
+            if (ck.ptype != PF_BYTE_ARRAY || ctx->host_status[pg.chunk] != 0) continue;
+            const bool is_dict = pg.flags & PG_DICT;
+            if (pass == 0 ? !is_dict : (is_dict || pg.encoding != PF_ENC_PLAIN)) continue;
+            BaJob J{};
+            J.n_cap = pg.body_len;
+            J.n_tiles = std::max<uint32_t>(1u, (pg.body_len + BA_TILE_BYTES - 1) / BA_TILE_BYTES);
+            J.chunk = pg.chunk;
+            J.page = int32_t(i);
+            J.state = BA_SKIP;
+            const size_t words = size_t(J.n_tiles) * (BA_TILE_BYTES / 32);
+            ba_bm.push_back(take(scratch, 4 * (3 * words + J.n_tiles), 256));
+            const int rel = int(ctx->bajobs.size()) - (pass == 0 ? 0 : ctx->n_ba_dict);
+            for (uint32_t t = 0; t < J.n_tiles; t++) ctx->ba_tiles.push_back(int2{rel, int(t)});
+            if (pass == 1) pg.ba_job = int32_t(ctx->bajobs.size());
+            ctx->bajobs.push_back(J);
+        }
+        if (pass == 0) { ctx->n_ba_dict = int(ctx->bajobs.size()); ctx->n_ba_dict_tiles = int(ctx->ba_tiles.size()); }
+    }
     // ---- allocate arenas ----
     HIPCHK(ctx, ctx->d_scratch.ensure(std::max<size_t>(scratch, 1)));
     HIPCHK(ctx, ctx->d_out.ensure(std::max<size_t>(out, 1)));
@@ -483,6 +528,26 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     ck.dict_len = ck.dict_pos + (pg.num_values + 1);
                 }
             }
+        }
+    }
+    for (size_t b = 0; b < ctx->bajobs.size(); b++) {
+        BaJob& J = ctx->bajobs[b];
+        const size_t words = size_t(J.n_tiles) * (BA_TILE_BYTES / 32);
+        J.cand = reinterpret_cast<uint32_t*>(S + ba_bm[b]);
+        J.link1 = J.cand + words;
+        J.link2 = J.link1 + words;
+        J.tile_cnt = J.link2 + words;
+        const DevPage& pg = ctx->pages[J.page];
+        if (int(b) < ctx->n_ba_dict) {
+            const DevChunk& ck = ctx->chunks[J.chunk];
+            J.p = pg.body;
+            J.n = pg.body_len;
+            J.count = ck.dict_n;
+            J.pos = ck.dict_pos;
+            J.len = ck.dict_len;
+            J.state = ck.dict_n > 0 ? BA_OK : BA_SKIP;
+        } else {
+            J.pos = pg.aux;   // p, n, count, state: k_count
         }
     }
     for (int c = 0; c < n_chunks; c++) {
@@ -526,6 +591,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);
     ctx->off_fallback = take(m, sizeof(int) * ctx->jobs.size());
     ctx->off_wins = take(m, sizeof(int2) * ctx->wins.size());
+    ctx->off_bajobs = take(m, sizeof(BaJob) * ctx->bajobs.size());
+    ctx->off_batiles = take(m, sizeof(int2) * ctx->ba_tiles.size());
     m = take(m, 256) + 256;   // arena counter lives in the last 256 bytes
     ctx->meta_bytes = m;
     HIPCHK(ctx, ctx->d_meta.ensure(m));

@@ -21,5 +21,5 @@ buf = (C.c_ulonglong * 16)()
 f(buf, 16, 1)
 got = decode_file(path, row_groups=[0])
 f(buf, 16, 0)
-names = ["calls", "tiles", "fallbacks", "walk_cyc", "serial_cyc", "cap", "entry", "chainbreak", "short", "ph_stage", "ph_cand", "ph_link", "ph_accept", "ph_check"]
+names = ["calls", "tiles", "fallbacks", "walk_cyc", "serial_cyc", "cap", "ba_verify_fail", "chainbreak", "short", "ph_stage", "ph_cand", "ph_link", "ph_accept", "ph_check", "ba_count_mismatch", "ba_excess"]
 print({k: int(buf[i]) for i, k in enumerate(names)}, "status", got["_status"])
