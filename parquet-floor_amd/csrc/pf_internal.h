@@ -63,7 +63,13 @@ struct DevPage {
     int64_t aux_cap;          // entries
     int32_t ba_job;           // PLAIN BYTE_ARRAY data page: its BaJob (k_count fills it), else -1
     int32_t pad_;
+    uint32_t* runtab;         // dictionary data page of a flat chunk: id run table (k_runs), else null
 };
+
+// k_runs run table of a page: {nruns, values covered, all levels present, valid}, then nruns
+// entries {first | packed << 31, RLE value or bit offset}; a run's count is the next first - first.
+constexpr uint32_t RT_CAP = 1024;
+constexpr uint32_t RT_BYTES = 16 + 8 * RT_CAP;
 
 // One PLAIN BYTE_ARRAY length walk (a BYTE_ARRAY dictionary page, or the values section of a
 // PLAIN BYTE_ARRAY data page), done tile-parallel by the k_ba_* kernels (pf_pages.hip).

@@ -569,6 +569,15 @@ __global__ __launch_bounds__(NT) void k_ba_fallback(BaJob* __restrict__ jobs, De
 }
 
 // ---- values helpers ------------------------------------------------------------------------
+constexpr uint32_t FBLK = 4096;      // entries per k_flat workgroup: pages are split into blocks
+
+// BYTE_ARRAY data pages: chars of the entries before each FBLK block (k_count, dictionary pages),
+// kept after the page's aux entries.
+__device__ __forceinline__ uint64_t* flat_block_chars(const DevPage& pg) {
+    if (!pg.aux) return nullptr;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(pg.aux + pg.aux_cap + 1);
+    return reinterpret_cast<uint64_t*>((a + 7) & ~uintptr_t(7));
+}
 __device__ __forceinline__ bool is_dict_enc(int e) { return e == 2 || e == 8; }
 
 // ---- k_count ---------------------------------------------------------------------------------
@@ -600,8 +609,10 @@ __global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunk
     const bool binary = ck.ptype == 6;
     const int id_bw = (dict && s.val_n > 0) ? int(s.val[0]) : 0;
     uint64_t slots = 0, vals = 0, rows = 0;
+    uint64_t* blk_chars = flat_block_chars(pg);
     for (uint64_t e0 = 0; e0 < uint64_t(pg.num_values); e0 += TILE) {
         uint32_t want = uint32_t(min<uint64_t>(TILE, uint64_t(pg.num_values) - e0));
+        if (binary && dict && blk_chars && e0 % FBLK == 0 && threadIdx.x == 0) blk_chars[e0 / FBLK] = chars_acc;
         decode_level_tile(L, s, ck, e0, want);
         if (L.err) break;
         uint32_t ns = 0, nv = 0, nr = 0;
@@ -987,14 +998,21 @@ struct Run {
 };
 
 // Walk RLE/bit-packed hybrid run headers of p[0..n) (parquet-mr RunLengthBitPackingHybridDecoder)
-// until `limit` values are covered. Returns 0 covered, 1 stream ended or corrupt first, 2 table full.
-__device__ int walk_runs(const uint8_t* p, uint64_t n, int bw, uint32_t limit, Run* runs, int cap, int& nruns,
-                         uint32_t& covered) {
-    uint64_t pos = 0;
+// from the walker state (pos = next header, first = index of its first value) until `limit`
+// values are covered. Runs that end at or before `lo` are skipped, the others are stored. Returns
+// 0 covered (covered = limit), 1 stream ended or corrupt first, 2 table full (covered = end of the
+// last stored run; the state points after it).
+struct RunWalk {
+    uint64_t pos;
+    uint32_t first;
+};
+
+__device__ int walk_runs(const uint8_t* p, uint64_t n, int bw, uint32_t lo, uint32_t limit, Run* runs, int cap,
+                         int& nruns, uint32_t& covered, RunWalk& st) {
     nruns = 0;
-    covered = 0;
-    while (covered < limit) {
-        uint64_t h;
+    covered = st.first;
+    while (st.first < limit) {
+        uint64_t pos = st.pos, h;
         if (!uvarint(p, n, pos, h)) return 1;
         Run r;
         uint64_t cnt;
@@ -1014,14 +1032,66 @@ __device__ int walk_runs(const uint8_t* p, uint64_t n, int bw, uint32_t limit, R
             r.data = v;
             r.packed = 0;
         }
-        if (cnt == 0) continue;
-        if (nruns == cap) return 2;
-        r.first = covered;
-        r.count = uint32_t(cnt < uint64_t(limit - covered) ? cnt : uint64_t(limit - covered));
-        runs[nruns++] = r;
-        covered += r.count;
+        if (cnt == 0) { st.pos = pos; continue; }
+        const uint32_t c = uint32_t(cnt < uint64_t(limit - st.first) ? cnt : uint64_t(limit - st.first));
+        if (st.first + c > lo) {
+            if (nruns == cap) return 2;
+            r.first = st.first;
+            r.count = c;
+            runs[nruns++] = r;
+            covered = st.first + c;
+        } else {
+            covered = st.first + c;
+        }
+        st.pos = pos;
+        st.first += c;
     }
     return 0;
+}
+
+// Definition levels of p[0..n): 1 if every one of the `ne` levels is max_def (RLE runs only),
+// 0 otherwise (or corrupt: the single-workgroup path reports it).
+__device__ int all_present(const uint8_t* p, uint64_t n, int bw, uint32_t ne, uint32_t max_def) {
+    uint64_t pos = 0;
+    uint32_t covered = 0;
+    while (covered < ne) {
+        uint64_t h;
+        if (!uvarint(p, n, pos, h)) return 0;
+        if (h & 1) return 0;
+        const int nbv = (bw + 7) >> 3;
+        if (pos + nbv > n) return 0;
+        uint32_t v = 0;
+        for (int b = 0; b < nbv; b++) v |= uint32_t(p[pos + b]) << (8 * b);
+        pos += nbv;
+        if ((h >> 1) == 0) continue;
+        if (v != max_def) return 0;
+        covered += uint32_t(min<uint64_t>(h >> 1, uint64_t(ne - covered)));
+    }
+    return 1;
+}
+
+// Unaligned loads from global memory as aligned dwords + v_alignbyte (the dwords covering
+// [p, p + 4 or 8) plus up to 3 following bytes must be readable).
+__device__ __forceinline__ uint32_t ld_u32_any(const uint8_t* p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    const uint32_t sh = uint32_t(a & 3u);
+    if (!sh) return q[0];
+    return __builtin_amdgcn_alignbyte(q[1], q[0], sh);   // byte shift
+}
+__device__ __forceinline__ uint64_t ld_u64_any(const uint8_t* p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    const uint32_t sh = uint32_t(a & 3u);
+    const uint32_t d0 = q[0], d1 = q[1];
+    if (!sh) return uint64_t(d0) | (uint64_t(d1) << 32);
+    const uint32_t d2 = q[2];
+    return uint64_t(__builtin_amdgcn_alignbyte(d1, d0, sh)) | (uint64_t(__builtin_amdgcn_alignbyte(d2, d1, sh)) << 32);
+}
+// LSB-first bit field of width w <= 32 starting at bit `sh` (< 8) of p (12 bytes readable from p).
+__device__ __forceinline__ uint32_t bits_fast(const uint8_t* p, uint32_t sh, int w) {
+    const uint64_t v = ld_u64_any(p) >> sh;
+    return uint32_t(v & (w == 32 ? 0xffffffffull : ((1ull << w) - 1ull)));
 }
 
 // Index of the run holding value i (runs sorted by `first`, runs[0].first == 0).
@@ -1083,6 +1153,51 @@ __device__ inline void copy_chars(const uint32_t* coff, const uint32_t* csrc, ui
     }
 }
 
+// One 128-thread workgroup per dictionary data page of a flat chunk: walks the page's
+// dictionary-id run headers ONCE (wave 1) and checks whether every definition level is present
+// (wave 0), so that k_flat's blocks of the page load a ready run table instead of each walking
+// the headers from the page start.
+__global__ __launch_bounds__(128) void k_runs(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                              const int* __restrict__ list, DevChunkResult* res) {
+    __shared__ Run R[RUN_CAP];
+    __shared__ int s_allp, s_nr, s_res;
+    __shared__ uint32_t s_cov;
+    const int pi = list[blockIdx.x];
+    DevPage& pg = pages[pi];
+    uint32_t* T = pg.runtab;
+    if (!T) return;
+    const DevChunk& ck = chunks[pg.chunk];
+    const int tid = threadIdx.x;
+    Sections s;
+    if (res[pg.chunk].status != 0 || !page_sections(pg, ck, s) || s.val_n == 0 || s.val[0] > 32) {
+        if (tid == 0) T[3] = 0;
+        return;
+    }
+    const uint32_t ne = uint32_t(pg.num_values);
+    const int id_bw = int(s.val[0]);
+    if (tid == 0) {
+        s_allp = ck.max_def == 0 ? 1 : (s.def_rle ? all_present(s.def, s.def_n, bit_width(ck.max_def), ne, uint32_t(ck.max_def)) : 0);
+    } else if (tid == 64) {
+        RunWalk st{0, 0};
+        int nr = 0;
+        uint32_t cov = 0;
+        s_res = walk_runs(s.val + 1, s.val_n - 1, id_bw, 0, ne, R, RUN_CAP, nr, cov, st);
+        s_nr = nr;
+        s_cov = cov;
+    }
+    __syncthreads();
+    const int nr = s_nr;
+    if (s_res == 2 || !s_allp) {   // too many runs for the table / levels with nulls: blocks walk themselves
+        if (tid == 0) T[3] = 0;
+        return;
+    }
+    for (int i = tid; i < nr; i += 128) {
+        T[4 + 2 * i] = R[i].first | (R[i].packed << 31);
+        T[5 + 2 * i] = R[i].data;
+    }
+    if (tid == 0) { T[0] = uint32_t(nr); T[1] = s_cov; T[2] = 1u; T[3] = 1u; }
+}
+
 struct FlatLds {
     Run drun[RUN_CAP];
     Run vrun[RUN_CAP];
@@ -1090,14 +1205,99 @@ struct FlatLds {
     uint32_t csrc[FT];
     uint32_t vbits[FT / 32 + 2];
     uint32_t scan_tmp[NT / 64];
-    int ndrun, nvrun, dres, vres;
-    uint32_t dcover, vcover;
+    RunWalk dst, vst;
+    int ndrun, nvrun, dres, vres, allp;
+    uint32_t dcover, vcover, vlo;
 };
 
+// k_flat, all levels present, fixed-width values: value index = entry index, lane-consecutive
+// entries so every load and store of a wave is one contiguous run of memory. Returns err.
+__device__ int flat_present_fixed(FlatLds& S, const DevChunk& ck, const DevPage& pg, const Sections& s, bool dict,
+                                  bool boolean, int enc, int w, const uint8_t* ids, uint64_t ids_n, int id_bw,
+                                  uint64_t slot_base, uint32_t e_begin, uint32_t e_end) {
+    const int tid = threadIdx.x;
+    const uint8_t* vend = s.val + s.val_n;
+    const bool dalign = dict && (reinterpret_cast<uintptr_t>(ck.dict_data) & uintptr_t(w - 1)) == 0;
+    for (uint32_t e0 = e_begin; e0 < e_end; e0 += FT) {
+        const uint32_t want = min(uint32_t(FT), e_end - e0);
+        int bad = 0;
+        if (dict) {
+            if ((S.vlo > e0 || e0 + want > S.vcover) && S.vres == 2) {
+                __syncthreads();
+                if (tid == 0) {   // next window of runs (re-walk from the page start)
+                    S.vst = RunWalk{0, 0};
+                    S.vlo = e0;
+                    S.vres = walk_runs(ids, ids_n, id_bw, e0, e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst);
+                }
+                __syncthreads();
+            }
+            if (id_bw > 32 || s.val_n == 0 || ck.dict_data == nullptr || e0 + want > S.vcover || S.vlo > e0) bad = 1;
+            if (!bad && uint32_t(tid) < (want + 63) / 64) S.coff[tid] = uint32_t(run_find(S.vrun, S.nvrun, e0 + tid * 64));
+            __syncthreads();
+        }
+        if (!bad) {
+            #pragma unroll 2
+            for (uint32_t k = 0; k < FEPT; k++) {
+                const uint32_t e = e0 + k * NT + uint32_t(tid);
+                if (e >= e0 + want) break;
+                uint8_t* dst = ck.values + (slot_base + e) * uint64_t(w);
+                if (dict) {
+                    int r = int(S.coff[(e - e0) >> 6]);
+                    while (e >= S.vrun[r].first + S.vrun[r].count) r++;
+                    const Run R = S.vrun[r];
+                    uint32_t id = R.data;
+                    if (R.packed) {
+                        const uint64_t bit = uint64_t(R.data) + uint64_t(e - R.first) * uint64_t(id_bw);
+                        id = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
+                                                      : bits_le(ids, ids_n, bit, id_bw);
+                    }
+                    if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
+                    const uint8_t* src = ck.dict_data + uint64_t(id) * uint64_t(w);
+                    if (w == 8 && dalign) *reinterpret_cast<uint64_t*>(dst) = *reinterpret_cast<const uint64_t*>(src);
+                    else if (w == 4 && dalign) *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(src);
+                    else copy_value(dst, src, w);
+                } else if (boolean) {
+                    if ((e >> 3) >= s.val_n) { bad = 1; continue; }
+                    dst[0] = uint8_t((s.val[e >> 3] >> (e & 7)) & 1u);
+                } else if (enc == 0) {
+                    if ((uint64_t(e) + 1) * uint64_t(w) > s.val_n) { bad = 1; continue; }
+                    const uint8_t* src = s.val + uint64_t(e) * uint64_t(w);
+                    if (w == 8 && src + 12 <= vend) *reinterpret_cast<uint64_t*>(dst) = ld_u64_any(src);
+                    else if (w == 4 && src + 8 <= vend) *reinterpret_cast<uint32_t*>(dst) = ld_u32_any(src);
+                    else copy_value(dst, src, w);
+                } else {   // DELTA_BINARY_PACKED, decoded by k_delta into aux
+                    const uint64_t* dv = reinterpret_cast<const uint64_t*>(pg.aux);
+                    if (w == 8) *reinterpret_cast<uint64_t*>(dst) = dv[e];
+                    else *reinterpret_cast<uint32_t*>(dst) = uint32_t(dv[e]);
+                }
+            }
+        }
+        if (ck.max_def > 0 && ck.validity) {   // all present: the tile's validity bits are ones
+            const uint64_t b0 = slot_base + e0, b1 = b0 + want;
+            uint32_t* vw = reinterpret_cast<uint32_t*>(ck.validity);
+            for (uint64_t wd = (b0 >> 5) + tid; wd <= ((b1 - 1) >> 5); wd += NT) {
+                const uint64_t lo = max(b0, wd << 5), hi = min(b1, (wd + 1) << 5);
+                const uint32_t m = uint32_t((hi - lo >= 32 ? 0xffffffffull : ((1ull << (hi - lo)) - 1ull)) << (lo & 31));
+                if (lo == (wd << 5) && hi == ((wd + 1) << 5)) vw[wd] = m;
+                else atomicOr(vw + wd, m);
+            }
+        }
+        if (__syncthreads_or(bad)) return 1;
+    }
+    return 0;
+}
+
+// One workgroup per (page, FBLK block of entries). Pages whose levels are all present (max_def
+// == 0 or RLE runs of max_def) are decoded block by block in parallel: value index = entry
+// index, each block walks the dictionary-id run headers up to its own range (windowed when a
+// block needs more than RUN_CAP runs) and takes its chars base from k_count's block table or,
+// for PLAIN BYTE_ARRAY, from the value positions. Pages with nulls are decoded by block 0 alone.
 __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                             const int* page_list, DevChunkResult* res) {
+                                             const int2* __restrict__ blocks, DevChunkResult* res) {
     __shared__ FlatLds S;
-    const int pi = page_list[blockIdx.x];
+    const int2 pbk = blocks[blockIdx.x];
+    const int pi = pbk.x;
+    const uint32_t blk = uint32_t(pbk.y);
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
@@ -1117,36 +1317,94 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
     const int bwd = bit_width(ck.max_def);
     const uint32_t ne = uint32_t(pg.num_values);
     const int id_bw = (dict && s.val_n > 0) ? int(s.val[0]) : 0;
+    const uint8_t* ids = dict && s.val_n > 0 ? s.val + 1 : s.val;
+    const uint64_t ids_n = dict && s.val_n > 0 ? s.val_n - 1 : 0;
+    const bool counted = ck.needs_count != 0;
+    const uint64_t slot_base = uint64_t(pg.entry_start);   // flat: slot == entry
+    if (blk > 0 && blk * FBLK >= ne) return;
+    const uint32_t* T = pg.runtab;
+    const bool tab = T != nullptr && T[3] == 1u && T[0] <= uint32_t(RUN_CAP);   // k_runs: levels all present
+    if (tid == 0) S.allp = tab ? 1 : (ck.max_def == 0 ? 1 : all_present(s.def, s.def_n, bwd, ne, uint32_t(ck.max_def)));
+    __syncthreads();
+    const bool split = S.allp;
+    if (!split && blk > 0) return;                          // block 0 decodes the whole page
+    const uint32_t e_begin = split ? blk * FBLK : 0u;
+    const uint32_t e_end = split ? min(ne, e_begin + FBLK) : ne;
+#ifdef PF_STAMPS
+    const unsigned long long ft0 = __builtin_amdgcn_s_memtime();
+    if (tid == 0) { PSTAMP(0, 1); if (dict) PSTAMP(6, 1); if (binary) PSTAMP(7, 1); }
+#endif
     if (tid == 0) {
         S.ndrun = 0; S.dcover = ne; S.dres = 0;
-        if (ck.max_def > 0) S.dres = walk_runs(s.def, s.def_n, bwd, ne, S.drun, RUN_CAP, S.ndrun, S.dcover);
-    } else if (tid == 64) {
-        S.nvrun = 0; S.vcover = 0; S.vres = 0;
+        if (!split && ck.max_def > 0) {
+            S.dst = RunWalk{0, 0};
+            S.dres = walk_runs(s.def, s.def_n, bwd, 0, ne, S.drun, RUN_CAP, S.ndrun, S.dcover, S.dst);
+        }
+    } else if (tid == 64 && !(split && tab)) {
+        S.nvrun = 0; S.vcover = 0; S.vres = 0; S.vlo = e_begin;
+        S.vst = RunWalk{0, 0};
         if (dict && s.val_n > 0 && id_bw <= 32)
-            S.vres = walk_runs(s.val + 1, s.val_n - 1, id_bw, ne, S.vrun, RUN_CAP, S.nvrun, S.vcover);
+            S.vres = walk_runs(ids, ids_n, id_bw, e_begin, split ? e_end : ne, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst);
+    }
+    if (split && tab) {   // the page's run table (k_runs), loaded by all threads
+        const uint32_t nr = T[0], cov = T[1];
+        for (uint32_t i = tid; i < nr; i += NT) {
+            const uint32_t f = T[4 + 2 * i];
+            const uint32_t nf = i + 1 < nr ? (T[4 + 2 * (i + 1)] & 0x7fffffffu) : cov;
+            Run r;
+            r.first = f & 0x7fffffffu;
+            r.count = nf - r.first;
+            r.data = T[5 + 2 * i];
+            r.packed = f >> 31;
+            S.vrun[i] = r;
+        }
+        if (tid == 0) { S.nvrun = int(nr); S.vcover = cov; S.vlo = 0; S.vres = cov >= ne ? 0 : 1; }
     }
     __syncthreads();
-    if (S.dres == 2 || S.vres == 2) return;                // too many runs: k_decode takes the page
+#ifdef PF_STAMPS
+    unsigned long long ft1 = __builtin_amdgcn_s_memtime();
+    if (tid == 0) PSTAMP(2, ft1 - ft0);
+#endif
+    if (!split && (S.dres == 2 || S.vres == 2)) return;    // too many runs: k_decode takes the page
     bool allp = true, lvl_bad = S.dres != 0;
-    for (int r = 0; r < S.ndrun; r++) {
-        const Run& R = S.drun[r];
-        if (R.packed || R.data != uint32_t(ck.max_def)) allp = false;
-        if (!R.packed && R.data > uint32_t(ck.max_def)) lvl_bad = true;
+    if (!split) {
+        for (int r = 0; r < S.ndrun; r++) {
+            const Run& R = S.drun[r];
+            if (R.packed || R.data != uint32_t(ck.max_def)) allp = false;
+            if (!R.packed && R.data > uint32_t(ck.max_def)) lvl_bad = true;
+        }
     }
     if (lvl_bad) {
         if (tid == 0) { set_status(res, pg.chunk, ST_CORRUPT, pi); pg.done = 1; }
         return;
     }
-    const uint8_t* ids = dict && s.val_n > 0 ? s.val + 1 : s.val;
-    const uint64_t ids_n = dict && s.val_n > 0 ? s.val_n - 1 : 0;
-    const bool counted = ck.needs_count != 0;
-    const uint64_t slot_base = uint64_t(pg.entry_start);   // flat: slot == entry
-    uint64_t char_base = counted ? uint64_t(pg.char_start) : 0;
-    uint64_t vidx = 0;                                      // page-relative index of the next present value
+    uint64_t char_base = 0;
+    if (binary && counted) {
+        char_base = uint64_t(pg.char_start);
+        if (e_begin > 0) {
+            if (dict) char_base += flat_block_chars(pg)[blk];
+            else char_base += uint64_t(pg.aux[e_begin]) - 4ull * (uint64_t(e_begin) + 1);
+        }
+    }
+    uint64_t vidx = e_begin;                                // page-relative index of the next present value
     int err = 0;
 
-    for (uint32_t e0 = 0; e0 < ne; e0 += FT) {
-        const uint32_t want = min(uint32_t(FT), ne - e0);
+    if (split && !binary) {
+        err = flat_present_fixed(S, ck, pg, s, dict, boolean, enc, w, ids, ids_n, id_bw, slot_base, e_begin, e_end);
+#ifdef PF_STAMPS
+        if (tid == 0) { const unsigned long long dt_ = __builtin_amdgcn_s_memtime() - ft0; PSTAMP(1, dt_); atomicMax(&pf_pstamps[9], dt_); }
+#endif
+        if (tid == 0) {
+            if (err) set_status(res, pg.chunk, ST_CORRUPT, pi);
+            else if (!counted) atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values),
+                                         (unsigned long long)(e_end - e_begin));
+            pg.done = 1;
+        }
+        return;
+    }
+
+    for (uint32_t e0 = e_begin; e0 < e_end; e0 += FT) {
+        const uint32_t want = min(uint32_t(FT), e_end - e0);
         const uint32_t eb = uint32_t(tid) * FEPT;
         for (uint32_t i = tid; i < FT / 32 + 2; i += NT) S.vbits[i] = 0;
         // ---- definition levels -> present bits of this thread's entries
@@ -1171,10 +1429,20 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
         uint32_t vo;
         if (allp) { vo = min(eb, want); tv = want; }
         else vo = block_excl_scan<NT>(__popc(fv), S.scan_tmp, tv);
-        // ---- dictionary / stream checks that need the value count
+        // ---- dictionary: this tile's values [vidx, vidx + tv) must be in the run table
         if (tv > 0 && dict) {
+            if (split && (uint64_t(S.vlo) > vidx || vidx + tv > uint64_t(S.vcover)) && S.vres == 2) {
+                __syncthreads();
+                if (tid == 0) {   // next window of runs (re-walk from the page start)
+                    S.vst = RunWalk{0, 0};
+                    S.vlo = uint32_t(vidx);
+                    S.vres = walk_runs(ids, ids_n, id_bw, uint32_t(vidx), e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover,
+                                       S.vst);
+                }
+                __syncthreads();
+            }
             if (id_bw > 32 || s.val_n == 0 || (binary ? ck.dict_pos == nullptr : ck.dict_data == nullptr) ||
-                vidx + tv > uint64_t(S.vcover))
+                vidx + tv > uint64_t(S.vcover) || uint64_t(S.vlo) > vidx)
                 bad = 1;
         }
         if (__syncthreads_or(bad)) { err = 1; break; }
@@ -1221,7 +1489,7 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
                         const uint32_t id = run_value(S.vrun[vr], ids, ids_n, uint32_t(gv), id_bw);
                         if (int64_t(id) >= ck.dict_n) bad = 1;
                         else { src = ck.dict_pos[id]; l = ck.dict_len[id]; }
-                    } else {   // PLAIN: value positions from k_count's walk
+                    } else {   // PLAIN: value positions from the k_ba walk
                         const uint32_t p = pg.aux[gv];
                         const uint32_t ln = (p >= 4 && p <= s.val_n) ? ld32le(s.val, p - 4, s.val_n) : 0xffffffffu;
                         if (ln <= s.val_n - p) { src = p; l = ln; }
@@ -1261,16 +1529,30 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
             if (sh + FEPT > 32 && sh) atomicOr(&S.vbits[(rb >> 5) + 1], fv >> (32 - sh));
         }
         __syncthreads();
+#ifdef PF_STAMPS
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) { PSTAMP(4, t_ - ft1); PSTAMP(3, 1); } ft1 = t_; }
+#endif
         if (binary) copy_chars(S.coff, S.csrc, tv, tchars, dict ? ck.dict_data : s.val, ck.chars + char_base);
         if (ck.max_def > 0 && ck.validity) flush_bits(S.vbits, slot_base + e0, want, ck.validity);
         vidx += tv;
         char_base += tchars;
         __syncthreads();
+#ifdef PF_STAMPS
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) PSTAMP(5, t_ - ft1); ft1 = t_; }
+#endif
     }
+#ifdef PF_STAMPS
+    if (tid == 0) {
+        const unsigned long long dt_ = __builtin_amdgcn_s_memtime() - ft0;
+        PSTAMP(1, dt_);
+        atomicMax(&pf_pstamps[binary ? 8 : 9], dt_);
+        if (!split) PSTAMP(10, 1);
+    }
+#endif
     if (tid == 0) {
         if (err) set_status(res, pg.chunk, ST_CORRUPT, pi);
         else if (!counted) atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values),
-                                     (unsigned long long)vidx);
+                                     (unsigned long long)(vidx - e_begin));
         pg.done = 1;
     }
 }
@@ -1296,9 +1578,14 @@ void launch_scan(DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n,
                  uint8_t* arena, uint64_t cap, unsigned long long* used, hipStream_t st) {
     if (n > 0) hipLaunchKernelGGL(k_scan, dim3(n), dim3(64), 0, st, d_chunks, d_pages, d_list, d_res, arena, cap, used);
 }
-void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
+void launch_runs(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                  hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res);
+    if (n > 0) hipLaunchKernelGGL(k_runs, dim3(n), dim3(128), 0, st, d_chunks, d_pages, d_list, d_res);
+}
+void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
+                 hipStream_t st) {   // d_list: n (page, block) pairs
+    if (n > 0)
+        hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, reinterpret_cast<const int2*>(d_list), d_res);
 }
 void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                    hipStream_t st) {

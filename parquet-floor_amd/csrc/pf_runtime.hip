@@ -29,6 +29,7 @@ void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, h
 void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, BaJob*, hipStream_t);
 void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
 void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 }  // namespace pf
 
@@ -71,7 +72,8 @@ struct HostBuf {
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 constexpr int N_EVENTS = 9;
-constexpr uint32_t BA_TILE_BYTES = 8192;   // pf_pages.hip BA_TILE   // h2d, snappy, dict, delta, count, scan, flat, decode
+constexpr uint32_t BA_TILE_BYTES = 8192;   // pf_pages.hip BA_TILE
+constexpr int64_t FLAT_BLK = 4096;         // pf_pages.hip FBLK   // h2d, snappy, dict, delta, count, scan, flat, decode
 
 }  // namespace
 
@@ -89,7 +91,7 @@ struct pf_ctx {
     std::vector<DevChunk> chunks;          // host copies (device pointers)
     std::vector<DevPage> pages;
     std::vector<SnappyJob> jobs;
-    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode;
+    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode, l_runs;
     std::vector<int2> wins, pieces;       // Snappy index windows / 64 KiB pieces (job, index)
     std::vector<BaJob> bajobs;             // PLAIN BYTE_ARRAY walks: dictionary pages, then data pages
     std::vector<int2> ba_tiles;            // (job relative to its batch, tile)
@@ -152,6 +154,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     int* d_scan = lists + lo; lo += ctx->l_scan.size();
     int* d_flat = lists + lo; lo += ctx->l_flat.size();
     int* d_decode = lists + lo; lo += ctx->l_decode.size();
+    int* d_runs = lists + lo; lo += ctx->l_runs.size();
     unsigned long long* used = reinterpret_cast<unsigned long long*>(meta + ctx->meta_bytes - 256);
     const int2* d_pieces = reinterpret_cast<const int2*>(meta + ctx->off_pieces);
     uint32_t* d_splits = reinterpret_cast<uint32_t*>(meta + ctx->off_splits);
@@ -170,6 +173,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], st));
     launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), d_res, st);
+    launch_runs(d_chunks, d_pages, d_runs, int(ctx->l_runs.size()), d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], st));
     launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st);
     launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
@@ -178,7 +182,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], st));
-    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size()), d_res, st);
+    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], st));
     launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[8], st));
@@ -241,7 +245,7 @@ int upload_meta(pf_ctx* ctx) {
     }
     int* lists = reinterpret_cast<int*>(h + ctx->off_lists);
     size_t lo = 0;
-    for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_flat, &ctx->l_decode}) {
+    for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_flat, &ctx->l_decode, &ctx->l_runs}) {
         std::copy(v->begin(), v->end(), lists + lo);
         lo += v->size();
     }
@@ -346,6 +350,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->chunks.assign(n_chunks, DevChunk{});
     ctx->pages.clear(); ctx->jobs.clear();
     ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_flat.clear(); ctx->l_decode.clear();
+    ctx->l_runs.clear();
     ctx->wins.clear(); ctx->pieces.clear(); ctx->n_splits = 0;
     ctx->host_status.assign(n_chunks, 0);
     ctx->info.assign(n_chunks, pf_column_info{});
@@ -363,7 +368,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->d_bytes = d_bytes;
 
     // ---- plan: sizes of scratch / outputs ----
-    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; };
+    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; };
     std::vector<PagePlan> pplan;
     size_t scratch = 0, out = 0, bits = 0;
     uint64_t chars_hint = 0;
@@ -411,7 +416,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     hs = PF_ERR_CORRUPT_PAGE; break;
                 }
                 bool compressed = cd.codec == PF_CODEC_SNAPPY && (!v2 || pd.is_compressed);
-                PagePlan pp{0, ~0ull, is_dict};
+                PagePlan pp{0, ~0ull, is_dict, ~0ull};
                 if (v2) { pg.lvl = src; pg.rep_len = uint32_t(pd.rep_bytes); pg.def_len = uint32_t(pd.def_bytes); }
                 if (compressed) {
                     pp.scratch_off = take(scratch, pd.uncompressed_size - lvl, 16);
@@ -439,10 +444,14 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     pg.entry_start = entries;
                     entries += pd.num_values;
                     ck.n_pages++;
-                    if (cd.physical_type == PF_BYTE_ARRAY) pp.aux_off = take(scratch, 4ull * pd.num_values + 4, 256);
+                    if (cd.physical_type == PF_BYTE_ARRAY)   // value positions / ids + per-block chars (k_flat)
+                        pp.aux_off = take(scratch, 4ull * pd.num_values + 16 + 8ull * (uint64_t(pd.num_values) / FLAT_BLK + 2), 256);
                     else if (pd.encoding == PF_ENC_DELTA_BINARY_PACKED && (cd.physical_type == PF_INT32 || cd.physical_type == PF_INT64))
                         pp.aux_off = take(scratch, 8ull * pd.num_values + 8, 256);
                     if (cd.physical_type == PF_BYTE_ARRAY) chars_hint += pd.uncompressed_size;
+                    if (cd.max_rep == 0 && cd.physical_type != PF_BOOLEAN &&
+                        (pd.encoding == PF_ENC_PLAIN_DICTIONARY || pd.encoding == PF_ENC_RLE_DICTIONARY))
+                        pp.rt_off = take(scratch, RT_BYTES, 256);   // k_runs table
                 }
                 pplan.push_back(pp);
                 ctx->pages.push_back(pg);
@@ -520,6 +529,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                 pg.aux = reinterpret_cast<uint32_t*>(S + pp.aux_off);
                 pg.aux_cap = pg.num_values;
             }
+            if (pp.rt_off != ~0ull) {
+                pg.runtab = reinterpret_cast<uint32_t*>(S + pp.rt_off);
+                ctx->l_runs.push_back(int(i));
+            }
             DevChunk& ck = ctx->chunks[pg.chunk];
             if (pp.is_dict) {
                 ck.dict_data = pg.body;
@@ -571,7 +584,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         const DevChunk& ck = ctx->chunks[pg.chunk];
         if (pg.encoding == PF_ENC_DELTA_BINARY_PACKED && pg.aux && ck.ptype != PF_BYTE_ARRAY) ctx->l_delta.push_back(int(i));
         if (ck.needs_count) ctx->l_count.push_back(int(i));
-        if (ck.max_rep == 0) ctx->l_flat.push_back(int(i));
+        if (ck.max_rep == 0) {   // (page, block) pairs
+            const int nb = std::max(1, int((int64_t(pg.num_values) + FLAT_BLK - 1) / FLAT_BLK));
+            for (int b = 0; b < nb; b++) { ctx->l_flat.push_back(int(i)); ctx->l_flat.push_back(b); }
+        }
         ctx->l_decode.push_back(int(i));
     }
     // ---- Snappy tables: 8 KiB index windows, 64 KiB pieces ----
@@ -585,7 +601,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_pages = take(m, sizeof(DevPage) * ctx->pages.size());
     ctx->off_jobs = take(m, sizeof(SnappyJob) * ctx->jobs.size());
     ctx->off_lists = take(m, sizeof(int) * (ctx->l_dictbin.size() + ctx->l_delta.size() + ctx->l_count.size() +
-                                            ctx->l_scan.size() + ctx->l_flat.size() + ctx->l_decode.size()));
+                                            ctx->l_scan.size() + ctx->l_flat.size() + ctx->l_decode.size() + ctx->l_runs.size()));
     ctx->off_res = take(m, sizeof(DevChunkResult) * n_chunks);
     ctx->off_pieces = take(m, sizeof(int2) * ctx->pieces.size());
     ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);

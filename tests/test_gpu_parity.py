@@ -158,3 +158,41 @@ def test_corrupt_pages_error_not_fault(decoder, tmp_path):
     # still healthy afterwards
     got = decode_file(os.path.join(GOLDEN, "ref_roundtrip.parquet"), decoder=decoder)
     assert got["_status"] == 0
+
+
+def _big_file(tmp_path, rows, nulls):
+    """pyarrow-written file with pages of 20K entries (> one k_flat block of 4096), a dictionary
+    column in RLE runs of 9 (> RUN_CAP runs per block: windowed run tables), PLAIN and dictionary
+    strings, doubles and an INT64 key; generated at test time (pyarrow is in the image)."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    rng = np.random.default_rng(11)
+    key = np.arange(rows, dtype=np.int64) // 3
+    runs = (np.repeat(np.arange(rows // 9 + 1) % 50, 9)[:rows]).astype(np.int32)
+    dbl = rng.random(rows)
+    vocab = np.array([f"w{i:05d}" * (1 + i % 4) for i in range(700)])
+    sdict = vocab[rng.integers(0, 700, rows)]
+    text = np.array([f"comment {i} " + "x" * int(rng.integers(0, 30)) for i in range(rows)])
+    cols = {"key": key, "runs": runs, "dbl": dbl, "sdict": sdict, "text": text}
+    arrays = {}
+    for k, v in cols.items():
+        mask = (rng.random(rows) < 0.3) if nulls else None
+        arrays[k] = pa.array(v, mask=mask)
+    t = pa.table(arrays)
+    path = str(tmp_path / f"big_{rows}_{int(nulls)}.parquet")
+    pq.write_table(t, path, compression="snappy", row_group_size=rows // 2,
+                   use_dictionary=["runs", "sdict", "key"], data_page_size=1 << 20)
+    return path
+
+
+@pytest.mark.parametrize("nulls", [False, True])
+def test_gpu_multiblock_pages_match_oracle(decoder, oracle, tmp_path, nulls):
+    from pfloor.decoder import decode_file
+    path = _big_file(tmp_path, 120000, nulls)
+    got = decode_file(path, decoder=decoder)
+    with oracle.open(path) as of:
+        for rg in range(of.num_row_groups):
+            for c in range(of.num_columns):
+                g = got[(rg, c)]
+                assert g["status"] == 0, (rg, c, got["_error"])
+                assert_chunk_equal(g, of.decode(rg, c), f"big rg{rg} c{c} nulls={nulls}")
