@@ -62,7 +62,7 @@ struct DevPage {
     uint32_t* aux;
     int64_t aux_cap;          // entries
     int32_t ba_job;           // PLAIN BYTE_ARRAY data page: its BaJob (k_count fills it), else -1
-    int32_t pad_;
+    int32_t counted;          // 1: k_count_flat counted the page (k_count skips it)
     uint32_t* runtab;         // dictionary data page of a flat chunk: id run table (k_runs), else null
 };
 

@@ -595,6 +595,7 @@ __global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunk
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     if (res[pg.chunk].status != 0) return;   // an earlier stage failed this chunk
+    if (pg.counted == 1) return;                 // counted by k_count_flat
     Sections s;
     const bool ok = page_sections(pg, ck, s);
     if (threadIdx.x == 0) {
@@ -1088,6 +1089,12 @@ __device__ __forceinline__ uint64_t ld_u64_any(const uint8_t* p) {
     const uint32_t d2 = q[2];
     return uint64_t(__builtin_amdgcn_alignbyte(d1, d0, sh)) | (uint64_t(__builtin_amdgcn_alignbyte(d2, d1, sh)) << 32);
 }
+__device__ __forceinline__ uint64_t ld64_bytes(const uint8_t* p) {
+    uint64_t v = 0;
+    #pragma unroll
+    for (int k = 0; k < 8; k++) v |= uint64_t(p[k]) << (8 * k);
+    return v;
+}
 // LSB-first bit field of width w <= 32 starting at bit `sh` (< 8) of p (12 bytes readable from p).
 __device__ __forceinline__ uint32_t bits_fast(const uint8_t* p, uint32_t sh, int w) {
     const uint64_t v = ld_u64_any(p) >> sh;
@@ -1198,6 +1205,98 @@ __global__ __launch_bounds__(128) void k_runs(const DevChunk* __restrict__ chunk
     if (tid == 0) { T[0] = uint32_t(nr); T[1] = s_cov; T[2] = 1u; T[3] = 1u; }
 }
 
+// k_count for flat BYTE_ARRAY pages whose levels are all present: slots = rows = values =
+// entries; dictionary strings sum their chars over the run table (k_runs) FBLK entries at a time,
+// which also gives k_flat's per-block chars bases; PLAIN pages hand their value chain to the k_ba
+// walk. Every thread's loads are independent (no run-header walk). Marks the page counted
+// (pg.counted) so k_count skips it; pages it leaves alone (nulls, corrupt) go through k_count.
+__global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                   const int* __restrict__ page_list, DevChunkResult* res,
+                                                   BaJob* bajobs) {
+    __shared__ Run R[RUN_CAP];
+    __shared__ int s_ok;
+    __shared__ unsigned long long s_acc;
+    const int pi = page_list[blockIdx.x];
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    const int tid = threadIdx.x;
+    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.ptype != 6) return;
+    Sections s;
+    if (!page_sections(pg, ck, s)) return;
+    const bool dict = is_dict_enc(pg.encoding);
+    const uint32_t ne = uint32_t(pg.num_values);
+    const uint32_t* T = pg.runtab;
+    uint64_t total = 0;
+    if (dict) {
+        if (!(T != nullptr && T[3] == 1u && T[0] <= uint32_t(RUN_CAP) && T[1] >= ne) || !ck.dict_len || s.val_n == 0)
+            return;
+        const uint32_t nr = T[0], cov = T[1];
+        for (uint32_t i = tid; i < nr; i += NT) {
+            const uint32_t f = T[4 + 2 * i];
+            const uint32_t nf = i + 1 < nr ? (T[4 + 2 * (i + 1)] & 0x7fffffffu) : cov;
+            Run r;
+            r.first = f & 0x7fffffffu;
+            r.count = nf - r.first;
+            r.data = T[5 + 2 * i];
+            r.packed = f >> 31;
+            R[i] = r;
+        }
+        const uint8_t* ids = s.val + 1;
+        const uint64_t ids_n = s.val_n - 1;
+        const int id_bw = int(s.val[0]);
+        uint64_t* bc = flat_block_chars(pg);
+        int bad = 0;
+        __syncthreads();
+        for (uint32_t b0 = 0; b0 < ne; b0 += FBLK) {
+            const uint32_t b1 = min(ne, b0 + FBLK);
+            if (tid == 0) s_acc = 0;
+            __syncthreads();
+            uint64_t acc = 0;
+            int r = -1;
+            for (uint32_t e = b0 + uint32_t(tid); e < b1; e += NT) {
+                if (r < 0) r = run_find(R, int(nr), e);
+                while (e >= R[r].first + R[r].count) r++;
+                const Run& Rr = R[r];
+                uint32_t id = Rr.data;
+                if (Rr.packed) {
+                    const uint64_t bit = uint64_t(Rr.data) + uint64_t(e - Rr.first) * uint64_t(id_bw);
+                    id = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
+                                                  : bits_le(ids, ids_n, bit, id_bw);
+                }
+                if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
+                acc += ck.dict_len[id];
+            }
+            atomicAdd(&s_acc, (unsigned long long)acc);
+            __syncthreads();
+            if (tid == 0 && bc) bc[b0 / FBLK] = total;
+            total += s_acc;
+            __syncthreads();
+        }
+        if (__syncthreads_or(bad)) return;   // k_count reports the bad id
+    } else {
+        if (pg.encoding != 0 || pg.ba_job < 0) return;
+        if (tid == 0)
+            s_ok = ck.max_def == 0 ? 1
+                                   : (s.def_rle ? all_present(s.def, s.def_n, bit_width(ck.max_def), ne, uint32_t(ck.max_def)) : 0);
+        __syncthreads();
+        if (!s_ok) return;
+        if (tid == 0) {   // the value chain is walked by the k_ba_* kernels
+            BaJob& J = bajobs[pg.ba_job];
+            J.p = s.val;
+            J.n = uint32_t(min<uint64_t>(s.val_n, J.n_cap));
+            J.count = int64_t(ne);
+            J.state = ne > 0 ? BA_OK : BA_SKIP;
+        }
+    }
+    if (tid == 0) {
+        pg.n_slots = int64_t(ne);
+        pg.n_values = int64_t(ne);
+        pg.n_rows = int64_t(ne);
+        pg.n_chars = int64_t(total);
+        pg.counted = 1;
+    }
+}
+
 struct FlatLds {
     Run drun[RUN_CAP];
     Run vrun[RUN_CAP];
@@ -1212,7 +1311,16 @@ struct FlatLds {
 
 // k_flat, all levels present, fixed-width values: value index = entry index, lane-consecutive
 // entries so every load and store of a wave is one contiguous run of memory. Returns err.
-__device__ int flat_present_fixed(FlatLds& S, const DevChunk& ck, const DevPage& pg, const Sections& s, bool dict,
+struct FixedLds {
+    Run vrun[RUN_CAP];
+    uint32_t coff[FT / 64];
+    RunWalk vst;
+    int nvrun, vres, allp;
+    uint32_t vcover, vlo;
+};
+
+template <class Lds>
+__device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg, const Sections& s, bool dict,
                                   bool boolean, int enc, int w, const uint8_t* ids, uint64_t ids_n, int id_bw,
                                   uint64_t slot_base, uint32_t e_begin, uint32_t e_end) {
     const int tid = threadIdx.x;
@@ -1235,7 +1343,58 @@ __device__ int flat_present_fixed(FlatLds& S, const DevChunk& ck, const DevPage&
             if (!bad && uint32_t(tid) < (want + 63) / 64) S.coff[tid] = uint32_t(run_find(S.vrun, S.nvrun, e0 + tid * 64));
             __syncthreads();
         }
-        if (!bad) {
+        const bool wide = w == 4 || w == 8;
+        if (!bad && wide && ((dict && dalign) || enc == 0 || enc == 5)) {
+            // batched: the loads of FB entries per thread are in flight together
+            constexpr uint32_t FB = FEPT / 2;
+            for (uint32_t kb = 0; kb < FEPT; kb += FB) {
+            uint64_t v[FB];
+            uint32_t id[FB];
+            #pragma unroll
+            for (uint32_t k = 0; k < FB; k++) {
+                const uint32_t e = e0 + (kb + k) * NT + uint32_t(tid);
+                id[k] = 0;
+                v[k] = 0;
+                if (e >= e0 + want) continue;
+                if (dict) {
+                    int r = int(S.coff[(e - e0) >> 6]);
+                    while (e >= S.vrun[r].first + S.vrun[r].count) r++;
+                    const Run R = S.vrun[r];
+                    id[k] = R.data;
+                    if (R.packed) {
+                        const uint64_t bit = uint64_t(R.data) + uint64_t(e - R.first) * uint64_t(id_bw);
+                        id[k] = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
+                                                         : bits_le(ids, ids_n, bit, id_bw);
+                    }
+                } else if (enc == 0) {
+                    if ((uint64_t(e) + 1) * uint64_t(w) > s.val_n) { bad = 1; continue; }
+                    const uint8_t* src = s.val + uint64_t(e) * uint64_t(w);
+                    if (w == 8) v[k] = src + 12 <= vend ? ld_u64_any(src) : ld64_bytes(src);
+                    else v[k] = src + 8 <= vend ? ld_u32_any(src) : ld32le(src, 0, 4);
+                } else {
+                    v[k] = reinterpret_cast<const uint64_t*>(pg.aux)[e];
+                }
+            }
+            if (dict) {
+                #pragma unroll
+                for (uint32_t k = 0; k < FB; k++) {
+                    const uint32_t e = e0 + (kb + k) * NT + uint32_t(tid);
+                    if (e >= e0 + want) continue;
+                    if (int64_t(id[k]) >= ck.dict_n) { bad = 1; continue; }
+                    const uint8_t* src = ck.dict_data + uint64_t(id[k]) * uint64_t(w);
+                    v[k] = w == 8 ? *reinterpret_cast<const uint64_t*>(src) : *reinterpret_cast<const uint32_t*>(src);
+                }
+            }
+            #pragma unroll
+            for (uint32_t k = 0; k < FB; k++) {
+                const uint32_t e = e0 + (kb + k) * NT + uint32_t(tid);
+                if (e >= e0 + want) continue;
+                uint8_t* dst = ck.values + (slot_base + e) * uint64_t(w);
+                if (w == 8) *reinterpret_cast<uint64_t*>(dst) = v[k];
+                else *reinterpret_cast<uint32_t*>(dst) = uint32_t(v[k]);
+            }
+            }
+        } else if (!bad) {
             #pragma unroll 2
             for (uint32_t k = 0; k < FEPT; k++) {
                 const uint32_t e = e0 + k * NT + uint32_t(tid);
@@ -1287,6 +1446,81 @@ __device__ int flat_present_fixed(FlatLds& S, const DevChunk& ck, const DevPage&
     return 0;
 }
 
+// k_flat for fixed-width pages whose levels are all present (the common case), with a small LDS
+// footprint and its own register budget: one workgroup per (page, FBLK block). Marks the page
+// done; k_flat decodes everything else (strings, pages with nulls).
+__global__ __launch_bounds__(NT) void k_flat_fixed(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                   const int2* __restrict__ blocks, DevChunkResult* res) {
+    __shared__ FixedLds S;
+    const int2 pbk = blocks[blockIdx.x];
+    const int pi = pbk.x;
+    const uint32_t blk = uint32_t(pbk.y);
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    const int tid = threadIdx.x;
+    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.ptype == 6) return;
+    Sections s;
+    if (!page_sections(pg, ck, s)) return;
+    const int enc = pg.encoding;
+    const bool boolean = ck.ptype == 0, dict = is_dict_enc(enc);
+    const int w = ck.width;
+    bool take = ck.max_def == 0 || s.def_rle;
+    if (enc == 0) {
+    } else if (dict) take = take && !boolean;
+    else if (enc == 5) take = take && (ck.ptype == 1 || ck.ptype == 2) && pg.aux != nullptr;
+    else take = false;
+    if (!take) return;
+    const uint32_t ne = uint32_t(pg.num_values);
+    if (blk > 0 && blk * FBLK >= ne) return;
+    const int id_bw = (dict && s.val_n > 0) ? int(s.val[0]) : 0;
+    const uint8_t* ids = dict && s.val_n > 0 ? s.val + 1 : s.val;
+    const uint64_t ids_n = dict && s.val_n > 0 ? s.val_n - 1 : 0;
+    const uint32_t* T = pg.runtab;
+    const bool tab = T != nullptr && T[3] == 1u && T[0] <= uint32_t(RUN_CAP);   // k_runs: levels all present
+    if (tid == 0)
+        S.allp = tab ? 1 : (ck.max_def == 0 ? 1 : all_present(s.def, s.def_n, bit_width(ck.max_def), ne, uint32_t(ck.max_def)));
+    __syncthreads();
+    if (!S.allp) return;
+    const uint32_t e_begin = blk * FBLK;
+    const uint32_t e_end = min(ne, e_begin + FBLK);
+#ifdef PF_STAMPS
+    const unsigned long long ft0 = __builtin_amdgcn_s_memtime();
+#endif
+    if (dict) {
+        if (tab) {
+            const uint32_t nr = T[0], cov = T[1];
+            for (uint32_t i = tid; i < nr; i += NT) {
+                const uint32_t f = T[4 + 2 * i];
+                const uint32_t nf = i + 1 < nr ? (T[4 + 2 * (i + 1)] & 0x7fffffffu) : cov;
+                Run r;
+                r.first = f & 0x7fffffffu;
+                r.count = nf - r.first;
+                r.data = T[5 + 2 * i];
+                r.packed = f >> 31;
+                S.vrun[i] = r;
+            }
+            if (tid == 0) { S.nvrun = int(nr); S.vcover = cov; S.vlo = 0; S.vres = cov >= ne ? 0 : 1; }
+        } else if (tid == 0) {
+            S.nvrun = 0; S.vcover = 0; S.vres = 0; S.vlo = e_begin;
+            S.vst = RunWalk{0, 0};
+            if (s.val_n > 0 && id_bw <= 32)
+                S.vres = walk_runs(ids, ids_n, id_bw, e_begin, e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst);
+        }
+        __syncthreads();
+    }
+    const int err = flat_present_fixed(S, ck, pg, s, dict, boolean, enc, w, ids, ids_n, id_bw,
+                                       uint64_t(pg.entry_start), e_begin, e_end);
+#ifdef PF_STAMPS
+    if (tid == 0) { const unsigned long long dt_ = __builtin_amdgcn_s_memtime() - ft0; PSTAMP(1, dt_); PSTAMP(0, 1); atomicMax(&pf_pstamps[9], dt_); }
+#endif
+    if (tid == 0) {
+        if (err) set_status(res, pg.chunk, ST_CORRUPT, pi);
+        else if (ck.needs_count == 0)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values), (unsigned long long)(e_end - e_begin));
+        pg.done = 1;
+    }
+}
+
 // One workgroup per (page, FBLK block of entries). Pages whose levels are all present (max_def
 // == 0 or RLE runs of max_def) are decoded block by block in parallel: value index = entry
 // index, each block walks the dictionary-id run headers up to its own range (windowed when a
@@ -1301,7 +1535,7 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
-    if (res[pg.chunk].status != 0 || ck.max_rep != 0) return;
+    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || pg.done) return;   // done: k_flat_fixed took it
     Sections s;
     if (!page_sections(pg, ck, s)) return;                 // k_decode reports it
     const int enc = pg.encoding;
@@ -1389,19 +1623,6 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
     uint64_t vidx = e_begin;                                // page-relative index of the next present value
     int err = 0;
 
-    if (split && !binary) {
-        err = flat_present_fixed(S, ck, pg, s, dict, boolean, enc, w, ids, ids_n, id_bw, slot_base, e_begin, e_end);
-#ifdef PF_STAMPS
-        if (tid == 0) { const unsigned long long dt_ = __builtin_amdgcn_s_memtime() - ft0; PSTAMP(1, dt_); atomicMax(&pf_pstamps[9], dt_); }
-#endif
-        if (tid == 0) {
-            if (err) set_status(res, pg.chunk, ST_CORRUPT, pi);
-            else if (!counted) atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values),
-                                         (unsigned long long)(e_end - e_begin));
-            pg.done = 1;
-        }
-        return;
-    }
 
     for (uint32_t e0 = e_begin; e0 < e_end; e0 += FT) {
         const uint32_t want = min(uint32_t(FT), e_end - e0);
@@ -1560,7 +1781,9 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
 // ---- launchers -------------------------------------------------------------------------------
 void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                   BaJob* d_bajobs, hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_count, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res, d_bajobs);
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_count_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res, d_bajobs);
+    hipLaunchKernelGGL(k_count, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res, d_bajobs);
 }
 // PLAIN BYTE_ARRAY walks of jobs [0, n_jobs) over tiles [0, n_tiles).
 void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevChunkResult* d_res, hipStream_t st) {
@@ -1584,8 +1807,10 @@ void launch_runs(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
 }
 void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                  hipStream_t st) {   // d_list: n (page, block) pairs
-    if (n > 0)
-        hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, reinterpret_cast<const int2*>(d_list), d_res);
+    if (n <= 0) return;
+    const int2* blocks = reinterpret_cast<const int2*>(d_list);
+    hipLaunchKernelGGL(k_flat_fixed, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
+    hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
 }
 void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                    hipStream_t st) {
