@@ -78,10 +78,12 @@ def page_stats(descs):
     return dict(pages=pages, compressed=comp, uncompressed=uncomp, snappy_in=snappy_in, snappy_out=snappy_out)
 
 
-def decoded_bytes(dec, n_chunks, pf, items):
+def decoded_bytes(decs, parts, pf, items):
     tot = 0
     rows = 0
-    for i, (rg, col, *_r) in enumerate(items):
+    for dec, idx in zip(decs, parts):
+      for i, j in enumerate(idx):
+        rg, col = items[j][0], items[j][1]
         ci = dec.info(i)
         c = pf.columns[col]
         b = ci.num_slots * ci.width
@@ -159,6 +161,8 @@ def main():
     ap.add_argument("--rows", type=int, default=SF1_ROWS)
     ap.add_argument("--data-dir", default=os.environ.get("PF_BENCH_DIR", "/tmp/pfloor_bench"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="decode contexts (HIP streams) per GPU; row groups are dealt round-robin to them")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -185,21 +189,29 @@ def main():
     torch.cuda.set_device(device)
     pf, items, host, descs = plan_file(path)
     st = page_stats(descs)
-    dec = GpuDecoder(device)
+    # S contexts on this GPU (one HIP stream each): row group r goes to context r % S, so one row
+    # group's latency-bound Snappy index / chain passes overlap another's decode kernels.
+    S = max(1, min(args.streams, pf.num_row_groups))
+    decs = [GpuDecoder(device) for _ in range(S)]
+    dec = decs[0]
+    parts = [[i for i, it in enumerate(items) if it[0] % S == k] for k in range(S)]
+    part_descs = [[descs[i] for i in idx] for idx in parts]
     L = _native.lib()
     d_in = C.c_void_p()
     _native.check(L.pf_device_alloc(dec.h, host.nbytes, C.byref(d_in)), dec.h, "pf_device_alloc")
     _native.check(L.pf_memcpy_h2d(dec.h, d_in, host.ctypes.data, host.nbytes), dec.h, "h2d")
 
     def step():
-        dec.decode(descs, d_in.value, host.nbytes, on_device=True)
-        rc = dec.wait()
-        if rc != 0:
-            raise RuntimeError(dec.error())
+        for d, dd in zip(decs, part_descs):
+            d.decode(dd, d_in.value, host.nbytes, on_device=True)
+        for d in decs:
+            rc = d.wait()
+            if rc != 0:
+                raise RuntimeError(d.error())
 
     for _ in range(args.warmup):
         step()
-    dbytes, rows = decoded_bytes(dec, len(descs), pf, items)
+    dbytes, rows = decoded_bytes(decs, parts, pf, items)
     stage_acc = {}
     torch.cuda.synchronize()
     if dist:
@@ -222,17 +234,21 @@ def main():
     n = world
     value = dbytes * n * args.steps / dt / 1e9
 
-    # roofline of the dominant kernel (HIP events on the decoder's stream)
+    # roofline of the dominant kernel stage: HIP events on context 0's stream, priced with the
+    # algorithmic bytes of context 0's share of the pages
+    st0 = page_stats(part_descs[0])
+    dbytes0, _ = decoded_bytes(decs[:1], parts[:1], pf, items)
     kern_bytes = {
-        "snappy": st["snappy_in"] + st["snappy_out"],
-        "decode": st["uncompressed"] + dbytes,   # page bodies read + decoded bytes written
+        "snappy_exec": st0["snappy_in"] + st0["snappy_out"],   # compressed read + decompressed written
+        "snappy_parse": st0["snappy_in"],                       # compressed read (token index)
+        "decode": st0["uncompressed"] + dbytes0,   # page bodies read + decoded bytes written
+        "flat": st0["uncompressed"] + dbytes0,
     }
-    dom = max(("snappy", "decode", "count", "dict", "delta", "scan"), key=lambda k: stage_ms.get(k, 0.0))
+    dom = max((k for k in stage_ms if k != "h2d"), key=lambda k: stage_ms.get(k, 0.0))
     dom_ms = stage_ms.get(dom, 0.0)
     dom_bytes = kern_bytes.get(dom)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if (dom_bytes and dom_ms > 0) else None
     b_alg = st["compressed"] + dbytes
-    gpu_ms = sum(stage_ms.get(k, 0.0) for k in ("snappy", "dict", "delta", "count", "scan", "decode"))
     out = {
         "metric": "decoded GB/s + rows/s (node), lineitem-shape Snappy+dict, 1/2/4/8 GPUs",
         "value": round(value, 3), "unit": "decoded GB/s",
@@ -245,15 +261,15 @@ def main():
                                "Snappy + dictionary, 1Mi-row row groups, device-resident",
                    "rows": rows, "row_groups": pf.num_row_groups, "compressed_page_bytes": st["compressed"],
                    "uncompressed_page_bytes": st["uncompressed"], "decoded_bytes": dbytes,
-                   "parallelism": f"row groups sharded per GPU x{n} (no collective)"},
+                   "parallelism": f"row groups sharded per GPU x{n} (no collective), {S} decode streams per GPU"},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "roofline": {"bound": "hbm", "kernel": f"k_{dom}", "achieved": round(achieved, 2) if achieved else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": None,
                      "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4)},
-        "pipeline_roofline": {"b_alg": b_alg, "gpu_ms": round(gpu_ms, 4),
-                              "achieved": round(b_alg / (gpu_ms * 1e-3) / 1e9, 2) if gpu_ms else None,
-                              "frac": round(b_alg / (gpu_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if gpu_ms else None},
+        "pipeline_roofline": {"b_alg": b_alg, "ms_per_step": round(ms_per_step, 4),
+                              "achieved": round(b_alg * n / (ms_per_step * 1e-3) / 1e9, 2),
+                              "frac": round(b_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
     }
     if rank == 0 and n == 1 and not args.no_cpu_baseline:
         try:
@@ -261,7 +277,8 @@ def main():
         except Exception as e:   # reported, never fatal
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     L.pf_device_free(dec.h, d_in)
-    dec.close()
+    for d in decs:
+        d.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -24,6 +24,9 @@
 namespace pf {
 void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, const int2*, int, uint32_t*,
                    int*, DevChunkResult*, hipStream_t);
+void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, int*,
+                         hipStream_t);
+void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*, DevChunkResult*, hipStream_t);
 void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, BaJob*, hipStream_t);
@@ -71,7 +74,7 @@ struct HostBuf {
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-constexpr int N_EVENTS = 9;
+constexpr int N_EVENTS = 10;  // h2d, snappy parse, snappy exec, dict, delta, count, scan, flat, decode
 constexpr uint32_t BA_TILE_BYTES = 8192;   // pf_pages.hip BA_TILE
 constexpr int64_t FLAT_BLK = 4096;         // pf_pages.hip FBLK   // h2d, snappy, dict, delta, count, scan, flat, decode
 
@@ -163,29 +166,31 @@ int enqueue_kernels(pf_ctx* ctx) {
 
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
-    launch_snappy(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent, ctx->d_lane_out, d_pieces,
-                  int(ctx->pieces.size()), d_splits, d_fallback, d_res, st);
+    launch_snappy_parse(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent,
+                        ctx->d_lane_out, d_splits, d_fallback, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
+    launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res, st);
+    HIPCHK(ctx, hipEventRecord(ctx->ev[3], st));
     BaJob* d_bajobs = reinterpret_cast<BaJob*>(meta + ctx->off_bajobs);
     const int2* d_batiles = reinterpret_cast<const int2*>(meta + ctx->off_batiles);
     const int n_ba = int(ctx->bajobs.size()), n_bt = int(ctx->ba_tiles.size());
     (void)d_dictbin;
     launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[3], st));
+    HIPCHK(ctx, hipEventRecord(ctx->ev[4], st));
     launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), d_res, st);
     launch_runs(d_chunks, d_pages, d_runs, int(ctx->l_runs.size()), d_res, st);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[4], st));
+    HIPCHK(ctx, hipEventRecord(ctx->ev[5], st));
     launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st);
     launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
               d_res, st);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[5], st));
+    HIPCHK(ctx, hipEventRecord(ctx->ev[6], st));
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[6], st));
-    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], st));
-    launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), d_res, st);
+    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[8], st));
+    launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), d_res, st);
+    HIPCHK(ctx, hipEventRecord(ctx->ev[9], st));
     HIPCHK(ctx, hipGetLastError());
     // results + device-written chunk fields (chars base) back to pinned host memory
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_res.p, meta + ctx->off_res, sizeof(DevChunkResult) * ctx->n_chunks,

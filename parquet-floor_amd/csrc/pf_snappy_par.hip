@@ -38,10 +38,21 @@ namespace pf {
 #ifdef PF_STAMPS
 __device__ unsigned long long pf_stamps[16];
 #define STAMP_ADD(i, v) atomicAdd(&pf_stamps[i], (unsigned long long)(v))
+__device__ unsigned long long pf_cstamps[32];
+#define CSTAMP(i, v) atomicAdd(&pf_cstamps[i], (unsigned long long)(v))
+extern "C" int pf_debug_cstamps(unsigned long long* out, int n, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_cstamps), sizeof(unsigned long long) * (n < 32 ? n : 32)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(pf_cstamps), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
 #define XT_DECL unsigned long long xt_ = __builtin_amdgcn_s_memtime()
 #define XT(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (lane == 0) STAMP_ADD(i, t_ - xt_); xt_ = t_; } while (0)
 #else
 #define STAMP_ADD(i, v) ((void)0)
+#define CSTAMP(i, v) ((void)0)
 #define XT_DECL ((void)0)
 #define XT(i) ((void)0)
 #endif
@@ -199,16 +210,16 @@ __device__ __forceinline__ uint32_t wave_sum_sat(uint32_t v) {
 
 // Exact whole-wave parse of the chain from e (a token start, W0 <= e < stop) up to the first chain
 // position >= stop, on a staged window. 64 lanes decode the token at cur + lane; the chain through
-// those 64 candidates is followed in scalar registers (readlane), so each 64-byte block costs one
-// LDS read per lane plus one scalar step per token. Token starts are OR-ed into sbits (bit i =
-// W0 + i) and output lengths added to slo[(pos - W0) / SNAP_RB] (both zeroed by the caller).
-// Returns the exit (SNAP_INVALID if the chain runs past n) and the output byte total in `out`.
+// those 64 candidates is followed in scalar registers (readlane) and its 64-bit start mask is
+// OR-ed into sbits (bit i = W0 + i) by one lane. Afterwards every lane sums the output lengths of
+// the tokens in its SNAP_RB region into slo. sbits must be zero on entry. Returns the exit
+// (SNAP_INVALID if the chain runs past n) and the output byte total in `out`.
 __device__ uint32_t seq_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t e, uint64_t stop,
                               uint32_t* sbits, uint32_t* slo, uint32_t& out) {
     const int lane = threadIdx.x & 63;
     uint64_t cur = e;
-    uint32_t acc = 0;
     out = 0;
+    bool bad = false;
     while (cur < stop) {
         const uint64_t q = cur + uint64_t(lane);
         const SnapTok t = snap_tok(lds_read8(stage, woff + uint32_t(q - W0)));
@@ -220,16 +231,32 @@ __device__ uint32_t seq_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, 
             mask |= 1ull << k;
             k += __builtin_amdgcn_readlane(tl, k);
         }
-        if ((mask >> lane) & 1ull) {
-            const uint32_t r = uint32_t(q - W0);
-            atomicOr(&sbits[r >> 5], 1u << (r & 31u));
-            atomicAdd(&slo[r / SNAP_RB], t.ol);
-            const uint32_t a = acc + t.ol;
-            acc = a < acc ? 0xffffffffu : a;
+        if (lane == 0) {
+            const uint32_t r0 = uint32_t(cur - W0), wi = r0 >> 5, sh = r0 & 31u;
+            sbits[wi] |= uint32_t(mask << sh);
+            const uint32_t m1 = sh ? uint32_t(mask >> (32u - sh)) : uint32_t(mask >> 32);
+            const uint32_t m2 = sh ? uint32_t(mask >> (64u - sh)) : 0u;
+            if (m1 && wi + 1 < SNAP_WWORDS) sbits[wi + 1] |= m1;
+            if (m2 && wi + 2 < SNAP_WWORDS) sbits[wi + 2] |= m2;
         }
         cur += k;
-        if (cur > n) return SNAP_INVALID;
+        if (cur > n) { bad = true; break; }
     }
+    __syncthreads();
+    // output bytes per lane region, from the marked tokens
+    uint32_t acc = 0;
+    #pragma unroll
+    for (int kw = 0; kw < 4; kw++) {
+        uint32_t m = sbits[lane * 4 + kw];
+        while (m) {
+            const uint32_t i = uint32_t(lane) * SNAP_RB + uint32_t(kw) * 32u + uint32_t(__ffs(m) - 1);
+            m &= m - 1;
+            const uint32_t o = snap_tok(lds_read8(stage, woff + i)).ol;
+            acc = acc + o < acc ? 0xffffffffu : acc + o;
+        }
+    }
+    slo[lane] = acc;
+    if (bad) return SNAP_INVALID;
     out = wave_sum_sat(acc);
     return uint32_t(cur);
 }
@@ -270,10 +297,16 @@ __global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict
         return;
     }
     const uint64_t wend = min(uint64_t(W0) + SNAP_WIN, n);
+#ifdef PF_STAMPS
+    unsigned long long it0 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
     __syncthreads();
     uint32_t flags;
     uint32_t X = win_parse(stage, woff, W0, n, entry, L, flags);
+#ifdef PF_STAMPS
+    { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (lane == 0) { CSTAMP(0, 1); CSTAMP(1, t_ - it0); if (flags & WIN_NOCONV) CSTAMP(2, 1); } it0 = t_; }
+#endif
     uint32_t sum;
     if (flags & WIN_NOCONV) {   // chains that do not synchronise: exact whole-wave parse instead
         reinterpret_cast<uint4*>(sbits)[lane] = make_uint4(0, 0, 0, 0);
@@ -290,6 +323,9 @@ __global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict
     }
     store_window(tm, lo, L, lane);
     if (lane == 0) win[wi] = SnapWin{entry, X, sum, flags};
+#ifdef PF_STAMPS
+    { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (lane == 0) CSTAMP(3, t_ - it0); it0 = t_; }
+#endif
     if (jw.y == 0) return;   // window 0's entry is exact: no table
     // entry table: lane d follows the chain from W0 + d until it meets this window's chain
     __syncthreads();
@@ -301,6 +337,15 @@ __global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict
                      [&](uint32_t q) { return (sbits[(q - W0) >> 5] >> ((q - W0) & 31u)) & 1u; },
                      [&](uint32_t q) { return snap_tok(lds_read8(stage, woff + (q - W0))); });
     ent[size_t(wi) * 64 + lane] = T;
+#ifdef PF_STAMPS
+    {
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();
+        if (lane == 0) CSTAMP(4, t_ - it0);
+        const unsigned long long sl = __ballot((T.pos >> 30) == ENT_SLOW);
+        if (lane == 0 && sl) CSTAMP(5, 1);
+        if (lane == 0) CSTAMP(6, __popcll(sl));
+    }
+#endif
 }
 
 #ifdef PF_SNAP_TRACE
@@ -370,6 +415,10 @@ __global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict
     const SnapWin w0 = Wn[0];
     uint32_t e = w0.exit;
     if (lane == 0) Wn[0] = SnapWin{w0.entry, w0.exit, w0.out, WM_KEEP};
+#ifdef PF_STAMPS
+    const unsigned long long cstart = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { CSTAMP(17, 1); CSTAMP(18, nw); }
+#endif
     bool bad = false;
     for (uint32_t w = 1; w < nw; w++) {
         const uint32_t W0 = w * SNAP_WIN;
@@ -384,17 +433,28 @@ __global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict
             __syncthreads();
         }
         if (uint64_t(e) >= wend) {   // inside a literal that started earlier: no token here
-            if (lane == 0) Wn[w] = SnapWin{e, e, 0, WM_SKIP};
+            if (lane == 0) { Wn[w] = SnapWin{e, e, 0, WM_SKIP}; CSTAMP(10, 1); }
             continue;
         }
         const SnapWin sw = s_win[cb];
         const uint32_t d = e - W0;
         const uint32_t* tm = job.tokmap + size_t(w) * SNAP_WWORDS;
         SnapEnt T;
+#ifdef PF_STAMPS
+        const unsigned long long ct0 = __builtin_amdgcn_s_memtime();
+#endif
         if (sw.flags & WIN_BROKEN) T = mk_ent(e, ENT_SLOW, 0);
         else if (d < 64) T = s_tab[cb * 64 + d];
-        else T = ent_walk(e, W0, wend, n, [&](uint32_t q) { return tm_get(tm, q - W0); },
-                          [&](uint32_t q) { return snap_tok(glb_read8(job.src, n, q)); });
+        else {
+            T = ent_walk(e, W0, wend, n, [&](uint32_t q) { return tm_get(tm, q - W0); },
+                         [&](uint32_t q) { return snap_tok(glb_read8(job.src, n, q)); });
+#ifdef PF_STAMPS
+            if (lane == 0) { CSTAMP(11, 1); CSTAMP(12, __builtin_amdgcn_s_memtime() - ct0); }
+#endif
+        }
+#ifdef PF_STAMPS
+        if (lane == 0) { CSTAMP(13, 1); if ((T.pos >> 30) == ENT_SLOW) CSTAMP(14, 1); if ((T.pos >> 30) == ENT_NOMERGE) CSTAMP(15, 1); }
+#endif
         const uint32_t fl = T.pos >> 30, pos = T.pos & ENT_POS;
         if (fl == ENT_BAD) { bad = true; break; }
         if (fl == ENT_MERGE) {
@@ -421,10 +481,16 @@ __global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict
         LO[size_t(w) * 64 + lane] = slo[lane];
         if (lane == 0) Wn[w] = SnapWin{e, X, sum, WM_DONE};
         e = X;
+#ifdef PF_STAMPS
+        if (lane == 0) CSTAMP(16, __builtin_amdgcn_s_memtime() - ct0);
+#endif
     }
     if (bad || uint64_t(e) != n) {
         if (lane == 0) fb[j] = FB_SERIAL;
     }
+#ifdef PF_STAMPS
+    if (lane == 0) { const unsigned long long dt_ = __builtin_amdgcn_s_memtime() - cstart; CSTAMP(19, dt_); atomicMax(&pf_cstamps[20], dt_); }
+#endif
 }
 
 // One wave per window: make the bitmap and lane output counts of windows whose true entry is not
@@ -929,19 +995,32 @@ extern "C" int pf_debug_stamps(unsigned long long* out, int n, int reset) {
 
 void launch_snappy_serial(const SnappyJob*, int, const int*, DevChunkResult*, hipStream_t);
 
-// All Snappy work of one batch, in stream order. fb must be zero on entry.
-void launch_snappy(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
-                   SnapEnt* d_ent, uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
-                   int* d_fb, DevChunkResult* d_res, hipStream_t s) {
+// Parse stage (token-start bitmaps, chain, 64 KiB split points) and execute stage, separately so
+// the runtime can time them apart.
+void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
+                         SnapEnt* d_ent, uint32_t* d_lane_out, uint32_t* d_splits, int* d_fb, hipStream_t s) {
     if (n_jobs <= 0) return;
     hipLaunchKernelGGL(k_snappy_index, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, d_win, d_ent, d_lane_out, d_fb);
     hipLaunchKernelGGL(k_snappy_chain, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_win, (const SnapEnt*)d_ent, d_lane_out, d_fb);
     hipLaunchKernelGGL(k_snappy_repair, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, (const SnapWin*)d_win, d_lane_out, d_fb);
     hipLaunchKernelGGL(k_snappy_splits, dim3(n_jobs), dim3(64), 0, s, d_jobs, (const SnapWin*)d_win,
                        (const uint32_t*)d_lane_out, d_splits, d_fb);
+}
+
+void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
+                        int* d_fb, DevChunkResult* d_res, hipStream_t s) {
+    if (n_jobs <= 0) return;
     hipLaunchKernelGGL(k_snappy_exec, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
     hipLaunchKernelGGL(k_snappy_exec, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
     launch_snappy_serial(d_jobs, n_jobs, d_fb, d_res, s);
+}
+
+// All Snappy work of one batch, in stream order. fb must be zero on entry.
+void launch_snappy(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
+                   SnapEnt* d_ent, uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
+                   int* d_fb, DevChunkResult* d_res, hipStream_t s) {
+    launch_snappy_parse(d_jobs, n_jobs, d_wins, n_wins, d_win, d_ent, d_lane_out, d_splits, d_fb, s);
+    launch_snappy_exec(d_jobs, n_jobs, d_pieces, n_pieces, d_splits, d_fb, d_res, s);
 }
 
 }  // namespace pf
