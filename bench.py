@@ -248,6 +248,17 @@ def main():
     dom_ms = stage_ms.get(dom, 0.0)
     dom_bytes = kern_bytes.get(dom)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if (dom_bytes and dom_ms > 0) else None
+    # HBM traffic of the dominant kernel: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE per
+    # launch over the whole file at 1 stream (tools/gpu_pmc.sh -> tools/pmc_traffic.json), scaled
+    # to context 0's share of the algorithmic bytes
+    traffic = None
+    try:
+        pmc = json.load(open(os.path.join(ROOT, "tools", "pmc_traffic.json")))
+        whole = {"snappy_exec": st["snappy_in"] + st["snappy_out"]}
+        if f"k_{dom}" in pmc and dom in whole and dom_bytes:
+            traffic = round(pmc[f"k_{dom}"]["traffic_bytes"] * dom_bytes / whole[dom])
+    except (OSError, ValueError, KeyError):
+        pass
     b_alg = st["compressed"] + dbytes
     out = {
         "metric": "decoded GB/s + rows/s (node), lineitem-shape Snappy+dict, 1/2/4/8 GPUs",
@@ -265,7 +276,8 @@ def main():
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "roofline": {"bound": "hbm", "kernel": f"k_{dom}", "achieved": round(achieved, 2) if achieved else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": traffic,
+                     "traffic_source": "rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE per launch (tools/gpu_pmc.sh)",
                      "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4)},
         "pipeline_roofline": {"b_alg": b_alg, "ms_per_step": round(ms_per_step, 4),
                               "achieved": round(b_alg * n / (ms_per_step * 1e-3) / 1e9, 2),
