@@ -629,14 +629,15 @@ __global__ __launch_bounds__(64) void k_snappy_splits(const SnappyJob* __restric
 // ======================================================================== executor
 
 
-constexpr uint32_t XRING = 8192;     // output ring (LDS)
+constexpr uint32_t XRING = 4096;     // output ring (LDS)
 constexpr uint32_t XRMASK = XRING - 1;
-constexpr uint32_t XSLOT = 2048;     // flush granule
+constexpr uint32_t XSLOT = 1024;     // flush granule
 constexpr uint32_t XCHUNK = 1024;    // input bytes whose tokens are enumerated at once
 constexpr uint32_t XSTAGE = XCHUNK + 64 + 16;
-constexpr uint32_t XBATCH = 2048;    // output bytes of one parallel step (ring: XBATCH + XSLOT <= XRING)
+constexpr uint32_t XBATCH = 1024;    // output bytes of one parallel step (ring: XBATCH + XSLOT <= XRING)
 constexpr uint32_t XLIT = 1024;      // long literals are copied in pieces of this many bytes
-constexpr uint32_t FBUF_W = 17;      // dwords per lane of far-copy source (64 bytes + misalignment)
+constexpr uint32_t FBUF_W = 17;      // dwords per far copy's source slot (64 bytes + misalignment)
+constexpr uint32_t XFAR = 16;        // far copies per step (the step is cut before the next one)
 
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -666,18 +667,18 @@ __device__ __forceinline__ uint32_t lanes_below(uint32_t key, uint32_t x) {
 
 __device__ __forceinline__ uint64_t lane_mask_lt(uint32_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }
 
-// Store ring bytes [F, upto) in whole XSLOT slots (16-byte stores, 32 B per lane). Returns the
-// number of slots stored (2 store instructions each).
+// Store ring bytes [F, upto) in whole XSLOT slots (16-byte stores, XSLOT / 64 bytes per lane).
+// Returns the number of store instructions issued.
+constexpr uint32_t XST = XSLOT / 64 / 16;   // 16-byte stores per lane per slot
 __device__ __forceinline__ uint32_t flush_slots(const uint8_t* ring, uint8_t* dst, uint32_t& F, uint32_t upto, int lane) {
     uint32_t nsl = 0;
     while (upto - F >= XSLOT) {
-        const uint32_t a0 = F + uint32_t(lane) * 32u;
-        const uint4 v0 = *reinterpret_cast<const uint4*>(ring + (a0 & XRMASK));
-        const uint4 v1 = *reinterpret_cast<const uint4*>(ring + ((a0 + 16u) & XRMASK));
-        *reinterpret_cast<uint4*>(dst + a0) = v0;
-        *reinterpret_cast<uint4*>(dst + a0 + 16) = v1;
+        const uint32_t a0 = F + uint32_t(lane) * (XSLOT / 64);
+        #pragma unroll
+        for (uint32_t u = 0; u < XST; u++)
+            *reinterpret_cast<uint4*>(dst + a0 + 16 * u) = *reinterpret_cast<const uint4*>(ring + ((a0 + 16 * u) & XRMASK));
         F += XSLOT;
-        nsl++;
+        nsl += XST;
     }
     return nsl;
 }
@@ -696,7 +697,10 @@ __device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {               // lane
     return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xf, 0xf, false);  // wave_shr:1
 }
 
-__device__ __forceinline__ void wait_vmem_but2() { asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
+__device__ __forceinline__ void wait_vmem_last_slot() {   // all but the last flush slot's XST stores
+    if constexpr (XST == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+}
 
 // Executor step descriptor of one token (LDS, indexed by the token's lane).
 enum : uint32_t { XD_LIT = 0, XD_NEAR = 1, XD_FAR = 2, XD_DEP = 3 };
@@ -728,7 +732,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict_
     __shared__ __attribute__((aligned(16))) uint8_t ring[XRING];
     __shared__ __attribute__((aligned(16))) uint8_t stage[XSTAGE];
     __shared__ uint16_t tokpos[XCHUNK / 2];
-    __shared__ __attribute__((aligned(16))) uint32_t fbuf[64 * FBUF_W];   // far-copy sources, one slot per lane
+    __shared__ __attribute__((aligned(16))) uint32_t fbuf[XFAR * FBUF_W];  // far-copy sources, one slot per far token
     __shared__ __attribute__((aligned(16))) XDesc desc[64];
     __shared__ uint32_t sbits[XBATCH / 32];                               // token starts of the step's output
     __shared__ uint32_t wpre[XBATCH / 32];                                // tokens starting in earlier words
@@ -823,7 +827,14 @@ __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict_
             XT(1);
             if (lane == 0) STAMP_ADD(0, 1);
             // step = tokens before the first long / unstaged literal and within XBATCH output bytes
-            const unsigned long long cutm = __ballot(take && (ol > 64u || inc > XBATCH || (kd == 0 && !lstaged)));
+            // far copies: source wholly before the step and older than the ring can hold for any
+            // step (offset-independent of where the step is cut); at most XFAR per step
+            const uint32_t a = otok - off;                       // copy source start
+            const bool farc = take && kd != 0 && a + min(ol, off) <= op && int32_t(a - (op + XBATCH - XRING)) < 0;
+            const unsigned long long farm = __ballot(farc);
+            const uint32_t frank = uint32_t(__popcll(farm & lane_mask_lt(uint32_t(lane))));
+            const unsigned long long cutm = __ballot(take && (ol > 64u || inc > XBATCH || (kd == 0 && !lstaged) ||
+                                                              (farc && frank >= XFAR)));
             const uint32_t cut = cutm ? uint32_t(__ffsll(cutm) - 1) : uint32_t(nt);
             uint32_t used, btot;
             if (cut == 0) {
@@ -845,7 +856,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict_
                     }
                     fl_slots += flush_slots(ring, dst, F, op + d0 + c, lane);
                 }
-                nst = fl_slots * 2;
+                nst = fl_slots;
                 used = 1;
                 btot = L0;
                 XT(11);
@@ -856,14 +867,13 @@ __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict_
                 const bool lit = inb && kd == 0;
                 const bool cp = inb && kd != 0;
                 if (__any(cp && (off == 0 || off > otok - out_start))) { bad = true; break; }
-                const uint32_t a = otok - off;                       // copy source start
                 const bool dep = cp && a + min(ol, off) > op;        // reads this step's output
-                const bool far = cp && !dep && int32_t(a - (op + btot - XRING)) < 0;
+                const bool far = cp && farc;
                 const bool anyfar = __any(far);
                 // far copies: issue the HBM loads of their source now (flushed output)
                 uint32_t fw[FBUF_W];
                 if (anyfar) {
-                    if (nst == 2) wait_vmem_but2();   // all but the last slot's stores have landed
+                    if (nst == XST) wait_vmem_last_slot();   // all but the last slot's stores have landed
                     else wait_vmem();
                     const uint32_t* fsrc = reinterpret_cast<const uint32_t*>(dst + (a & ~3u));
                     const uint32_t nwd = far ? ((a & 3u) + ol + 3u) >> 2 : 0u;
@@ -878,17 +888,18 @@ __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict_
                     dd.off = off;
                     if (lit) { dd.kind = XD_LIT; dd.src = woff + (srcv - I); }
                     else if (dep) { dd.kind = XD_DEP; dd.src = a; }
-                    else if (far) { dd.kind = XD_FAR; dd.src = uint32_t(lane) * (FBUF_W * 4) + (a & 3u); }
+                    else if (far) { dd.kind = XD_FAR; dd.src = frank * (FBUF_W * 4) + (a & 3u); }
                     else { dd.kind = XD_NEAR; dd.src = a; }
                     desc[lane] = dd;
                 }
-                sbits[lane & (XBATCH / 32 - 1)] = 0;
+                if (lane < int(XBATCH / 32)) sbits[lane] = 0;
                 __syncthreads();
                 if (inb) atomicOr(&sbits[rel >> 5], 1u << (rel & 31u));
                 __syncthreads();
                 {
-                    const uint32_t c = __popc(sbits[lane]);
-                    wpre[lane] = dpp_incl_scan(c) - c;
+                    const uint32_t c = lane < int(XBATCH / 32) ? __popc(sbits[lane]) : 0u;
+                    const uint32_t ex = dpp_incl_scan(c) - c;
+                    if (lane < int(XBATCH / 32)) wpre[lane] = ex;
                 }
                 __syncthreads();
                 XT(3);
@@ -923,7 +934,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict_
                 XT(2);
                 if (anyfar) {   // F: far copies (never self-overlapping: offset > ring > 64)
                     if (lane == 0) STAMP_ADD(9, 1);
-                    uint32_t* fl = fbuf + lane * FBUF_W;
+                    uint32_t* fl = fbuf + (far ? frank : 0u) * FBUF_W;
                     const uint32_t nwd = far ? ((a & 3u) + ol + 3u) >> 2 : 0u;
                     #pragma unroll
                     for (int u = 0; u < int(FBUF_W); u++)
@@ -961,7 +972,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict_
 #endif
                 XT(5);
                 const uint32_t sl = flush_slots(ring, dst, F, op + btot, lane);
-                if (sl) nst = 2 * sl;
+                if (sl) nst = sl;
                 XT(6);
             }
             op += btot;
