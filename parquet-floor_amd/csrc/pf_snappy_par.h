@@ -46,35 +46,24 @@ struct SnapTok {
 };
 
 // Decode the token whose tag is the low byte of v (v = the 8 stream bytes from the tag on).
+// Branch-free (selects), so lanes holding different token kinds do not diverge.
 __device__ __forceinline__ SnapTok snap_tok(uint64_t v) {
     SnapTok t;
     const uint32_t tag = uint32_t(v) & 0xffu;
     const uint32_t L = tag >> 2;
-    t.kind = tag & 3u;
-    if (t.kind == 0) {
-        if (L < 60) {
-            t.ol = L + 1;
-            t.arg = 1;
-        } else {
-            const uint32_t nb = L - 59;                               // 1..4 length bytes
-            const uint32_t len = uint32_t((v >> 8) & ((1ull << (8 * nb)) - 1ull));
-            t.ol = len + 1u;                                          // 0 only for a 4 GiB literal
-            t.arg = 1 + nb;
-        }
-        t.tl = uint64_t(t.arg) + (t.ol ? uint64_t(t.ol) : (1ull << 32));
-    } else if (t.kind == 1) {
-        t.tl = 2;
-        t.ol = 4 + (L & 7u);
-        t.arg = ((tag >> 5) << 8) | uint32_t((v >> 8) & 0xffu);
-    } else if (t.kind == 2) {
-        t.tl = 3;
-        t.ol = L + 1;
-        t.arg = uint32_t((v >> 8) & 0xffffu);
-    } else {
-        t.tl = 5;
-        t.ol = L + 1;
-        t.arg = uint32_t(v >> 8);
-    }
+    const uint32_t b1 = uint32_t(v >> 8);                             // the 4 bytes after the tag
+    const uint32_t kind = tag & 3u;
+    // literal: length-1 in L, or in 1..4 little-endian bytes after the tag when L >= 60
+    const uint32_t nb = L >= 60 ? L - 59 : 0u;
+    const uint32_t lmask = nb >= 4 ? 0xffffffffu : ((1u << (8u * nb)) - 1u);
+    const uint32_t lit_ol = (L < 60 ? L : (b1 & lmask)) + 1u;          // 0 only for a 4 GiB literal
+    const uint32_t lit_arg = 1u + nb;
+    const uint64_t lit_tl = uint64_t(lit_arg) + (lit_ol ? uint64_t(lit_ol) : (1ull << 32));
+    t.kind = kind;
+    t.ol = kind == 0 ? lit_ol : (kind == 1 ? 4u + (L & 7u) : L + 1u);
+    t.arg = kind == 0 ? lit_arg
+                      : (kind == 1 ? (((tag >> 5) << 8) | (b1 & 0xffu)) : (kind == 2 ? (b1 & 0xffffu) : b1));
+    t.tl = kind == 0 ? lit_tl : uint64_t(kind == 1 ? 2u : (kind == 2 ? 3u : 5u));
     return t;
 }
 
