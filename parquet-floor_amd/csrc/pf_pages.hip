@@ -1297,11 +1297,93 @@ __global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ 
     }
 }
 
+// copy_chars with a chunk -> value table (no per-chunk binary search) and 16-byte source reads
+// (aligned dwords + v_alignbyte) for chunks inside one value; other chunks byte by byte.
+// cv: LDS table of CV_CAP u16; send: end of the readable source buffer.
+constexpr uint32_t CV_CAP = 4096;
+__device__ inline void copy_chars_fast(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
+                                       const uint8_t* sbase, const uint8_t* send, uint8_t* obase, uint16_t* cv) {
+    if (total == 0 || nv == 0) return;
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(obase);
+    const uintptr_t c0 = a0 & ~uintptr_t(15);
+    const uint32_t nch = uint32_t(((a0 + total + 15) & ~uintptr_t(15)) - c0) / 16u;
+    if (nch > CV_CAP) { copy_chars(coff, csrc, nv, total, sbase, obase); return; }
+    // value v owns the chunks whose first byte lies inside it
+    if (threadIdx.x == 0) cv[0] = 0;
+    for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {
+        const uint32_t b = coff[v], e = v + 1 < nv ? coff[v + 1] : total;
+        if (e <= b) continue;
+        const uintptr_t ab = a0 + b, ae = a0 + e;
+        for (uintptr_t c = (ab + 15) & ~uintptr_t(15); c < ae; c += 16) cv[(c - c0) >> 4] = uint16_t(v);
+    }
+    __syncthreads();
+    for (uint32_t ci = threadIdx.x; ci < nch; ci += blockDim.x) {
+        const uintptr_t c = c0 + uintptr_t(ci) * 16u;
+        const int64_t r0 = int64_t(c) - int64_t(a0);
+        uint32_t v = cv[ci];
+        uint32_t vb = coff[v];
+        uint32_t vend = v + 1 < nv ? coff[v + 1] : total;
+        while (r0 >= 0 && uint32_t(r0) >= vend && v + 1 < nv) {   // zero-length values share a start
+            v++;
+            vb = coff[v];
+            vend = v + 1 < nv ? coff[v + 1] : total;
+        }
+        uint8_t* dst = reinterpret_cast<uint8_t*>(c);
+        if (r0 >= 0 && uint32_t(r0) >= vb && uint64_t(r0) + 16 <= vend) {
+            const uint8_t* sp = sbase + csrc[v] + (uint32_t(r0) - vb);
+            if (sp + 20 <= send) {
+                const uintptr_t sa = reinterpret_cast<uintptr_t>(sp);
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(sa & ~uintptr_t(3));
+                const uint32_t sh = uint32_t(sa & 3u);
+                uint32_t d[5];
+                #pragma unroll
+                for (int k = 0; k < 5; k++) d[k] = q[k];
+                uint4 o;
+                if (sh) {
+                    o.x = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+                    o.y = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+                    o.z = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
+                    o.w = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+                } else {
+                    o = make_uint4(d[0], d[1], d[2], d[3]);
+                }
+                *reinterpret_cast<uint4*>(dst) = o;
+                continue;
+            }
+        }
+        const uint8_t* sp = sbase + (int64_t(csrc[v]) - int64_t(vb));
+        uint32_t word[4] = {0, 0, 0, 0};
+        #pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int64_t r = r0 + k;
+            if (r >= 0 && r < int64_t(total)) {
+                while (uint32_t(r) >= vend) {
+                    v++;
+                    vb = coff[v];
+                    vend = v + 1 < nv ? coff[v + 1] : total;
+                    sp = sbase + (int64_t(csrc[v]) - int64_t(vb));
+                }
+                word[k >> 2] |= uint32_t(sp[r]) << (8 * (k & 3));
+            }
+        }
+        if (r0 >= 0 && r0 + 16 <= int64_t(total)) {
+            *reinterpret_cast<uint4*>(dst) = make_uint4(word[0], word[1], word[2], word[3]);
+        } else {
+            #pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int64_t r = r0 + k;
+                if (r >= 0 && r < int64_t(total)) dst[k] = uint8_t(word[k >> 2] >> (8 * (k & 3)));
+            }
+        }
+    }
+}
+
 struct FlatLds {
     Run drun[RUN_CAP];
     Run vrun[RUN_CAP];
     uint32_t coff[FT];
     uint32_t csrc[FT];
+    uint16_t cv[CV_CAP];
     uint32_t vbits[FT / 32 + 2];
     uint32_t scan_tmp[NT / 64];
     RunWalk dst, vst;
@@ -1753,7 +1835,11 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
 #ifdef PF_STAMPS
         { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) { PSTAMP(4, t_ - ft1); PSTAMP(3, 1); } ft1 = t_; }
 #endif
-        if (binary) copy_chars(S.coff, S.csrc, tv, tchars, dict ? ck.dict_data : s.val, ck.chars + char_base);
+        if (binary) {
+            const uint8_t* sb = dict ? ck.dict_data : s.val;
+            const uint8_t* se = dict ? pages[ck.dict_page].body + pages[ck.dict_page].body_len : s.val + s.val_n;
+            copy_chars_fast(S.coff, S.csrc, tv, tchars, sb, se, ck.chars + char_base, S.cv);
+        }
         if (ck.max_def > 0 && ck.validity) flush_bits(S.vbits, slot_base + e0, want, ck.validity);
         vidx += tv;
         char_base += tchars;
