@@ -29,7 +29,10 @@ def _payloads(rng):
     runs = b"".join(bytes([int(b)]) * int(k) for b, k in zip(rng.integers(0, 4, 4000), rng.integers(1, 300, 4000)))
     mixed = b"".join((rng.integers(0, 256, int(rng.integers(1, 80)), dtype=np.uint8).tobytes() if rng.random() < 0.3
                       else words[int(rng.integers(0, 7))] * int(rng.integers(1, 20))) for _ in range(6000))
-    return {"text": text, "ints": ints, "random": rnd, "runs": runs, "mixed": mixed, "tiny": b"ab", "empty": b""}
+    # dense chains of dependent copies (offset 4/8 copies between 1-3 byte literals)
+    stride = np.arange(0, 7 * 90000, 7, dtype=np.int64).tobytes()
+    small = (np.arange(150000, dtype=np.int32) // 3).tobytes()
+    return {"text": text, "ints": ints, "stride": stride, "small": small, "random": rnd, "runs": runs, "mixed": mixed, "tiny": b"ab", "empty": b""}
 
 
 def test_known_answer_vectors(dec, oracle):
