@@ -64,6 +64,14 @@ struct DevPage {
     int32_t ba_job;           // PLAIN BYTE_ARRAY data page: its BaJob (k_count fills it), else -1
     int32_t counted;          // 1: k_count_flat counted the page (k_count skips it)
     uint32_t* runtab;         // dictionary data page of a flat chunk: id run table (k_runs), else null
+    // DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY page (k_dlen, pf_delta.hip): {cpos[aux_cap + 1],
+    // lenA[aux_cap], lenB[aux_cap]} (u64), values in the length streams, first bad value, and
+    // where the chars / suffixes start in the values section; else null
+    uint64_t* dx;
+    int64_t dx_total;
+    int64_t dx_bad;
+    uint32_t dx_data;
+    uint32_t dx_pad;
 };
 
 // k_runs run table of a page: {nruns, values covered, all levels present, valid}, then nruns

@@ -655,7 +655,15 @@ __global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunk
         __syncthreads();
     }
     if (L.err || verr) { if (threadIdx.x == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
-    if (binary && !dict) {
+    if (binary && (pg.encoding == 6 || pg.encoding == 7) && pg.dx) {
+        // DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY: lengths decoded by k_dlen (pf_delta.hip)
+        if (threadIdx.x == 0) {
+            if (int64_t(vals) > pg.dx_total || int64_t(vals) > pg.dx_bad) verr = 1;
+            else chars_acc = pg.dx[vals];
+        }
+        __syncthreads();
+        if (verr) { if (threadIdx.x == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
+    } else if (binary && !dict) {
         if (pg.encoding != 0 || pg.ba_job < 0) {
             if (threadIdx.x == 0) set_status(res, pg.chunk, ST_ENCODING, pi);
             return;
@@ -804,6 +812,7 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
     else if (enc == 3) supported = boolean;
     else if (enc == 5) supported = (ck.ptype == 1 || ck.ptype == 2) && pg.aux != nullptr;
     else if (enc == 9) supported = (ck.ptype == 4 || ck.ptype == 5);
+    else if (enc == 6 || enc == 7) supported = binary && pg.dx != nullptr;   // k_dlen lengths
     if (!supported) { if (tid == 0) set_status(res, pg.chunk, dict ? ST_CORRUPT : ST_ENCODING, pi); return; }
     if (dict && id_bw > 32) { if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
     if (binary && !ck.chars) return;   // capacity error already recorded by k_scan
@@ -875,6 +884,9 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
                         uint32_t id = S.ids[v];
                         if (int64_t(id) < ck.dict_n) { my_src[k] = ck.dict_pos[id]; my_len[k] = ck.dict_len[id]; }
                         else S.verr = 1;
+                    } else if (enc == 6 || enc == 7) {   // cpos: chars before value gv (checked by k_count)
+                        my_src[k] = uint64_t(pg.dx_data) + pg.dx[gv];
+                        my_len[k] = uint32_t(pg.dx[gv + 1] - pg.dx[gv]);
                     } else {
                         uint32_t p = pg.aux[gv];
                         uint32_t l = (p >= 4 && p <= s.val_n) ? ld32le(s.val, p - 4, s.val_n) : 0xffffffffu;
@@ -930,7 +942,8 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
                 if (binary) {
                     if (present) {
                         const uint8_t* src = dict ? ck.dict_data + my_src[k] : s.val + my_src[k];
-                        for (uint32_t j = 0; j < my_len[k]; j++) ck.chars[cpos + j] = src[j];
+                        if (enc != 7)   // DELTA_BYTE_ARRAY chars: k_dba_chars (values depend on their predecessor)
+                            for (uint32_t j = 0; j < my_len[k]; j++) ck.chars[cpos + j] = src[j];
                         cpos += my_len[k];
                     }
                     ck.offsets[slot + 1] = int32_t(cpos);

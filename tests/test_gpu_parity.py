@@ -10,9 +10,9 @@ from golden_util import assert_chunk_equal, load_expected
 
 pytestmark = pytest.mark.gpu
 
-# Encodings the HIP path does not decode yet: chunks using them must
-# fail loudly with PF_ERR_UNSUPPORTED_ENCODING (-3), never return wrong data.
-UNSUPPORTED = {"DELTA_LENGTH_BYTE_ARRAY", "DELTA_BYTE_ARRAY"}
+# Encodings the HIP path does not decode (none at present): chunks using them must fail loudly
+# with PF_ERR_UNSUPPORTED_ENCODING (-3), never return wrong data.
+UNSUPPORTED = set()
 
 
 @pytest.fixture(scope="module")
@@ -143,7 +143,7 @@ def test_corrupt_pages_error_not_fault(decoder, tmp_path):
     the GPU never faults and the context stays usable."""
     from pfloor.decoder import decode_file
     rng = np.random.default_rng(3)
-    for name in ("c2_lineitem", "c5_nested", "c1_flat_none_v1"):
+    for name in ("c2_lineitem", "c5_nested", "c1_flat_none_v1", "edge_encodings"):
         data = open(os.path.join(GOLDEN, name + ".parquet"), "rb").read()
         for i, bad in enumerate(_corrupt_variants(data, rng, 6)):
             p = tmp_path / f"{name}_{i}.parquet"
