@@ -1406,7 +1406,12 @@ struct FlatLds {
 
 // k_flat, all levels present, fixed-width values: value index = entry index, lane-consecutive
 // entries so every load and store of a wave is one contiguous run of memory. Returns err.
+#ifndef PF_DICT_LDS
+#define PF_DICT_LDS 32768
+#endif
+constexpr uint32_t DICT_LDS = PF_DICT_LDS;   // bytes of a fixed-width dictionary staged in LDS (k_flat_fixed)
 struct FixedLds {
+    uint64_t dict[DICT_LDS / 8 + 1];
     Run vrun[RUN_CAP];
     uint32_t coff[FT / 64];
     RunWalk vst;
@@ -1421,6 +1426,20 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
     const int tid = threadIdx.x;
     const uint8_t* vend = s.val + s.val_n;
     const bool dalign = dict && (reinterpret_cast<uintptr_t>(ck.dict_data) & uintptr_t(w - 1)) == 0;
+    // dictionary gather from LDS when the whole dictionary fits (north_star: K3 LDS / global)
+    const bool dlds = DICT_LDS > 0 && dict && dalign && (w == 4 || w == 8) && ck.dict_data != nullptr &&
+                      ck.dict_n > 0 && uint64_t(ck.dict_n) * uint64_t(w) <= DICT_LDS;
+    if (dlds) {
+        if (w == 8) {
+            const uint64_t* g = reinterpret_cast<const uint64_t*>(ck.dict_data);
+            for (uint32_t i = tid; i < uint32_t(ck.dict_n); i += NT) S.dict[i] = g[i];
+        } else {
+            const uint32_t* g = reinterpret_cast<const uint32_t*>(ck.dict_data);
+            uint32_t* d32 = reinterpret_cast<uint32_t*>(S.dict);
+            for (uint32_t i = tid; i < uint32_t(ck.dict_n); i += NT) d32[i] = g[i];
+        }
+        __syncthreads();
+    }
     for (uint32_t e0 = e_begin; e0 < e_end; e0 += FT) {
         const uint32_t want = min(uint32_t(FT), e_end - e0);
         int bad = 0;
@@ -1476,8 +1495,12 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
                     const uint32_t e = e0 + (kb + k) * NT + uint32_t(tid);
                     if (e >= e0 + want) continue;
                     if (int64_t(id[k]) >= ck.dict_n) { bad = 1; continue; }
-                    const uint8_t* src = ck.dict_data + uint64_t(id[k]) * uint64_t(w);
-                    v[k] = w == 8 ? *reinterpret_cast<const uint64_t*>(src) : *reinterpret_cast<const uint32_t*>(src);
+                    if (dlds) {
+                        v[k] = w == 8 ? S.dict[id[k]] : reinterpret_cast<const uint32_t*>(S.dict)[id[k]];
+                    } else {
+                        const uint8_t* src = ck.dict_data + uint64_t(id[k]) * uint64_t(w);
+                        v[k] = w == 8 ? *reinterpret_cast<const uint64_t*>(src) : *reinterpret_cast<const uint32_t*>(src);
+                    }
                 }
             }
             #pragma unroll
