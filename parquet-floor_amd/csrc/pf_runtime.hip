@@ -817,6 +817,26 @@ int pf_debug_snappy_tables(pf_ctx* ctx, uint32_t* splits, int n_splits, uint32_t
     return PF_OK;
 }
 
+// Diagnostics (not part of pfloor.h): per Snappy job of the last finished pf_decode_row_group,
+// {fallback flag (FB_*), compressed length, decompressed length, chunk, page}. Returns the job count.
+int pf_debug_snappy_fallback(pf_ctx* ctx, int* out, int n_jobs) {
+    if (!ctx || !ctx->d_meta.p) return fail(ctx, PF_ERR_STATE, "no decode");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int nj = int(ctx->jobs.size());
+    const int m = n_jobs < nj ? n_jobs : nj;
+    if (out && m > 0) {
+        std::vector<int> fb(size_t(m), 0);
+        HIPCHK(ctx, hipMemcpy(fb.data(), static_cast<uint8_t*>(ctx->d_meta.p) + ctx->off_fallback, 4 * size_t(m),
+                              hipMemcpyDeviceToHost));
+        for (int i = 0; i < m; i++) {
+            const SnappyJob& jb = ctx->jobs[size_t(i)];
+            const int rec[5] = {fb[size_t(i)], int(jb.src_len), int(jb.dst_len), jb.chunk, jb.page};
+            for (int q = 0; q < 5; q++) out[5 * i + q] = rec[q];
+        }
+    }
+    return nj;
+}
+
 int pf_last_timing(pf_ctx* ctx, float* stage_ms, int n_stages, int* n_written) {
     if (!ctx || !stage_ms || n_stages < 0) return fail(ctx, PF_ERR_INVALID_ARG, "bad arg");
     if (!ctx->timing_valid) return fail(ctx, PF_ERR_STATE, "no finished decode");

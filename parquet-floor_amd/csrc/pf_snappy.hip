@@ -56,15 +56,9 @@ __device__ __forceinline__ void flush(const uint8_t* ring, uint8_t* dst, uint32_
     for (uint32_t q = tail_start + lane; q < to; q += WAVE) dst[q] = ring[q & RMASK];
 }
 
-__global__ __launch_bounds__(64) void k_snappy_serial(const SnappyJob* __restrict__ jobs, const int* __restrict__ fallback,
-                                                      DevChunkResult* res) {
-    if (fallback[blockIdx.x] != FB_SERIAL) return;   // the block-parallel path decoded this page
-    __shared__ uint8_t ring[RING];
-    __shared__ Token toks[TOK_BATCH];
-    __shared__ int ntok_s, err_s;
-    __shared__ uint32_t ip_s;
-
-    const SnappyJob job = jobs[blockIdx.x];
+// One page, serially, by one wave (LDS passed in by the kernel).
+__device__ void serial_page(const SnappyJob& job, DevChunkResult* res, uint8_t* ring, Token* toks, int& ntok_s,
+                            int& err_s, uint32_t& ip_s) {
     const uint8_t* in = job.src;
     const uint64_t n = job.src_len;
     uint8_t* dst = job.dst;
@@ -184,9 +178,30 @@ __global__ __launch_bounds__(64) void k_snappy_serial(const SnappyJob* __restric
 
 
 
+// Grid-stride over the jobs with a small grid: nearly every page was decoded by the parallel path,
+// and a block per job would hold 70 KB of LDS each just to read its flag, waiting for CUs that the
+// other context's executor occupies (a no-op launch measured up to 1.1 ms with two streams).
+constexpr int SERIAL_GRID = 64;
+
+__global__ __launch_bounds__(64) void k_snappy_serial(const SnappyJob* __restrict__ jobs, const int* __restrict__ fallback,
+                                                      int n_jobs, DevChunkResult* res) {
+    __shared__ uint8_t ring[RING];
+    __shared__ Token toks[TOK_BATCH];
+    __shared__ int ntok_s, err_s;
+    __shared__ uint32_t ip_s;
+    for (int j = blockIdx.x; j < n_jobs; j += gridDim.x) {
+        if (fallback[j] != FB_SERIAL) continue;   // the block-parallel path decoded this page
+        const SnappyJob job = jobs[j];
+        serial_page(job, res, ring, toks, ntok_s, err_s, ip_s);
+        __syncthreads();
+    }
+}
+
 void launch_snappy_serial(const SnappyJob* d_jobs, int n_jobs, const int* d_fallback, DevChunkResult* d_res,
                           hipStream_t s) {
-    if (n_jobs > 0) hipLaunchKernelGGL(k_snappy_serial, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_fallback, d_res);
+    if (n_jobs > 0)
+        hipLaunchKernelGGL(k_snappy_serial, dim3(n_jobs < SERIAL_GRID ? n_jobs : SERIAL_GRID), dim3(64), 0, s, d_jobs,
+                           d_fallback, n_jobs, d_res);
 }
 
 }  // namespace pf
