@@ -85,6 +85,11 @@ constexpr int64_t FLAT_BLK = 4096;         // pf_pages.hip FBLK   // h2d, snappy
 struct pf_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // PF_EXEC_STREAM=1: the Snappy executor runs on a low-priority stream of its own (event-ordered
+    // with `stream`, which then gets the high priority), so the short kernels of another context
+    // get CUs ahead of this context's executor waves as those retire.
+    hipStream_t exec_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev[N_EVENTS] = {};
     std::string err;
     DevBuf d_in, d_scratch, d_out, d_bits, d_chars, d_meta, d_tokmap;
@@ -173,7 +178,16 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_snappy_parse(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent,
                         ctx->d_lane_out, d_splits, d_fallback, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
-    launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res, st);
+    if (ctx->exec_stream) {
+        HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
+        HIPCHK(ctx, hipStreamWaitEvent(ctx->exec_stream, ctx->ev_fork, 0));
+        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res,
+                           ctx->exec_stream);
+        HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->exec_stream));
+        HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_join, 0));
+    } else {
+        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res, st);
+    }
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], st));
     BaJob* d_bajobs = reinterpret_cast<BaJob*>(meta + ctx->off_bajobs);
     const int2* d_batiles = reinterpret_cast<const int2*>(meta + ctx->off_batiles);
@@ -301,7 +315,17 @@ int pf_ctx_create(int device, pf_ctx** out) {
     auto ctx = std::make_unique<pf_ctx>();
     ctx->device = device;
     HIPCHK(nullptr, hipSetDevice(device));
-    HIPCHK(nullptr, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    const char* es = std::getenv("PF_EXEC_STREAM");
+    if (es && es[0] && es[0] != '0') {
+        int least = 0, greatest = 0;
+        HIPCHK(nullptr, hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIPCHK(nullptr, hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, greatest));
+        HIPCHK(nullptr, hipStreamCreateWithPriority(&ctx->exec_stream, hipStreamNonBlocking, least));
+        HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+        HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    } else {
+        HIPCHK(nullptr, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    }
     for (auto& e : ctx->ev) HIPCHK(nullptr, hipEventCreate(&e));
     *out = ctx.release();
     return PF_OK;
@@ -311,11 +335,15 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     if (!ctx) return PF_OK;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->exec_stream) (void)hipStreamSynchronize(ctx->exec_stream);
     for (DevBuf* b : {&ctx->d_in, &ctx->d_scratch, &ctx->d_out, &ctx->d_bits, &ctx->d_chars, &ctx->d_meta, &ctx->d_tokmap})
         b->release();
     ctx->h_meta.release();
     ctx->h_res.release();
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->exec_stream) (void)hipStreamDestroy(ctx->exec_stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return PF_OK;
