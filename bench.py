@@ -162,7 +162,7 @@ def main():
     ap.add_argument("--rows", type=int, default=SF1_ROWS)
     ap.add_argument("--data-dir", default=os.environ.get("PF_BENCH_DIR", "/tmp/pfloor_bench"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=4,
                     help="decode contexts (HIP streams) per GPU; row groups are dealt round-robin to them")
     args = ap.parse_args()
 
@@ -246,7 +246,7 @@ def main():
         "flat": st0["uncompressed"] + dbytes0,
     }
     dom = max((k for k in stage_ms if k != "h2d"), key=lambda k: stage_ms.get(k, 0.0))
-    # per-launch kernel time of the dominant stage without a concurrent stream: with two contexts
+    # per-launch kernel time of the dominant stage without a concurrent stream: with several contexts
     # the HIP events on context 0 also count the time its kernels wait for CUs held by context 1,
     # which rocprof's kernel durations do not. Context 0's share, decoded alone, ROOF_PASSES times
     # after the timed region (HIP events on its stream bracket exactly that stage's launches).
