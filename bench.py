@@ -1,22 +1,43 @@
 #!/usr/bin/env python3
-"""Benchmark: decode a TPC-H lineitem-shaped Parquet file (SF1: 6,001,215 rows, 16 columns,
-Snappy + dictionary, 1 Mi-row row groups; BASELINE.json configs[1]) on MI355X.
+"""Benchmark of the Parquet column-chunk decode path (BASELINE.json: "decoded GB/s + rows/s (node),
+lineitem-shape Snappy+dict, 1/2/4/8 GPUs").
 
-One step = one pass of the hot path over the whole file: every page of all 96 column chunks
-decompressed and decoded into columnar buffers in HBM, with the chunk bytes already resident in
-HBM when the timed region starts (device-resident). N GPUs: one process per GPU, each decodes its
-own SF1 file per step (row groups are independent; no collective on the data path) -> weak
-scaling; `value` = decoded bytes of all ranks / max-over-ranks time.
+Workloads (--workload):
+  sf1    (default; BASELINE configs[1]) TPC-H lineitem-shaped SF1: 6,001,215 rows, 16 columns,
+         Snappy + dictionary, 1 Mi-row row groups, seed 42. At N GPUs the logical file is SF1 x N
+         (the 6 row groups repeated N times = 6N row groups) sharded round-robin by pfloor.shard:
+         weak scaling, every rank decodes 6 row groups per step.
+  sf100  (configs[2]) lineitem-shaped SF100: 150 row groups of 4,000,000 rows sharded round-robin
+         over the N GPUs (strong scaling). The two distinct synthetic row groups written on the box
+         stand for the 150 (logical row group g decodes physical row group g % 2 in full).
+  wide   (configs[3]) 1,000,000 rows x 500 nullable INT32/FLOAT columns, 30 % nulls, 100,000-value
+         dictionaries (400 KB, larger than LDS); the row group's columns are split over the streams.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+One step = one pass of the hot path over the rank's share: every page of every selected column
+chunk decompressed and decoded into columnar buffers in HBM, compressed bytes already resident in
+HBM (device-resident). `value` = decoded bytes of all ranks / max-over-ranks step time.
+After the timed region (never inside it): bit-exact parity of the timed outputs against the CPU
+oracle, the dominant kernel's isolated launch time (roofline), the end-to-end rate (pinned host
+input -> H2D -> decode -> D2H into pinned host columns), and CPU baselines on the host cores.
+The dominant kernel's HBM traffic comes from rocprofv3 --pmc passes run as child processes
+before this process touches the GPU.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload sf1|sf100|wide]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0.
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N ranks itself (child
+processes, before any GPU call). Prints ONE JSON line on rank 0.
 """
 import argparse
+import concurrent.futures as cf
+import csv
 import ctypes as C
+import glob
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -30,36 +51,119 @@ SF1_ROWS = 6001215
 RG_ROWS = 1 << 20
 SEED = 42
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-ROOF_PASSES = 3         # isolated decodes of context 0's share for the roofline kernel time
+PCIE_GBS = 63.0         # MI355X_MICROARCH.md: PCIe Gen5 x16 per direction
+ROOF_PASSES = 3         # isolated decodes of context 0's first batch for the roofline kernel time
+E2E_PASSES = 2
+METRIC = "decoded GB/s + rows/s (node), lineitem-shape Snappy+dict, 1/2/4/8 GPUs"
+
+WORKLOADS = {
+    # physical file, logical row groups, row groups per decode batch
+    "sf1": dict(rows=SF1_ROWS, rg_rows=RG_ROWS, seed=SEED, kind="lineitem", batch=0),
+    "sf100": dict(rows=8_000_000, rg_rows=4_000_000, seed=43, kind="lineitem", batch=1, logical=150),
+    "wide": dict(rows=1_000_000, rg_rows=1_000_000, seed=4, kind="wide", batch=1),
+}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_input(path, rows):
+def input_path(args):
+    w = WORKLOADS[args.workload]
+    return os.path.join(args.data_dir, f"{w['kind']}_{w['rows']}_seed{w['seed']}_rg{w['rg_rows']}.parquet")
+
+
+def make_input(args):
+    path = input_path(args)
+    if os.path.exists(path):
+        return path
     import pyarrow.parquet as pq
     from pfloor import datagen
+    w = WORKLOADS[args.workload]
     t0 = time.time()
-    t = datagen.lineitem_table(rows, seed=SEED)
-    tmp = path + ".tmp"
-    pq.write_table(t, tmp, compression="snappy", row_group_size=RG_ROWS)
+    os.makedirs(args.data_dir, exist_ok=True)
+    if w["kind"] == "lineitem":
+        # sf100's row groups are SF100-shaped (key ranges of the full 600M-row file)
+        t = datagen.lineitem_table(w["rows"], seed=w["seed"], scale=100.0 if args.workload == "sf100" else None)
+    else:
+        t = datagen.wide_table(w["rows"], seed=w["seed"])
+    tmp = path + f".tmp{os.getpid()}"
+    pq.write_table(t, tmp, compression="snappy", row_group_size=w["rg_rows"])
     os.replace(tmp, path)
     log(f"[bench] wrote {path} ({os.path.getsize(path) / 1e6:.1f} MB) in {time.time() - t0:.1f}s")
+    return path
 
 
-def plan_file(path):
-    """Chunk bytes (contiguous, 256-B aligned) + descriptors for every chunk of the file."""
-    from pfloor.decoder import ParquetFile
-    pf = ParquetFile(path)
-    items, total = pf.plan(range(pf.num_row_groups), range(pf.num_columns))
-    host = np.zeros(total, dtype=np.uint8)
-    descs = []
-    for rg, col, s, n, off in items:
-        if n:
-            pf.read_into(s, n, host.ctypes.data + off)
-        descs.append(pf.chunk_desc(rg, col, off))
-    return pf, items, host, descs
+# --------------------------------------------------------------------------- work plan
+
+def logical_row_groups(args, n_phys, world):
+    w = WORKLOADS[args.workload]
+    if args.workload == "sf1":
+        return n_phys * world              # SF1 x N (weak scaling)
+    return w.get("logical", n_phys)
+
+
+def units_for_rank(args, pf, world, rank, S):
+    """This rank's work units (logical rg, physical rg, columns), dealt to S contexts, then grouped
+    into decode batches: [[batch, ...] per context], batch = list of units."""
+    from pfloor.shard import row_groups_for_rank
+    n_phys = pf.num_row_groups
+    n_log = logical_row_groups(args, n_phys, world)
+    mine = row_groups_for_rank(n_log, rank, world)
+    cols = list(range(pf.num_columns))
+    units = [(g, g % n_phys, cols) for g in mine]
+    if args.workload == "wide" and units:   # one row group: split its columns over the contexts
+        g, p, _ = units[0]
+        k = max(1, min(S, len(cols)))
+        units = [(g, p, cols[i::k]) for i in range(k)] + units[1:]
+    S = max(1, min(S, len(units)))
+    per_ctx = [units[k::S] for k in range(S)]
+    bsz = WORKLOADS[args.workload]["batch"]
+    out = []
+    for us in per_ctx:
+        if bsz <= 0:
+            out.append([us])                  # sf1: the context's row groups in one batch
+        else:
+            out.append([us[i:i + bsz] for i in range(0, len(us), bsz)])
+    return out, n_log, mine
+
+
+class BatchInput:
+    """Chunk bytes of one batch (physical units) laid out back to back, 256-B aligned, with the
+    descriptors pointing into that buffer; kept in a pinned host buffer and in HBM."""
+
+    def __init__(self, pf, units, ctx):
+        from pfloor.decoder import PinnedBuffer
+        items = []
+        off = 0
+        for _g, p, cols in units:
+            for c in cols:
+                s, n = pf.chunk_range(p, c)
+                items.append((p, c, s, n, off))
+                off += (n + 255) // 256 * 256
+        self.items = items
+        self.nbytes = max(off, 1)
+        self.host = PinnedBuffer(ctx, self.nbytes)
+        for p, c, s, n, o in items:
+            if n:
+                pf.read_into(s, n, self.host.ptr.value + o)
+        self.descs = [pf.chunk_desc(p, c, o) for p, c, _s, _n, o in items]
+        self.dev = None
+
+    def upload(self, dec):
+        from pfloor import _native
+        L = _native.lib()
+        d = C.c_void_p()
+        _native.check(L.pf_device_alloc(dec.h, self.nbytes, C.byref(d)), dec.h, "pf_device_alloc")
+        _native.check(L.pf_memcpy_h2d(dec.h, d, self.host.ptr, self.nbytes), dec.h, "h2d")
+        self.dev = d
+
+    def free(self, dec):
+        from pfloor import _native
+        if self.dev:
+            _native.lib().pf_device_free(dec.h, self.dev)
+            self.dev = None
+        self.host.free()
 
 
 def page_stats(descs):
@@ -79,59 +183,129 @@ def page_stats(descs):
     return dict(pages=pages, compressed=comp, uncompressed=uncomp, snappy_in=snappy_in, snappy_out=snappy_out)
 
 
-def decoded_bytes(decs, parts, pf, items):
-    tot = 0
-    rows = 0
-    for dec, idx in zip(decs, parts):
-      for i, j in enumerate(idx):
-        rg, col = items[j][0], items[j][1]
-        ci = dec.info(i)
-        c = pf.columns[col]
-        b = ci.num_slots * ci.width
-        if c.max_def > 0:
-            b += (ci.num_slots + 7) // 8
-        if c.physical_type == 6:
-            b += 4 * (ci.num_slots + 1) + ci.num_chars
-        if c.max_rep == 1:
-            b += 4 * (ci.num_rows + 1) + (ci.num_rows + 7) // 8
-        if c.max_rep > 0:
-            b += 2 * ci.num_entries
-        tot += b
-    for rg in range(pf.num_row_groups):
-        rows += pf.row_group_rows(rg)
-    return tot, rows
+def chunk_decoded_bytes(col, ci):
+    b = ci.num_slots * ci.width
+    if col.max_def > 0:
+        b += (ci.num_slots + 7) // 8
+    if col.physical_type == 6:
+        b += 4 * (ci.num_slots + 1) + ci.num_chars
+    if col.max_rep == 1:
+        b += 4 * (ci.num_rows + 1) + (ci.num_rows + 7) // 8
+    if col.max_rep > 0:
+        b += 2 * ci.num_entries
+    return b
 
 
-def cpu_baseline(path, pf, seconds_budget=12.0, threads=8):
-    """The CPU oracle (oracle/pf_oracle.c, a plain-C port of the decode; not the Java reference,
-    which cannot run without a JDK + parquet-mr jars) on a bounded sample: row group 0, all
-    16 chunks, decoded by `threads` host threads, repeated until ~seconds_budget."""
+# --------------------------------------------------------------------------- rocprofv3 PMC child
+
+def pmc_child(args):
+    """Runs under rocprofv3 --pmc: context 0's first batch decoded alone (1 stream), 1 + 3 times.
+    ctypes only (no torch), so the profiled process is the decode and nothing else."""
+    from pfloor.decoder import GpuDecoder, ParquetFile
+    pf = ParquetFile(input_path(args))
+    plan, _, _ = units_for_rank(args, pf, 1, 0, args.streams)
+    dec = GpuDecoder(0)
+    bi = BatchInput(pf, plan[0][0], dec.h)
+    bi.upload(dec)
+    for _ in range(1 + ROOF_PASSES):
+        dec.decode(bi.descs, bi.dev.value, bi.nbytes, on_device=True)
+        if dec.wait() != 0:
+            raise RuntimeError(dec.error())
+    bi.free(dec)
+    dec.close()
+
+
+def measure_pmc(args, kernel_re):
+    """HBM traffic of the roofline kernels per launch: one rocprofv3 pass per counter (FETCH_SIZE and
+    WRITE_SIZE cannot share a pass on gfx950), FETCH_SIZE doubled (MI355X_MICROARCH.md, HBM)."""
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return {"error": "rocprofv3 not found"}
+    out = os.path.join(args.data_dir, f"pmc_{os.getpid()}")
+    res = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for cnt in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(out, cnt)
+        cmd = [prof, "--pmc", cnt, "--kernel-include-regex", kernel_re, "--output-format", "csv", "-d", d, "-o", "run",
+               "--", sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
+               "--data-dir", args.data_dir, "--streams", str(args.streams)]
+        t0 = time.time()
+        r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
+        log(f"[bench] rocprofv3 --pmc {cnt}: rc {r.returncode} in {time.time() - t0:.1f}s")
+        if r.returncode != 0:
+            return {"error": f"rocprofv3 {cnt} rc {r.returncode}: {r.stdout.decode(errors='replace')[-400:]}"}
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if not files:
+            return {"error": f"no counter_collection.csv for {cnt}"}
+        per_launch = []
+        with open(files[0]) as f:
+            for row in csv.DictReader(f):
+                per_launch.append((int(row.get("Dispatch_Id", 0) or 0), row["Kernel_Name"].split("(")[0].replace("pf::", ""),
+                                   float(row["Counter_Value"]) * 1024.0))   # KB -> bytes
+        res[cnt] = sorted(per_launch)
+    shutil.rmtree(out, ignore_errors=True)
+    return res
+
+
+def pmc_traffic_per_kernel(pmc):
+    """{kernel: mean bytes per decode} over the last ROOF_PASSES decodes (the first is the warm-up)."""
+    out = {}
+    for cnt, rows in pmc.items():
+        if not isinstance(rows, list):
+            continue
+        by = {}
+        for _i, name, v in rows:
+            by.setdefault(name, []).append(v)
+        for name, vals in by.items():
+            # every decode launches each kernel the same number of times
+            per_decode = len(vals) // (1 + ROOF_PASSES) if len(vals) >= 1 + ROOF_PASSES else 0
+            if per_decode == 0:
+                continue
+            tail = vals[per_decode:]
+            mean = sum(tail) / ROOF_PASSES
+            out.setdefault(name, {})[cnt] = mean * (2.0 if cnt == "FETCH_SIZE" else 1.0)
+    return {k: {"fetch_bytes_x2": round(v.get("FETCH_SIZE", 0)), "write_bytes": round(v.get("WRITE_SIZE", 0)),
+                "traffic_bytes": round(v.get("FETCH_SIZE", 0) + v.get("WRITE_SIZE", 0))} for k, v in out.items()}
+
+
+# --------------------------------------------------------------------------- CPU baselines
+
+def _host_cores():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))   # the GPU box's CPU share is 16 cores per GPU
+
+
+def cpu_baselines(path, pf, budget_s=8.0):
+    """The Java reference cannot run (no JDK / parquet-mr jars on the box). Timed instead, on the
+    whole file: the C oracle (oracle/pf_oracle.c, a plain-C port of parquet-mr's decode + Snappy) at
+    1 core and at all host cores, and pyarrow.parquet.read_table at the same core counts."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import subprocess
     lib = os.path.join(ROOT, "oracle", "libpf_oracle.so")
     if not os.path.exists(lib):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     from oracle_binding import Oracle
     orc = Oracle(lib)
-    of = orc.open(path)
-    ncols = of.num_columns
-    rows_rg0 = pf.row_group_rows(0)
-    # decoded bytes of rg0 (from one decode pass)
+    cores = _host_cores()
+    nrg, ncol = pf.num_row_groups, pf.num_columns
+    rows = pf.num_rows
+    work = [(g, c) for g in range(nrg) for c in range(ncol)]
+    files = [orc.open(path) for _ in range(cores)]   # one handle per thread
     dec_bytes = 0
-    for c in range(ncols):
-        r = of.decode(0, c)
+    for g, c in work:
+        r = files[0].decode(g, c)
         assert r["status"] == 0, r["error"]
-        for k in ("values", "validity", "offsets", "chars"):
-            if k in r:
-                dec_bytes += r[k].nbytes
-    work = [(0, c) for c in range(ncols)]
-    passes = 0
-    t0 = time.perf_counter()
-    while True:
+        dec_bytes += sum(r[k].nbytes for k in ("values", "validity", "offsets", "chars") if k in r)
+    out = []
+
+    def oracle_pass(threads):
         idx = [0]
         lock = threading.Lock()
 
-        def run():
+        def run(t):
+            of = files[t]
             while True:
                 with lock:
                     if idx[0] >= len(work):
@@ -139,32 +313,152 @@ def cpu_baseline(path, pf, seconds_budget=12.0, threads=8):
                     j = idx[0]
                     idx[0] += 1
                 of.decode(*work[j])
-
-        ts = [threading.Thread(target=run) for _ in range(threads)]
+        ts = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
         [t.start() for t in ts]
         [t.join() for t in ts]
-        passes += 1
-        if time.perf_counter() - t0 > seconds_budget or passes >= 20:
-            break
-    dt = time.perf_counter() - t0
-    of.close()
-    return {"value": round(dec_bytes * passes / dt / 1e9, 4), "unit": "decoded GB/s",
-            "rows_per_s": round(rows_rg0 * passes / dt, 1), "cores": threads, "kind": "port",
-            "sample": f"row group 0 of the SF1 file ({rows_rg0} rows x {ncols} chunks), {passes} passes, "
-                      f"{threads} threads, oracle/pf_oracle.c (C port of parquet-mr 1.12.2 + snappy decode)"}
+
+    for threads in (1, cores):
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            oracle_pass(threads)
+            passes += 1
+            if time.perf_counter() - t0 > budget_s or passes >= 20:
+                break
+        dt = time.perf_counter() - t0
+        out.append({"value": round(dec_bytes * passes / dt / 1e9, 4), "unit": "decoded GB/s",
+                    "rows_per_s": round(rows * passes / dt, 1), "cores": threads, "kind": "port",
+                    "sample": f"whole file ({nrg} row groups x {ncol} chunks, {rows} rows), {passes} passes, "
+                              f"{threads} thread(s), oracle/pf_oracle.c (C port of parquet-mr 1.12.2 + Snappy)"})
+    for of in files:
+        of.close()
+    try:
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+        for threads in (1, cores):
+            pa.set_cpu_count(threads)
+            passes, t0 = 0, time.perf_counter()
+            while True:
+                pq.read_table(path, use_threads=threads > 1)
+                passes += 1
+                if time.perf_counter() - t0 > budget_s or passes >= 20:
+                    break
+            dt = time.perf_counter() - t0
+            out.append({"value": round(dec_bytes * passes / dt / 1e9, 4), "unit": "decoded GB/s (same byte count)",
+                        "rows_per_s": round(rows * passes / dt, 1), "cores": threads, "kind": "pyarrow",
+                        "sample": f"pyarrow {pa.__version__} parquet.read_table of the whole file, {passes} passes, "
+                                  f"{threads} thread(s) (Arrow C++ reader, not the reference)"})
+    except Exception as e:   # reported, never fatal
+        out.append({"kind": "pyarrow", "error": repr(e)})
+    best = out[1]
+    return dict(best, variants=out, note="Java reference CPU baseline unavailable (no JDK / parquet-mr jars on "
+                                         "the box); the oracle port and pyarrow are timed instead")
+
+
+# --------------------------------------------------------------------------- parity of the timed outputs
+
+def check_parity(path, pf, decs, last_batches, budget_threads):
+    """Bit-exact comparison of every chunk of every context's last timed batch (still resident on
+    the device) with the CPU oracle; physical row groups the timed batches did not cover are decoded
+    once more and compared too. Oracle decodes run in a thread pool (outside any timing)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden_util import assert_chunk_equal
+    from oracle_binding import Oracle
+    orc = Oracle(os.path.join(ROOT, "oracle", "libpf_oracle.so"))
+    handles = threading.local()
+
+    def oracle_decode(key):
+        if not hasattr(handles, "f"):
+            handles.f = orc.open(path)
+        return handles.f.decode(*key)
+
+    todo = []
+    for dec, bi in zip(decs, last_batches):
+        for i, (p, c, *_r) in enumerate(bi.items):
+            col = pf.columns[c]
+            todo.append(((p, c), dec.fetch(i, col.physical_type, col.max_def, col.max_rep)))
+    checked = {k for k, _ in todo}
+    n_ok, bad = 0, []
+    with cf.ThreadPoolExecutor(budget_threads) as ex:
+        futs = {ex.submit(oracle_decode, k): (k, g) for k, g in todo}
+        for fu in cf.as_completed(futs):
+            k, g = futs[fu]
+            try:
+                assert g["status"] == 0, f"status {g['status']}"
+                assert_chunk_equal(g, fu.result(), f"rg{k[0]} c{k[1]}")
+                n_ok += 1
+            except AssertionError as e:
+                bad.append(str(e)[:200])
+    return {"chunks": len(todo), "bit_exact": not bad and n_ok == len(todo), "row_groups": sorted({k[0] for k in checked}),
+            "mismatches": bad[:5], "against": "oracle/pf_oracle.c (CPU restatement, pinned to pyarrow golden vectors)"}
+
+
+# --------------------------------------------------------------------------- main
+
+def spawn_ranks(args, argv):
+    """--gpus N without a launcher: start N ranks as child processes (no GPU call happens here)."""
+    make_input(args)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+def run_contexts(decs, batches, on_device):
+    """Each context decodes its batches in order on its own host thread (ctypes releases the GIL);
+    a single-batch context is enqueued from this thread."""
+    if all(len(b) <= 1 for b in batches):
+        for d, bl in zip(decs, batches):
+            for bi in bl:
+                d.decode(bi.descs, (bi.dev if on_device else bi.host.ptr).value, bi.nbytes, on_device=on_device)
+        for d, bl in zip(decs, batches):
+            if bl and d.wait() != 0:
+                raise RuntimeError(d.error())
+        return
+    errs = []
+
+    def worker(d, bl):
+        try:
+            for bi in bl:
+                d.decode(bi.descs, (bi.dev if on_device else bi.host.ptr).value, bi.nbytes, on_device=on_device)
+                if d.wait() != 0:
+                    raise RuntimeError(d.error())
+        except Exception as e:
+            errs.append(e)
+    ts = [threading.Thread(target=worker, args=(d, bl)) for d, bl in zip(decs, batches)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    if errs:
+        raise errs[0]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=SF1_ROWS)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="sf1")
     ap.add_argument("--data-dir", default=os.environ.get("PF_BENCH_DIR", "/tmp/pfloor_bench"))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=4,
-                    help="decode contexts (HIP streams) per GPU; row groups are dealt round-robin to them")
-    args = ap.parse_args()
+                    help="decode contexts (HIP streams) per GPU; work units are dealt round-robin to them")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    args, _ = ap.parse_known_args()
+    if args.pmc_child:
+        return pmc_child(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args, sys.argv[1:])
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -173,46 +467,62 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)   # barrier/timing only
+        dist.init_process_group("gloo", rank=rank, world_size=world)   # barriers + max-over-ranks time only
+    if rank == 0:
+        make_input(args)
+    if dist:
+        dist.barrier()
+    path = input_path(args)
+
+    # HBM traffic of the roofline kernels: rocprofv3 child processes, before this process touches the GPU
+    pmc = None
+    if world == 1 and not args.no_pmc:
+        try:
+            pmc = measure_pmc(args, "k_snappy_exec|k_snappy_index|k_snappy_chain|k_flat")
+        except Exception as e:
+            pmc = {"error": repr(e)}
 
     import torch
     from pfloor import _native
-    from pfloor.decoder import GpuDecoder
-
-    os.makedirs(args.data_dir, exist_ok=True)
-    path = os.path.join(args.data_dir, f"lineitem_{args.rows}_seed{SEED}_rg{RG_ROWS}.parquet")
-    if rank == 0 and not os.path.exists(path):
-        make_input(path, args.rows)
-    if dist:
-        dist.barrier()
+    from pfloor.decoder import GpuDecoder, ParquetFile
 
     device = local_rank
     torch.cuda.set_device(device)
-    pf, items, host, descs = plan_file(path)
-    st = page_stats(descs)
-    # S contexts on this GPU (one HIP stream each): row group r goes to context r % S, so one row
-    # group's latency-bound Snappy index / chain passes overlap another's decode kernels.
-    S = max(1, min(args.streams, pf.num_row_groups))
+    pf = ParquetFile(path)
+    plan, n_log, mine = units_for_rank(args, pf, world, rank, args.streams)
+    S = len(plan)
     decs = [GpuDecoder(device) for _ in range(S)]
-    dec = decs[0]
-    parts = [[i for i, it in enumerate(items) if it[0] % S == k] for k in range(S)]
-    part_descs = [[descs[i] for i in idx] for idx in parts]
-    L = _native.lib()
-    d_in = C.c_void_p()
-    _native.check(L.pf_device_alloc(dec.h, host.nbytes, C.byref(d_in)), dec.h, "pf_device_alloc")
-    _native.check(L.pf_memcpy_h2d(dec.h, d_in, host.ctypes.data, host.nbytes), dec.h, "h2d")
+    # batch inputs, cached by physical content (sf100 replicas share one device copy)
+    cache = {}
+    batches = []
+    for k, bl in enumerate(plan):
+        row = []
+        for units in bl:
+            key = tuple((p, tuple(cols)) for _g, p, cols in units)
+            if key not in cache:
+                bi = BatchInput(pf, units, decs[0].h)
+                bi.upload(decs[0])
+                cache[key] = bi
+            row.append(cache[key])
+        batches.append(row)
+    _native.check(_native.lib().pf_sync(decs[0].h), decs[0].h, "pf_sync")   # uploads done before any context reads them
 
     def step():
-        for d, dd in zip(decs, part_descs):
-            d.decode(dd, d_in.value, host.nbytes, on_device=True)
-        for d in decs:
-            rc = d.wait()
-            if rc != 0:
-                raise RuntimeError(d.error())
+        run_contexts(decs, batches, True)
 
     for _ in range(args.warmup):
         step()
-    dbytes, rows = decoded_bytes(decs, parts, pf, items)
+    # decoded bytes of one step (every batch's result is identical each step)
+    dbytes = 0
+    for d, bl in zip(decs, batches):
+        for bi in bl:
+            d.decode(bi.descs, bi.dev.value, bi.nbytes, on_device=True)
+            if d.wait() != 0:
+                raise RuntimeError(d.error())
+            for i, (p, c, *_r) in enumerate(bi.items):
+                dbytes += chunk_decoded_bytes(pf.columns[c], d.info(i))
+    rows = sum(pf.row_group_rows(g % pf.num_row_groups) for g in mine) if args.workload != "wide" else \
+        pf.row_group_rows(0)
     stage_acc = {}
     torch.cuda.synchronize()
     if dist:
@@ -220,97 +530,248 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        for k, v in dec.timing().items():
+        for k, v in decs[0].timing().items():
             stage_acc[k] = stage_acc.get(k, 0.0) + v
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    tot = np.array([dbytes, rows], dtype=np.float64)
     if dist:
-        t = torch.tensor([dt], dtype=torch.float64)
+        import torch as _t
+        t = _t.tensor([dt], dtype=_t.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        tt = _t.tensor(tot)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        tot = tt.numpy()
     stage_ms = {k: v / args.steps for k, v in stage_acc.items()}
     ms_per_step = dt / args.steps * 1e3
-    n = world
-    value = dbytes * n * args.steps / dt / 1e9
+    value = float(tot[0]) * args.steps / dt / 1e9
 
-    # roofline of the dominant kernel stage: HIP events on context 0's stream, priced with the
-    # algorithmic bytes of context 0's share of the pages
-    st0 = page_stats(part_descs[0])
-    dbytes0, _ = decoded_bytes(decs[:1], parts[:1], pf, items)
-    kern_bytes = {
-        "snappy_exec": st0["snappy_in"] + st0["snappy_out"],   # compressed read + decompressed written
-        "snappy_parse": st0["snappy_in"],                       # compressed read (token index)
-        "decode": st0["uncompressed"] + dbytes0,   # page bodies read + decoded bytes written
-        "flat": st0["uncompressed"] + dbytes0,
-    }
-    dom = max((k for k in stage_ms if k != "h2d"), key=lambda k: stage_ms.get(k, 0.0))
-    # per-launch kernel time of the dominant stage without a concurrent stream: with several contexts
-    # the HIP events on context 0 also count the time its kernels wait for CUs held by context 1,
-    # which rocprof's kernel durations do not. Context 0's share, decoded alone, ROOF_PASSES times
-    # after the timed region (HIP events on its stream bracket exactly that stage's launches).
+    # ---- parity of the timed outputs (each context's last batch is still resident) ----
+    parity = None
+    if not args.no_parity:
+        t1 = time.time()
+        try:
+            parity = check_parity(path, pf, decs, [bl[-1] for bl in batches], _host_cores())
+        except Exception as e:
+            parity = {"bit_exact": False, "error": repr(e)}
+        log(f"[bench] parity {parity.get('chunks')} chunks bit_exact={parity.get('bit_exact')} in {time.time() - t1:.1f}s")
+
+    # ---- roofline of the dominant stage: context 0's first batch decoded alone ----
+    b0 = batches[0][0]
+    st0 = page_stats(b0.descs)
+    dbytes0 = 0
     iso = {}
-    for _ in range(ROOF_PASSES):
-        dec.decode(part_descs[0], d_in.value, host.nbytes, on_device=True)
+    dec = decs[0]
+    for r in range(ROOF_PASSES):
+        dec.decode(b0.descs, b0.dev.value, b0.nbytes, on_device=True)
         if dec.wait() != 0:
             raise RuntimeError(dec.error())
         for k, v in dec.timing().items():
             iso[k] = iso.get(k, 0.0) + v / ROOF_PASSES
+    for i, (p, c, *_r) in enumerate(b0.items):
+        dbytes0 += chunk_decoded_bytes(pf.columns[c], dec.info(i))
+    kern_bytes = {
+        "snappy_exec": st0["snappy_in"] + st0["snappy_out"],   # compressed read + decompressed written
+        "snappy_parse": st0["snappy_in"],                       # compressed read (token index)
+        "flat": st0["uncompressed"] + dbytes0,                  # page bodies read + decoded bytes written
+        "decode": st0["uncompressed"] + dbytes0,
+    }
+    dom = max((k for k in iso if k in kern_bytes), key=lambda k: iso.get(k, 0.0))
     dom_ms = iso.get(dom, 0.0)
-    dom_bytes = kern_bytes.get(dom)
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if (dom_bytes and dom_ms > 0) else None
-    # HBM traffic of the dominant kernel: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE per
-    # launch over the whole file at 1 stream (tools/gpu_pmc.sh -> tools/pmc_traffic.json), scaled
-    # to context 0's share of the algorithmic bytes
-    traffic = None
-    try:
-        pmc = json.load(open(os.path.join(ROOT, "tools", "pmc_traffic.json")))
-        whole = {"snappy_exec": st["snappy_in"] + st["snappy_out"]}
-        if f"k_{dom}" in pmc and dom in whole and dom_bytes:
-            traffic = round(pmc[f"k_{dom}"]["traffic_bytes"] * dom_bytes / whole[dom])
-    except (OSError, ValueError, KeyError):
-        pass
-    b_alg = st["compressed"] + dbytes
+    dom_bytes = kern_bytes[dom]
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else None
+    traffic, traffic_detail = None, None
+    if pmc and "error" not in pmc:
+        traffic_detail = pmc_traffic_per_kernel(pmc)
+        kmap = {"snappy_exec": ["k_snappy_exec"], "snappy_parse": ["k_snappy_index", "k_snappy_chain"],
+                "flat": ["k_flat", "k_flat_fixed"]}
+        names = kmap.get(dom, [])
+        if names and all(n in traffic_detail for n in names):
+            traffic = sum(traffic_detail[n]["traffic_bytes"] for n in names)
+    b_alg_step = None
+    descs_all = [d for bl in batches for bi in bl for d in bi.descs]
+    st_all = page_stats(descs_all)
+    b_alg_step = st_all["compressed"] + dbytes
+
+    # ---- end to end: pinned host input -> H2D -> decode -> D2H into pinned host columns ----
+    e2e = None
+    if not args.no_e2e:
+        try:
+            e2e = measure_e2e(decs, batches, pf, st_all)
+        except Exception as e:
+            e2e = {"error": repr(e)}
+
+    w = WORKLOADS[args.workload]
+    if args.workload == "sf1":
+        wl = (f"lineitem SF1 x{world} ({w['rows']} rows x {world}, 16 cols, {pf.num_row_groups * world} row groups of 1Mi rows), "
+              "Snappy + dictionary, device-resident")
+        scaling = "weak"
+    elif args.workload == "sf100":
+        wl = (f"lineitem SF100-shaped ({n_log} row groups of {w['rg_rows']} rows = {n_log * w['rg_rows']} rows; the "
+              f"{pf.num_row_groups} distinct synthetic row groups stand for the {n_log}), Snappy + dictionary, device-resident")
+        scaling = "strong"
+    else:
+        wl = (f"wide: {w['rows']} rows x {pf.num_columns} nullable INT32/FLOAT columns, 30% nulls, 100K-value dictionaries, "
+              "Snappy, device-resident")
+        scaling = "strong"
     out = {
-        "metric": "decoded GB/s + rows/s (node), lineitem-shape Snappy+dict, 1/2/4/8 GPUs",
+        "metric": METRIC,
         "value": round(value, 3), "unit": "decoded GB/s",
-        "rows_per_s": round(rows * n * args.steps / dt, 1),
-        "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+        "rows_per_s": round(float(tot[1]) * args.steps / dt, 1),
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u8", "data": "synthetic (pyarrow-written lineitem-shaped file, seed 42)",
-        "config": {"workload": f"lineitem SF1 ({rows} rows, 16 cols, {len(descs)} chunks, {st['pages']} pages), "
-                               "Snappy + dictionary, 1Mi-row row groups, device-resident",
-                   "rows": rows, "row_groups": pf.num_row_groups, "compressed_page_bytes": st["compressed"],
-                   "uncompressed_page_bytes": st["uncompressed"], "decoded_bytes": dbytes,
-                   "parallelism": f"row groups sharded per GPU x{n} (no collective), {S} decode streams per GPU"},
+        "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
+        "dtype": "u8", "data": f"synthetic (pyarrow-written {w['kind']}-shaped file, seed {w['seed']})",
+        "config": {"workload": wl, "rows_per_step": int(tot[1]),
+                   "row_groups_per_rank": len(mine), "decoded_bytes_per_step": int(tot[0]),
+                   "compressed_page_bytes_rank0": st_all["compressed"],
+                   "parallelism": f"row groups sharded round-robin over {world} GPU(s) (pfloor.shard, no collective), "
+                                  f"{S} decode streams per GPU"},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "roofline": {"bound": "hbm", "kernel": f"k_{dom}", "achieved": round(achieved, 2) if achieved else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": traffic,
-                     "traffic_source": "rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE per launch (tools/gpu_pmc.sh)",
+                     "traffic_source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE per launch, measured in "
+                                       "this run (child processes, same batch, 1 stream)" if traffic else
+                                       (pmc or {}).get("error"),
                      "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4),
-                     "launch_ms_source": f"HIP events on context 0's stream, its row groups decoded alone x{ROOF_PASSES} "
+                     "launch_ms_source": f"HIP events on context 0's stream, its first batch decoded alone x{ROOF_PASSES} "
                                          "after the timed region",
                      "stage_ms_overlapped": round(stage_ms.get(dom, 0.0), 4)},
-        "pipeline_roofline": {"b_alg": b_alg, "ms_per_step": round(ms_per_step, 4),
-                              "achieved": round(b_alg * n / (ms_per_step * 1e-3) / 1e9, 2),
-                              "frac": round(b_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
+        "pipeline_roofline": {"b_alg_per_step_rank0": b_alg_step, "ms_per_step": round(ms_per_step, 4),
+                              "achieved": round(b_alg_step / (ms_per_step * 1e-3) / 1e9, 2),
+                              "frac": round(b_alg_step / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
     }
-    if rank == 0 and n == 1 and not args.no_cpu_baseline:
+    if traffic_detail:
+        out["pmc_traffic_per_launch"] = traffic_detail
+    if parity is not None:
+        out["parity"] = parity
+    if e2e is not None:
+        out["e2e"] = e2e
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(path, pf)
+            out["cpu_baseline"] = cpu_baselines(path, pf)
         except Exception as e:   # reported, never fatal
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
-    L.pf_device_free(dec.h, d_in)
+    for bi in cache.values():
+        bi.free(decs[0])
     for d in decs:
         d.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+    if parity is not None and not parity.get("bit_exact"):
+        log("[bench] PARITY FAILURE")
+        return 3
+    return 0
+
+
+def measure_e2e(decs, batches, pf, st_all):
+    """Whole rank share, E2E_PASSES times: per context, per batch: pinned H2D of the batch's chunk
+    bytes (inside pf_decode_row_group), decode, pf_wait, then pf_copy_columns_async of every chunk
+    into pinned host buffers; the next batch on that context is ordered after those copies."""
+    from pfloor import _native
+    from pfloor.decoder import PinnedBuffer
+    from pfloor._native import ColumnOut
+    L = _native.lib()
+    # output layout per batch from one decode (sizes are the same every pass)
+    layouts = []
+    d2h = 0
+    for d, bl in zip(decs, batches):
+        row = []
+        for bi in bl:
+            d.decode(bi.descs, bi.dev.value, bi.nbytes, on_device=True)
+            if d.wait() != 0:
+                raise RuntimeError(d.error())
+            infos = [d.info(i) for i in range(len(bi.items))]
+            row.append(infos)
+        layouts.append(row)
+    # pinned output buffers: one per context, sized for its largest batch
+    outs = []
+    for ctx_i, (d, bl) in enumerate(zip(decs, batches)):
+        per_batch = []
+        need_max = 0
+        for bj, bi in enumerate(bl):
+            fields = []
+            off = 0
+            for i, (p, c, *_r) in enumerate(bi.items):
+                ci = layouts[ctx_i][bj][i]
+                col = pf.columns[c]
+                f = {}
+
+                def take(name, n):
+                    nonlocal off
+                    f[name] = (off, n)
+                    off += (n + 255) // 256 * 256
+                if col.physical_type == 6:
+                    take("offsets", 4 * (ci.num_slots + 1))
+                    take("chars", ci.num_chars)
+                else:
+                    take("values", ci.num_slots * ci.width)
+                if col.max_def > 0:
+                    take("validity", (ci.num_slots + 7) // 8)
+                if col.max_rep == 1:
+                    take("list_offsets", 4 * (ci.num_rows + 1))
+                    take("list_validity", (ci.num_rows + 7) // 8)
+                if col.max_rep > 0:
+                    take("def_levels", ci.num_entries)
+                    take("rep_levels", ci.num_entries)
+                fields.append(f)
+            per_batch.append(fields)
+            need_max = max(need_max, off)
+        buf = PinnedBuffer(d.h, need_max)
+        arrs = []
+        for fields in per_batch:
+            arr = (ColumnOut * max(1, len(fields)))()
+            for i, f in enumerate(fields):
+                for name, (o, n) in f.items():
+                    setattr(arr[i], name, buf.ptr.value + o if n else None)
+                    setattr(arr[i], name + "_cap", n)
+                    d2h += n
+            idx = (C.c_int * max(1, len(fields)))(*range(len(fields)))
+            arrs.append((arr, idx, len(fields)))
+        outs.append((buf, arrs))
+    d2h_per_pass = d2h
+    h2d_per_pass = sum(bi.nbytes for bl in batches for bi in bl)
+    errs = []
+
+    def worker(ci, d, bl):
+        try:
+            for bj, bi in enumerate(bl):
+                d.decode(bi.descs, bi.host.ptr.value, bi.nbytes, on_device=False)
+                if d.wait() != 0:
+                    raise RuntimeError(d.error())
+                arr, idx, n = outs[ci][1][bj]
+                _native.check(L.pf_copy_columns_async(d.h, n, idx, arr), d.h, "pf_copy_columns_async")
+            _native.check(L.pf_sync(d.h), d.h, "pf_sync")
+        except Exception as e:
+            errs.append(e)
+
+    def one_pass():
+        ts = [threading.Thread(target=worker, args=(i, d, bl)) for i, (d, bl) in enumerate(zip(decs, batches))]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        if errs:
+            raise errs[0]
+    one_pass()   # warm-up (first touch of the pinned outputs)
+    t0 = time.perf_counter()
+    for _ in range(E2E_PASSES):
+        one_pass()
+    dt = (time.perf_counter() - t0) / E2E_PASSES
+    for buf, _ in outs:
+        buf.free()
+    decoded = d2h_per_pass
+    t_link = max(h2d_per_pass, d2h_per_pass) / (PCIE_GBS * 1e9)
+    return {"value": round(decoded / dt / 1e9, 3), "unit": "decoded GB/s (pinned host in -> host columns out)",
+            "ms_per_pass": round(dt * 1e3, 3), "h2d_bytes": h2d_per_pass, "d2h_bytes": d2h_per_pass,
+            "pcie_bound_gbs": PCIE_GBS, "frac": round(t_link / dt, 4),
+            "frac_definition": "max(H2D, D2H bytes) / 63 GB/s divided by the measured pass time",
+            "passes": E2E_PASSES}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -184,6 +184,17 @@ int pf_column_info_get(pf_ctx* ctx, int chunk, pf_column_info* out);
  * Fails with PF_ERR_CAPACITY (nothing copied) if any non-NULL buffer is too small. */
 int pf_copy_column(pf_ctx* ctx, int chunk, const pf_column_out* out);
 
+/* Batched, asynchronous form of pf_copy_column for the end-to-end pipeline (the Java side reads
+ * a row group's selected chunks into pinned output segments, ParquetReader.java:183-192): all
+ * capacities are checked first (PF_ERR_CAPACITY, nothing enqueued), then the D2H copies of the
+ * n chunks are enqueued on the context stream. Destination buffers should be pinned
+ * (pf_host_alloc) and stay valid until pf_sync. A later pf_decode_row_group on the same
+ * context is ordered after these copies (same stream), so decode i+1 can be enqueued at once. */
+int pf_copy_columns_async(pf_ctx* ctx, int n, const int* chunks, const pf_column_out* outs);
+
+/* Block until everything enqueued on the context (copies included) has finished. */
+int pf_sync(pf_ctx* ctx);
+
 /* Kernel timing of the last decode (sum of per-stage HIP-event times, ms). */
 int pf_last_timing(pf_ctx* ctx, float* stage_ms, int n_stages, int* n_written);
 
@@ -206,6 +217,7 @@ typedef struct pf_column_meta {
     int32_t physical_type, type_length, max_def, max_rep, repeated_def, list_null_def;
     int32_t converted_type;       /* SchemaElement.converted_type or -1 */
     int32_t logical_type;         /* LogicalType union field id or 0 */
+    int32_t scale, precision;     /* DECIMAL (SchemaElement 7/8 or LogicalType DecimalType) */
 } pf_column_meta;
 
 int pf_file_open(const char* path, pf_file** out);

@@ -79,6 +79,7 @@ int pf_file_column_meta(pf_file* f, int column, pf_column_meta* out) {
     out->max_def = L.max_def; out->max_rep = L.max_rep;
     out->repeated_def = L.repeated_def; out->list_null_def = L.list_null_def;
     out->converted_type = L.converted_type; out->logical_type = L.logical_type;
+    out->scale = L.scale; out->precision = L.precision;
     return PF_OK;
 }
 

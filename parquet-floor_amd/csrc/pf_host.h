@@ -37,6 +37,7 @@ struct LeafMeta {
     std::string path, top;
     int physical_type = -1, type_length = 0, max_def = 0, max_rep = 0, repeated_def = 0, list_null_def = 0;
     int converted_type = -1, logical_type = 0;
+    int scale = 0, precision = 0;
 };
 
 struct FileMeta {

@@ -106,6 +106,7 @@ struct ThriftReader {
 struct SchemaNode {
     std::string name;
     int type = -1, type_length = 0, repetition = 0, num_children = 0, converted = -1, logical = 0;
+    int scale = 0, precision = 0;                 // SchemaElement 7/8, or LogicalType DECIMAL {1 scale, 2 precision}
 };
 
 SchemaNode read_schema_node(ThriftReader& r) {
@@ -119,10 +120,22 @@ SchemaNode read_schema_node(ThriftReader& r) {
         case 4: n.name = r.str(t); break;
         case 5: n.num_children = int(r.integer(t)); break;
         case 6: n.converted = int(r.integer(t)); break;
+        case 7: n.scale = int(r.integer(t)); break;
+        case 8: n.precision = int(r.integer(t)); break;
         case 10:
             if (t == 12) {   // LogicalType union: remember which member is set
                 int l2 = 0, i2, t2;
-                while (r.field(l2, i2, t2)) { n.logical = i2; r.skip(t2); }
+                while (r.field(l2, i2, t2)) {
+                    n.logical = i2;
+                    if (i2 == 5 && t2 == 12) {   // DecimalType
+                        int l3 = 0, i3, t3;
+                        while (r.field(l3, i3, t3)) {
+                            if (i3 == 1) n.scale = int(r.integer(t3));
+                            else if (i3 == 2) n.precision = int(r.integer(t3));
+                            else r.skip(t3);
+                        }
+                    } else r.skip(t2);
+                }
             } else r.skip(t);
             break;
         default: r.skip(t);
@@ -214,6 +227,7 @@ void FileMeta::parse_footer(const uint8_t* p, size_t n) {
         L.repeated_def = me.rep ? me.repeated_def : 0;
         L.list_null_def = me.rep ? me.list_null_def : 0;
         L.converted_type = nd.converted; L.logical_type = nd.logical;
+        L.scale = nd.scale; L.precision = nd.precision;
         leaves.push_back(std::move(L));
     };
     walk(0, Frame{0, 0, 0, 0, "", ""});

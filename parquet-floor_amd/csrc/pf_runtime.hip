@@ -97,6 +97,8 @@ struct pf_ctx {
     // last batch
     int n_chunks = 0;
     bool pending = false;
+    bool copies_pending = false;           // pf_copy_columns_async enqueued, not yet pf_sync'ed
+    bool tables_from_decode = false;       // d_meta layout (off_fallback) belongs to a pf_decode_row_group
     bool timing_valid = false;
     std::vector<DevChunk> chunks;          // host copies (device pointers)
     std::vector<DevPage> pages;
@@ -287,6 +289,15 @@ int upload_meta(pf_ctx* ctx) {
         std::copy(v->begin(), v->end(), lists + lo);
         lo += v->size();
     }
+    {   // diagnostics: PF_DEBUG_FORCE_SERIAL=k sends every k-th Snappy job to the serial kernel
+        // (tests of k_snappy_serial's grid-stride over many jobs; valid streams never fall back)
+        const char* e = std::getenv("PF_DEBUG_FORCE_SERIAL");
+        const int k = e ? std::atoi(e) : 0;
+        int* fbh = reinterpret_cast<int*>(h + ctx->off_fallback);
+        if (k > 0)
+            for (size_t j = 0; j < ctx->jobs.size(); j++)
+                if (int(j % size_t(k)) == k - 1) fbh[j] = FB_SERIAL;
+    }
     DevChunkResult* r = reinterpret_cast<DevChunkResult*>(h + ctx->off_res);
     for (int c = 0; c < ctx->n_chunks; c++) {
         r[c].status = int32_t(ctx->host_status[c]);
@@ -318,15 +329,9 @@ int pf_device_count(int* count) {
     return PF_OK;
 }
 
-int pf_ctx_create(int device, pf_ctx** out) {
-    if (!out) return fail(nullptr, PF_ERR_INVALID_ARG, "null out");
-    *out = nullptr;
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
-        return fail(nullptr, PF_ERR_INVALID_ARG, "no such HIP device");
-    auto ctx = std::make_unique<pf_ctx>();
-    ctx->device = device;
-    HIPCHK(nullptr, hipSetDevice(device));
+namespace {
+int ctx_init(pf_ctx* ctx) {
+    HIPCHK(nullptr, hipSetDevice(ctx->device));
     const char* es = std::getenv("PF_EXEC_STREAM");
     if (es && es[0] && es[0] != '0') {
         int least = 0, greatest = 0;
@@ -339,7 +344,26 @@ int pf_ctx_create(int device, pf_ctx** out) {
         HIPCHK(nullptr, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     }
     for (auto& e : ctx->ev) HIPCHK(nullptr, hipEventCreate(&e));
-    *out = ctx.release();
+    return PF_OK;
+}
+}  // namespace
+
+int pf_ctx_create(int device, pf_ctx** out) {
+    if (!out) return fail(nullptr, PF_ERR_INVALID_ARG, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return fail(nullptr, PF_ERR_INVALID_ARG, "no such HIP device");
+    pf_ctx* ctx = new pf_ctx();
+    ctx->device = device;
+    const int rc = ctx_init(ctx);
+    if (rc != PF_OK) {   // release whatever streams / events were created before the failure
+        const std::string msg = g_err;
+        pf_ctx_destroy(ctx);
+        g_err = msg;
+        return rc;
+    }
+    *out = ctx;
     return PF_OK;
 }
 
@@ -561,10 +585,13 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         if (pass == 0) { ctx->n_ba_dict = int(ctx->bajobs.size()); ctx->n_ba_dict_tiles = int(ctx->ba_tiles.size()); }
     }
     // ---- allocate arenas ----
+    size_t chars_cap = std::max<size_t>(size_t(2 * chars_hint) + (16u << 20), ctx->chars_need);
+    if (ctx->copies_pending && (out > ctx->d_out.cap || bits > ctx->d_bits.cap || chars_cap > ctx->d_chars.cap))
+        HIPCHK(ctx, hipStreamSynchronize(st));   // a growing output arena must not be freed under a pending D2H copy
+    ctx->copies_pending = false;
     HIPCHK(ctx, ctx->d_scratch.ensure(std::max<size_t>(scratch, 1)));
     HIPCHK(ctx, ctx->d_out.ensure(std::max<size_t>(out, 1)));
     HIPCHK(ctx, ctx->d_bits.ensure(std::max<size_t>(bits, 1)));
-    size_t chars_cap = std::max<size_t>(size_t(2 * chars_hint) + (16u << 20), ctx->chars_need);
     HIPCHK(ctx, ctx->d_chars.ensure(chars_cap));
     ctx->bits_bytes = bits;
     uint8_t* S = static_cast<uint8_t*>(ctx->d_scratch.p);
@@ -680,6 +707,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     rc = enqueue_kernels(ctx);
     if (rc) return rc;
     ctx->pending = true;
+    ctx->tables_from_decode = true;
     return PF_OK;
 }
 
@@ -751,7 +779,9 @@ int pf_column_info_get(pf_ctx* ctx, int chunk, pf_column_info* out) {
     return PF_OK;
 }
 
-int pf_copy_column(pf_ctx* ctx, int chunk, const pf_column_out* o) {
+namespace {
+// Enqueue the D2H copies of chunk i's arrays on the context stream (no synchronisation).
+int enqueue_copy(pf_ctx* ctx, int chunk, const pf_column_out* o) {
     if (!ctx || !o) return fail(ctx, PF_ERR_INVALID_ARG, "null arg");
     if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
     if (chunk < 0 || chunk >= ctx->n_chunks) return fail(ctx, PF_ERR_INVALID_ARG, "chunk index out of range");
@@ -773,7 +803,53 @@ int pf_copy_column(pf_ctx* ctx, int chunk, const pf_column_out* o) {
     HIPCHK(ctx, hipSetDevice(ctx->device));
     for (const Item& it : items)
         if (it.dst && it.src && it.n) HIPCHK(ctx, hipMemcpyAsync(it.dst, it.src, it.n, hipMemcpyDeviceToHost, ctx->stream));
+    return PF_OK;
+}
+}  // namespace
+
+int pf_copy_column(pf_ctx* ctx, int chunk, const pf_column_out* o) {
+    const int rc = enqueue_copy(ctx, chunk, o);
+    if (rc) return rc;
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return PF_OK;
+}
+
+int pf_copy_columns_async(pf_ctx* ctx, int n, const int* chunks, const pf_column_out* outs) {
+    if (!ctx || n < 0 || (n > 0 && (!chunks || !outs))) return fail(ctx, PF_ERR_INVALID_ARG, "bad arguments");
+    for (int i = 0; i < n; i++) {   // capacities first: nothing is enqueued if any buffer is too small
+        if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
+        const int c = chunks[i];
+        if (c < 0 || c >= ctx->n_chunks) return fail(ctx, PF_ERR_INVALID_ARG, "chunk index out of range");
+        const pf_column_info& ci = ctx->info[c];
+        if (ci.status != 0) return fail(ctx, ci.status, "chunk failed to decode");
+        const pf_column_out& o = outs[i];
+        const size_t need[8] = {size_t(ci.num_slots) * size_t(ci.width), size_t((ci.num_slots + 7) / 8),
+                                ci.d_offsets ? 4 * size_t(ci.num_slots + 1) : 0, size_t(ci.num_chars),
+                                ci.d_list_offsets ? 4 * size_t(ci.num_rows + 1) : 0, size_t((ci.num_rows + 7) / 8),
+                                size_t(ci.num_entries), size_t(ci.num_entries)};
+        const void* dst[8] = {o.values, o.validity, o.offsets, o.chars, o.list_offsets, o.list_validity, o.def_levels,
+                              o.rep_levels};
+        const void* src[8] = {ci.d_values, ci.d_validity, ci.d_offsets, ci.d_chars, ci.d_list_offsets, ci.d_list_validity,
+                              ci.d_def_levels, ci.d_rep_levels};
+        const size_t cap[8] = {o.values_cap, o.validity_cap, o.offsets_cap, o.chars_cap, o.list_offsets_cap,
+                               o.list_validity_cap, o.def_levels_cap, o.rep_levels_cap};
+        for (int k = 0; k < 8; k++)
+            if (dst[k] && src[k] && need[k] > cap[k]) return fail(ctx, PF_ERR_CAPACITY, "output buffer too small");
+    }
+    for (int i = 0; i < n; i++) {
+        const int rc = enqueue_copy(ctx, chunks[i], &outs[i]);
+        if (rc) return rc;
+    }
+    ctx->copies_pending = n > 0 || ctx->copies_pending;
+    return PF_OK;
+}
+
+int pf_sync(pf_ctx* ctx) {
+    if (!ctx) return fail(nullptr, PF_ERR_INVALID_ARG, "null ctx");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->copies_pending = false;
     return PF_OK;
 }
 
@@ -793,8 +869,11 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     if (n > 0xffffffffull || ulen > 0xffffffffull) return fail(ctx, PF_ERR_INVALID_ARG, "snappy: buffer too large");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
+    if (ctx->copies_pending) HIPCHK(ctx, hipStreamSynchronize(st));   // arenas may be reallocated below
+    ctx->copies_pending = false;
     ctx->n_chunks = 0;
     ctx->info.clear();
+    ctx->tables_from_decode = false;   // d_meta now holds this call's layout
     HIPCHK(ctx, ctx->d_in.ensure(std::max<size_t>(n, 1)));
     HIPCHK(ctx, ctx->d_scratch.ensure(std::max<size_t>(ulen, 1) + 16));
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
@@ -860,7 +939,8 @@ int pf_debug_snappy_tables(pf_ctx* ctx, uint32_t* splits, int n_splits, uint32_t
 // Diagnostics (not part of pfloor.h): per Snappy job of the last finished pf_decode_row_group,
 // {fallback flag (FB_*), compressed length, decompressed length, chunk, page}. Returns the job count.
 int pf_debug_snappy_fallback(pf_ctx* ctx, int* out, int n_jobs) {
-    if (!ctx || !ctx->d_meta.p) return fail(ctx, PF_ERR_STATE, "no decode");
+    if (!ctx || !ctx->d_meta.p || !ctx->tables_from_decode) return fail(ctx, PF_ERR_STATE, "no finished decode");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     const int nj = int(ctx->jobs.size());
     const int m = n_jobs < nj ? n_jobs : nj;

@@ -57,7 +57,7 @@ class ColumnMeta(C.Structure):
     _fields_ = [("path", C.c_char_p), ("top_name", C.c_char_p), ("physical_type", C.c_int32),
                 ("type_length", C.c_int32), ("max_def", C.c_int32), ("max_rep", C.c_int32),
                 ("repeated_def", C.c_int32), ("list_null_def", C.c_int32), ("converted_type", C.c_int32),
-                ("logical_type", C.c_int32)]
+                ("logical_type", C.c_int32), ("scale", C.c_int32), ("precision", C.c_int32)]
 
 
 class PfError(RuntimeError):
@@ -94,6 +94,8 @@ def lib():
         "pf_wait": ([vp], C.c_int),
         "pf_column_info_get": ([vp, i32, C.POINTER(ColumnInfo)], C.c_int),
         "pf_copy_column": ([vp, i32, C.POINTER(ColumnOut)], C.c_int),
+        "pf_copy_columns_async": ([vp, i32, C.POINTER(C.c_int), C.POINTER(ColumnOut)], C.c_int),
+        "pf_sync": ([vp], C.c_int),
         "pf_last_timing": ([vp, C.POINTER(C.c_float), i32, C.POINTER(C.c_int)], C.c_int),
         "pf_snappy_decompress": ([vp, vp, sz, vp, sz, C.POINTER(C.c_size_t)], C.c_int),
         "pf_snappy_last_fallback": ([vp], C.c_int),

@@ -28,6 +28,8 @@ class ColumnDescriptor:
         self.list_null_def = m.list_null_def
         self.converted_type = m.converted_type
         self.logical_type = m.logical_type
+        self.scale = m.scale
+        self.precision = m.precision
 
     def getPath(self):
         return list(self.path)

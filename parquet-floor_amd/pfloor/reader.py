@@ -60,20 +60,85 @@ class IllegalArgumentException(Exception):
 
 
 _HEX = "0123456789ABCDEF"
+BINARY_INVALID = "<INVALID>"
+# SchemaElement.converted_type ids / LogicalType union member ids (parquet-format)
+CT_UTF8, CT_ENUM, CT_DECIMAL, CT_JSON, CT_BSON, CT_INTERVAL = 0, 4, 5, 19, 20, 21
+LT_STRING, LT_ENUM, LT_DECIMAL, LT_JSON, LT_BSON, LT_UUID = 1, 4, 5, 12, 13, 14
 
 
 def _default_stringify(b: bytes) -> str:
-    # parquet-mr PrimitiveStringifier.DEFAULT_STRINGIFIER for Binary: "0x" + upper-case hex
+    """PrimitiveStringifier.DEFAULT_STRINGIFIER for a Binary: "0x" + upper-case hex."""
     return "0x" + "".join(_HEX[(x >> 4) & 15] + _HEX[x & 15] for x in b)
 
 
+def _utf8_stringify(b: bytes) -> str:
+    """UTF8_STRINGIFIER: Binary.toStringUsingUTF8 (malformed input -> U+FFFD; the replacement
+    count for malformed sequences follows Python's decoder: parity unpinned)."""
+    return bytes(b).decode("utf-8", errors="replace")
+
+
+def java_big_decimal_str(unscaled: int, scale: int) -> str:
+    """java.math.BigDecimal(BigInteger unscaled, int scale).toString(): plain notation when
+    scale >= 0 and the adjusted exponent >= -6, otherwise scientific ("1E-7", "1.23E+5")."""
+    neg = unscaled < 0
+    coeff = str(-unscaled if neg else unscaled)
+    adjusted = -scale + (len(coeff) - 1)
+    if scale == 0:
+        body = coeff
+    elif scale > 0 and adjusted >= -6:
+        pad = scale - len(coeff)
+        body = "0." + "0" * pad + coeff if pad >= 0 else coeff[:-scale] + "." + coeff[-scale:]
+    else:
+        body = coeff[0] + ("." + coeff[1:] if len(coeff) > 1 else "")
+        if adjusted != 0:
+            body += "E" + ("+" if adjusted > 0 else "") + str(adjusted)
+    return ("-" if neg else "") + body
+
+
+def _decimal_stringifier(scale):
+    """PrimitiveStringifier.createDecimalStringifier(scale) for a Binary: two's-complement
+    big-endian unscaled value (new BigInteger(bytes)); empty -> NumberFormatException ->
+    "<INVALID>"."""
+    def f(b: bytes) -> str:
+        if len(b) == 0:
+            return BINARY_INVALID
+        return java_big_decimal_str(int.from_bytes(bytes(b), "big", signed=True), scale)
+    return f
+
+
+def _interval_stringify(b: bytes) -> str:
+    """INTERVAL_STRINGIFIER: 12 bytes = three little-endian unsigned 32-bit ints."""
+    if len(b) != 12:
+        return BINARY_INVALID
+    m, d, ms = struct.unpack("<III", bytes(b))
+    return f"interval({m} months, {d} days, {ms} millis)"
+
+
+def _uuid_stringify(b: bytes) -> str:
+    """UUID_STRINGIFIER: lower-case 8-4-4-4-12 hex of the 16 bytes."""
+    return str(_uuid.UUID(bytes=bytes(b)))
+
+
 def stringifier(col):
-    """PrimitiveType.stringifier() for BINARY / FIXED_LEN_BYTE_ARRAY / INT96 (upstream parquet-mr
-    1.12.2; restated): UTF8/ENUM/JSON -> UTF-8 text, UUID -> canonical uuid, else DEFAULT (hex)."""
-    if col.is_string:
-        return lambda b: b.decode("utf-8", errors="replace")
-    if col.logical_type == 14 and col.physical_type == 7 and col.type_length == 16:
-        return lambda b: str(_uuid.UUID(bytes=bytes(b)))
+    """PrimitiveType.stringifier() for BINARY / FIXED_LEN_BYTE_ARRAY / INT96, restating upstream
+    parquet-mr 1.12.2 (PrimitiveType.stringifier -> LogicalTypeAnnotation.valueStringifier, the
+    annotation taken from LogicalType, else from the converted type):
+      STRING / ENUM / JSON   -> UTF8_STRINGIFIER
+      DECIMAL(scale)         -> createDecimalStringifier(scale)
+      UUID (FLBA 16)         -> UUID_STRINGIFIER
+      INTERVAL (FLBA 12)     -> INTERVAL_STRINGIFIER
+      BSON / none (incl. INT96, unannotated BINARY / FLBA) -> DEFAULT_STRINGIFIER ("0x" + hex)
+    Pinned by the reference's own test only for UTF8 (ParquetReadWriteTest.java:66-82); the other
+    branches are parity unpinned (no parquet-mr in this image)."""
+    lt, ct = col.logical_type, col.converted_type
+    if lt in (LT_STRING, LT_ENUM, LT_JSON) or (lt == 0 and ct in (CT_UTF8, CT_ENUM, CT_JSON)):
+        return _utf8_stringify
+    if lt == LT_DECIMAL or (lt == 0 and ct == CT_DECIMAL):
+        return _decimal_stringifier(getattr(col, "scale", 0))
+    if lt == LT_UUID:
+        return _uuid_stringify
+    if lt == 0 and ct == CT_INTERVAL:
+        return _interval_stringify
     return _default_stringify
 
 

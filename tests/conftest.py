@@ -33,3 +33,35 @@ def oracle():
 
 def golden_files():
     return sorted(f[:-len(".parquet")] for f in os.listdir(GOLDEN) if f.endswith(".parquet"))
+
+
+# ---- two-process config-3 test (test_gpu_shard.py): its workers start right after collection,
+# before any test (and so this process) touches the GPU, and run alongside the other GPU tests.
+_SHARD = {"procs": [], "out": None}
+SHARD_TEST = "test_two_process_sharded_config3"
+
+
+def pytest_collection_finish(session):
+    if not any(it.name == SHARD_TEST for it in session.items):
+        return
+    import socket
+    import tempfile
+    out = tempfile.mkdtemp(prefix="pf_shard_")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    path = os.path.join(os.environ.get("PF_BENCH_DIR", "/tmp/pfloor_bench"), "lineitem_sf100rg_8000000_seed43.parquet")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    worker = os.path.join(ROOT, "tests", "shard_worker.py")
+    for r in range(2):
+        log = open(os.path.join(out, f"rank{r}.log"), "w")
+        _SHARD["procs"].append(subprocess.Popen(
+            [sys.executable, worker, "--rank", str(r), "--world", "2", "--port", str(port), "--path", path, "--out", out],
+            stdout=log, stderr=subprocess.STDOUT))
+    _SHARD["out"] = out
+
+
+@pytest.fixture(scope="session")
+def shard_run():
+    return _SHARD["procs"], _SHARD["out"]

@@ -81,3 +81,35 @@ def test_shard_helpers():
         reassemble([{0: 1}, {0: 2}], 2)
     with pytest.raises(ValueError):
         reassemble([{0: 1}, {}], 2)
+
+
+def test_bench_work_plan_shards_row_groups():
+    """bench.py's per-rank plan: SF1 x N logical row groups dealt round-robin (weak scaling), SF100's
+    150 logical row groups dealt round-robin (strong), each rank's units dealt to its streams."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import argparse
+    import bench
+
+    class FakePF:
+        def __init__(self, nrg, ncol):
+            self.num_row_groups, self.num_columns = nrg, ncol
+
+    for wl, nphys, expect_total in (("sf1", 6, None), ("sf100", 2, 150)):
+        for world in (1, 2, 4, 8):
+            seen = []
+            for rank in range(world):
+                a = argparse.Namespace(workload=wl)
+                plan, n_log, mine = bench.units_for_rank(a, FakePF(nphys, 16), world, rank, 4)
+                assert n_log == (expect_total or 6 * world)
+                units = [u for ctx in plan for b in ctx for u in b]
+                assert sorted(u[0] for u in units) == mine
+                assert all(u[1] == u[0] % nphys for u in units)
+                seen += mine
+                if wl == "sf1":
+                    assert len(mine) == 6 and len(plan) == 4 and all(len(ctx) == 1 for ctx in plan)
+            assert sorted(seen) == list(range(n_log))
+    a = argparse.Namespace(workload="wide")
+    plan, _, _ = bench.units_for_rank(a, FakePF(1, 500), 1, 0, 4)
+    cols = sorted(c for ctx in plan for b in ctx for u in b for c in u[2])
+    assert cols == list(range(500)) and len(plan) == 4
