@@ -34,6 +34,8 @@ struct SnappyJob {
     uint32_t n_win;       // ceil(src_len / 8192), >= 1
 };
 
+enum : int32_t { DONE_FIXED = 1, DONE_FLAT = 2 };
+
 struct DevPage {
     const uint8_t* body;      // v1: [rep][def][values] uncompressed; v2: values section
     const uint8_t* lvl;       // v2: [rep][def] raw levels (never compressed); v1: null
@@ -46,7 +48,7 @@ struct DevPage {
     int32_t def_enc;
     int32_t rep_enc;
     int32_t num_values;       // level entries
-    int32_t done;             // set by k_flat when it decoded (or failed) the page; k_decode skips it
+    int32_t done;             // DONE_FIXED | DONE_FLAT: k_flat_fixed / k_flat decoded (or failed) the page; k_decode skips it
     int64_t entry_start;      // first level entry of this page within its chunk (host prefix sum)
     // written by k_count, consumed by k_scan
     int64_t n_slots;

@@ -774,7 +774,7 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
-    if (pg.done || res[pg.chunk].status != 0) return;   // k_flat took it / an earlier stage failed this chunk
+    if (pg.done != 0 || res[pg.chunk].status != 0) return;   // k_flat[_fixed] took it / an earlier stage failed this chunk
     Sections s;
     const bool ok = page_sections(pg, ck, s);
     if (tid == 0) {
@@ -1635,7 +1635,7 @@ __global__ __launch_bounds__(NT) void k_flat_fixed(const DevChunk* __restrict__ 
         if (err) set_status(res, pg.chunk, ST_CORRUPT, pi);
         else if (ck.needs_count == 0)
             atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values), (unsigned long long)(e_end - e_begin));
-        pg.done = 1;
+        atomicOr(&pg.done, DONE_FIXED);
     }
 }
 
@@ -1653,7 +1653,9 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
-    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || pg.done) return;   // done: k_flat_fixed took it
+    // DONE_FIXED: k_flat_fixed took the page. Never test DONE_FLAT here: this kernel's own blocks of
+    // the same page set it when they finish, and a block that starts later must still run.
+    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || (pg.done & DONE_FIXED)) return;
     Sections s;
     if (!page_sections(pg, ck, s)) return;                 // k_decode reports it
     const int enc = pg.encoding;
@@ -1727,7 +1729,7 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
         }
     }
     if (lvl_bad) {
-        if (tid == 0) { set_status(res, pg.chunk, ST_CORRUPT, pi); pg.done = 1; }
+        if (tid == 0) { set_status(res, pg.chunk, ST_CORRUPT, pi); atomicOr(&pg.done, DONE_FLAT); }
         return;
     }
     uint64_t char_base = 0;
@@ -1896,7 +1898,7 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
         if (err) set_status(res, pg.chunk, ST_CORRUPT, pi);
         else if (!counted) atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values),
                                      (unsigned long long)(vidx - e_begin));
-        pg.done = 1;
+        atomicOr(&pg.done, DONE_FLAT);
     }
 }
 
