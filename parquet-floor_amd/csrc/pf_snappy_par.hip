@@ -31,6 +31,8 @@
 //                   corrupt is re-decoded serially — results never depend on the assumption.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "pf_snappy_par.h"
 
 namespace pf {
@@ -993,6 +995,246 @@ __global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict_
     for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) dst[a] = ring[a & XRMASK];
 }
 
+// ======================================================================== executor v2
+//
+// Same token supply, chain checks, step cuts and far-copy prefetch as k_snappy_exec, but every
+// output byte of a step is produced by one byte-lane pass: the step's output is walked in
+// sub-steps of 64 bytes, lane x owning byte x0 + x. Its token comes from the step's token-start
+// bitmap (word prefix counts + popcount), the token's packed descriptor from the token's lane
+// (ds_bpermute, no LDS table), and its source is
+//   a literal byte (staged input) or a far-copy byte (prefetched source slot): one LDS read;
+//   a copy byte whose source precedes the sub-step: one ring read (earlier sub-steps of the same
+//     step are already in the ring: single wave, LDS operations execute in order);
+//   a copy byte whose source lies in the same sub-step (dependent copies, self-overlapping runs):
+//     resolved across the 64 lanes by pointer jumping on a packed {value, pending, source lane}
+//     word (ds_bpermute per round; a source lane always precedes its reader, so <= 6 rounds).
+// Self-overlapping copies read source byte (j mod offset), so a run never chains through itself.
+// Dependent copies therefore cost a few register rounds per 64 bytes instead of one serial
+// read-then-write per token.
+constexpr uint32_t X2_STAGE_OFF = XRING;                            // [ring | stage | far slots] in one LDS array,
+constexpr uint32_t X2_FBUF_OFF = XRING + ((XSTAGE + 15u) & ~15u);   // so one byte address selects any source
+constexpr uint32_t X2_LDS = X2_FBUF_OFF + XFAR * FBUF_W * 4;
+enum : uint32_t { X2_LDSADDR = 0, X2_COPY = 1 };
+
+__global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
+                                                     const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
+    __shared__ __attribute__((aligned(16))) uint8_t L[X2_LDS];
+    __shared__ uint16_t tokpos[XCHUNK / 2];
+    __shared__ uint32_t sbits[XBATCH / 32];                               // token starts of the step's output
+    __shared__ uint32_t wpre[XBATCH / 32];                                // tokens starting in earlier words
+    uint8_t* const ring = L;
+    uint8_t* const stage = L + X2_STAGE_OFF;
+    uint32_t* const fbuf = reinterpret_cast<uint32_t*>(L + X2_FBUF_OFF);
+    const int lane = threadIdx.x;
+    int j, k;
+    if (mode == 0) { const int2 pc = pieces[blockIdx.x]; j = pc.x; k = pc.y; }
+    else { j = blockIdx.x; k = 0; }
+    const int f = fb[j];
+    bool whole;
+    if (mode == 0) {
+        if (f >= FB_REDO || (f == FB_WHOLE && k > 0)) return;
+        whole = f == FB_WHOLE;
+    } else {
+        if (f != FB_REDO) return;
+        whole = true;
+    }
+    const SnappyJob job = jobs[j];
+    const uint8_t* in = job.src;
+    uint8_t* dst = job.dst;
+    const uint64_t n = job.src_len;
+    const uint32_t* sp = splits + job.split_base;
+    uint64_t pos0 = 0, ulen = 0;
+    if (!uvarint(in, n, pos0, ulen) || ulen != job.dst_len) {
+        if (lane == 0) atomicMax(&fb[j], FB_SERIAL);
+        return;
+    }
+    uint32_t ip, out_start, out_end = job.dst_len;
+    if (whole) {
+        ip = uint32_t(pos0);
+        out_start = 0;
+    } else {
+        if (k > 0 && sp[k] == SNAP_INVALID) return;   // no token at this boundary: an earlier piece covers it
+        ip = k == 0 ? uint32_t(pos0) : sp[k];
+        out_start = uint32_t(k) * SNAP_BLOCK;
+        for (uint32_t k2 = k + 1; k2 < job.n_pieces; k2++)
+            if (sp[k2] != SNAP_INVALID) { out_end = k2 * SNAP_BLOCK; break; }
+    }
+    const uint16_t* tm16 = reinterpret_cast<const uint16_t*>(job.tokmap);
+    uint32_t op = out_start, F = out_start;
+    uint32_t nst = 0;   // store instructions issued by the last flush (still possibly in flight)
+    bool bad = false;
+    while (op < out_end && !bad) {
+        if (ip >= n) { bad = true; break; }
+        const uint32_t I = ip & ~15u;
+        __syncthreads();
+        const uint32_t woff = snap_stage(stage, in, n, I, XSTAGE, lane);
+        // token starts in [ip, I + XCHUNK): 16 input bytes per lane
+        const uint32_t p16 = I + 16u * uint32_t(lane);
+        uint32_t bits = uint64_t(p16) < n ? uint32_t(tm16[p16 >> 4]) : 0u;
+        if (p16 + 16u <= ip) bits = 0;
+        else if (p16 < ip) bits &= ~((1u << (ip - p16)) - 1u);
+        const uint32_t cnt = __popc(bits);
+        const uint32_t ex = dpp_incl_scan(cnt);
+        const uint32_t T = __builtin_amdgcn_readlane(ex, 63);
+        uint32_t q = ex - cnt;
+        while (bits) {
+            const uint32_t b = uint32_t(__ffs(bits) - 1);
+            bits &= bits - 1;
+            tokpos[q++] = uint16_t(16u * uint32_t(lane) + b);
+        }
+        nst = 0;   // the bitmap loads above waited for every earlier store
+        __syncthreads();
+        if (T == 0) { bad = true; break; }
+        uint32_t sb = 0;
+        while (sb < T && op < out_end) {
+            const uint32_t t = sb + uint32_t(lane);
+            const bool v = t < T;
+            const uint32_t pos = v ? uint32_t(tokpos[t]) : 0u;
+            const SnapTok tk = snap_tok(lds_read8(stage, woff + pos));
+            const uint32_t ol = v ? tk.ol : 0u;
+            const uint32_t start = I + pos;
+            const uint32_t endp = tk.tl > uint64_t(0xffffffffu - start) ? 0xffffffffu : start + uint32_t(tk.tl);
+            const uint32_t prev = dpp_prev(endp);
+            const uint32_t inc = dpp_incl_scan(ol);
+            const uint32_t otok = op + inc - ol;
+            const bool take = v && otok < out_end;
+            const int nt = __popcll(__ballot(take));
+            const bool wrong = take && ((lane == 0 ? start != ip : start != prev) || endp > n || op + inc > out_end ||
+                                        inc < ol);
+            if (__any(wrong)) { bad = true; break; }
+            if (nt == 0) break;   // the previous step ended exactly at out_end
+            const uint32_t kd = tk.kind;
+            const uint32_t off = tk.arg;
+            const uint32_t srcv = start + tk.arg;   // literal data position
+            const bool lstaged = srcv + ol <= I + XCHUNK + 64;
+            const uint32_t a = otok - off;                       // copy source start
+            const bool farc = take && kd != 0 && a + min(ol, off) <= op && int32_t(a - (op + XBATCH - XRING)) < 0;
+            const unsigned long long farm = __ballot(farc);
+            const uint32_t frank = uint32_t(__popcll(farm & lane_mask_lt(uint32_t(lane))));
+            const unsigned long long cutm = __ballot(take && (ol > 64u || inc > XBATCH || (kd == 0 && !lstaged) ||
+                                                              (farc && frank >= XFAR)));
+            const uint32_t cut = cutm ? uint32_t(__ffsll(cutm) - 1) : uint32_t(nt);
+            uint32_t used, btot;
+            if (cut == 0) {
+                // one literal, from HBM (copies are <= 64 bytes, so only a literal gets here)
+                const uint32_t L0 = __builtin_amdgcn_readfirstlane(ol);
+                const uint32_t s0 = __builtin_amdgcn_readfirstlane(srcv);
+                if (__builtin_amdgcn_readfirstlane(kd) != 0) { bad = true; break; }
+                uint32_t fl_slots = 0;
+                for (uint32_t d0 = 0; d0 < L0; d0 += XLIT) {
+                    const uint32_t c = min(L0 - d0, XLIT);
+                    const uint32_t b0 = uint32_t(lane) * 16u;
+                    if (b0 < c) {
+                        uint8_t by[16];
+                        #pragma unroll
+                        for (int u = 0; u < 16; u++) by[u] = b0 + u < c ? in[s0 + d0 + b0 + u] : uint8_t(0);
+                        #pragma unroll
+                        for (int u = 0; u < 16; u++)
+                            if (b0 + u < c) ring[(op + d0 + b0 + u) & XRMASK] = by[u];
+                    }
+                    fl_slots += flush_slots(ring, dst, F, op + d0 + c, lane);
+                }
+                nst = fl_slots;
+                used = 1;
+                btot = L0;
+            } else {
+                used = cut;
+                btot = __builtin_amdgcn_readlane(inc, cut - 1);
+                const bool inb = take && uint32_t(lane) < cut;
+                const bool lit = inb && kd == 0;
+                const bool cp = inb && kd != 0;
+                if (__any(cp && (off == 0 || off > otok - out_start))) { bad = true; break; }
+                const bool far = cp && farc;
+                // far copies: their source (flushed output) into this token's LDS slot
+                if (__any(far)) {
+                    if (nst == XST) wait_vmem_last_slot();   // all but the last slot's stores have landed
+                    else wait_vmem();
+                    if (far) {
+                        const uint32_t* fsrc = reinterpret_cast<const uint32_t*>(dst + (a & ~3u));
+                        const uint32_t nwd = ((a & 3u) + ol + 3u) >> 2;
+                        uint32_t fw[FBUF_W];
+                        #pragma unroll
+                        for (int u = 0; u < int(FBUF_W); u++) fw[u] = uint32_t(u) < nwd ? fsrc[u] : 0u;
+                        uint32_t* fl = fbuf + frank * FBUF_W;
+                        #pragma unroll
+                        for (int u = 0; u < int(FBUF_W); u++)
+                            if (uint32_t(u) < nwd) fl[u] = fw[u];
+                    }
+                }
+                // packed token descriptor, read by the byte lanes with ds_bpermute:
+                //   d0 = rel (11 bits) | kind (1 bit, 11) | self-overlap (bit 12) | offset << 16
+                //   d1 = LDS byte address of the token's first source byte (literal / far copy) or the
+                //        absolute output position of its source (near copy)
+                const uint32_t rel = otok - op;
+                uint32_t d0 = 0, d1 = 0;
+                if (inb) {
+                    const bool near = cp && !far;
+                    d0 = rel | ((near ? X2_COPY : X2_LDSADDR) << 11) | ((near && off < ol) ? (1u << 12) : 0u) |
+                         (min(off, 0xffffu) << 16);
+                    d1 = lit ? X2_STAGE_OFF + woff + (srcv - I)
+                             : (far ? X2_FBUF_OFF + frank * (FBUF_W * 4) + (a & 3u) : a);
+                }
+                if (lane < int(XBATCH / 32)) sbits[lane] = 0;
+                __syncthreads();
+                if (inb) atomicOr(&sbits[rel >> 5], 1u << (rel & 31u));
+                __syncthreads();
+                {
+                    const uint32_t c = lane < int(XBATCH / 32) ? __popc(sbits[lane]) : 0u;
+                    const uint32_t e2 = dpp_incl_scan(c) - c;
+                    if (lane < int(XBATCH / 32)) wpre[lane] = e2;
+                }
+                __syncthreads();
+                for (uint32_t x0 = 0; x0 < btot; x0 += 64) {
+                    const uint32_t x = x0 + uint32_t(lane);
+                    const bool act = x < btot;
+                    const uint32_t xw = act ? x : btot - 1u;
+                    const uint32_t wd = xw >> 5;
+                    const uint32_t ti = wpre[wd] + __popc(sbits[wd] & ((2u << (xw & 31u)) - 1u)) - 1u;
+                    const uint32_t i0 = uint32_t(__builtin_amdgcn_ds_bpermute(int(ti << 2), int(d0)));
+                    const uint32_t i1 = uint32_t(__builtin_amdgcn_ds_bpermute(int(ti << 2), int(d1)));
+                    const uint32_t jj = xw - (i0 & 0x7ffu);
+                    uint32_t addr, pl = 0;
+                    bool pend = false;
+                    if (((i0 >> 11) & 1u) == X2_COPY) {
+                        const uint32_t r = (i0 & (1u << 12)) ? mod_small(jj, i0 >> 16) : jj;
+                        const uint32_t y = i1 + r;                    // absolute output position of the source byte
+                        const uint32_t s0 = op + x0;
+                        pend = y >= s0;                               // produced in this sub-step
+                        pl = y - s0;
+                        addr = y & XRMASK;
+                    } else {
+                        addr = i1 + jj;
+                    }
+                    pend = pend && act;
+                    uint32_t val = (act && !pend) ? uint32_t(L[addr]) : 0u;
+                    while (__any(pend)) {
+                        const uint32_t w = val | (pend ? 0x100u : 0u) | (pl << 9);
+                        const uint32_t got = uint32_t(__builtin_amdgcn_ds_bpermute(int(pl << 2), int(w)));
+                        if (pend) {
+                            if (got & 0x100u) pl = (got >> 9) & 63u;
+                            else { val = got & 0xffu; pend = false; }
+                        }
+                    }
+                    if (act) ring[(op + x) & XRMASK] = uint8_t(val);
+                }
+                const uint32_t sl = flush_slots(ring, dst, F, op + btot, lane);
+                if (sl) nst = sl;
+            }
+            op += btot;
+            ip = __builtin_amdgcn_readlane(endp, int(used) - 1);
+            sb += used;
+        }
+    }
+    if (bad) {
+        if (lane == 0) atomicMax(&fb[j], whole ? FB_SERIAL : FB_REDO);
+        return;
+    }
+    // tail: bytes [F, op)
+    for (uint32_t a = F + uint32_t(lane) * 16u; a + 16u <= op; a += 1024u)
+        *reinterpret_cast<uint4*>(dst + a) = *reinterpret_cast<const uint4*>(ring + (a & XRMASK));
+    for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) dst[a] = ring[a & XRMASK];
+}
+
 #ifdef PF_STAMPS
 extern "C" int pf_debug_stamps(unsigned long long* out, int n, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_stamps), sizeof(unsigned long long) * (n < 16 ? n : 16)) != hipSuccess) return -1;
@@ -1021,8 +1263,11 @@ void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins
 void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
                         int* d_fb, DevChunkResult* d_res, hipStream_t s) {
     if (n_jobs <= 0) return;
-    hipLaunchKernelGGL(k_snappy_exec, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
-    hipLaunchKernelGGL(k_snappy_exec, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
+    // PF_EXEC=1: the token-serial executor (A/B); default: byte-lane executor v2
+    static const bool v1 = [] { const char* e = std::getenv("PF_EXEC"); return e && e[0] == '1'; }();
+    const auto kx = v1 ? k_snappy_exec : k_snappy_exec2;
+    hipLaunchKernelGGL(kx, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
+    hipLaunchKernelGGL(kx, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
     launch_snappy_serial(d_jobs, n_jobs, d_fb, d_res, s);
 }
 
