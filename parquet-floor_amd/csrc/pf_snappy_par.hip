@@ -88,7 +88,8 @@ __device__ __forceinline__ bool bit_get(const WinLane& L, uint32_t i) {
     return (v >> (i & 31u)) & 1u;
 }
 
-constexpr int WIN_ROUNDS = 8;        // lane-region fixed-point rounds before the exact whole-wave parse
+constexpr int WIN_ROUNDS = 66;       // lane-region fixed-point rounds: each fixes at least the first wrong lane,
+                                     // so 64 + 1 always converge (seq_parse stays as a guard)
 
 // Walk the chain from c while positions stay below re (bits relative to rs).
 __device__ void lane_walk(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t rs, uint32_t re,
@@ -112,7 +113,7 @@ __device__ void lane_walk(const uint8_t* stage, uint32_t woff, uint32_t W0, uint
 // Parse one window whose chain enters at `entry` (W0 <= entry < min(W0 + SNAP_WIN, n)). All 64
 // lanes. Returns the window exit; flags = WIN_BROKEN if the chain runs past the stream end.
 __device__ uint32_t win_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t entry, WinLane& L,
-                              uint32_t& flags) {
+                              uint32_t& flags, int max_rounds = WIN_ROUNDS) {
     const int lane = threadIdx.x & 63;
     const uint32_t rs = W0 + uint32_t(lane) * SNAP_RB;
     const uint32_t re = uint32_t(min(uint64_t(rs) + SNAP_RB, n));
@@ -125,7 +126,7 @@ __device__ uint32_t win_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, 
     uint32_t ent = SNAP_INVALID, X = SNAP_INVALID;
     bool converged = false;
     flags = 0;
-    for (int round = 0; round < WIN_ROUNDS; round++) {
+    for (int round = 0; round < max_rounds; round++) {
         // follow the chain lane to lane (uniform scalar loop)
         ent = SNAP_INVALID;
         flags = 0;
@@ -163,7 +164,7 @@ __device__ uint32_t win_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, 
 
 // Entry table (index pass -> chain pass): for an entry e = W0 + d, d < 64, where the chain from e
 // meets the window's own chain (bitmap) and the output difference up to that point.
-constexpr int ENT_STEPS = 384;       // longer walks are left to the chain pass (exact parse)
+constexpr int ENT_STEPS = 384;       // longer walks are left to the chain pass (exact lane-region parse)
 constexpr uint32_t ENT_POS = 0x3fffffffu;
 enum : uint32_t { ENT_MERGE = 0, ENT_NOMERGE = 1, ENT_SLOW = 2, ENT_BAD = 3 };
 
@@ -469,18 +470,29 @@ __global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict
             e = pos;
             continue;
         }
-        // unresolved: exact parse of the window from its true entry (whole wave)
+        // unresolved: exact parse of the window from its true entry (lane regions + fixed point)
         __syncthreads();
         const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
-        reinterpret_cast<uint4*>(sbits)[lane] = make_uint4(0, 0, 0, 0);
-        slo[lane] = 0;
         __syncthreads();
+        WinLane WL{};
+        uint32_t wfl;
+        uint32_t X = win_parse(stage, woff, W0, n, e, WL, wfl);
         uint32_t sum;
-        const uint32_t X = seq_parse(stage, woff, W0, n, e, wend, sbits, slo, sum);
+        if (wfl & WIN_NOCONV) {   // guard (cannot happen within WIN_ROUNDS): exact whole-wave parse
+            reinterpret_cast<uint4*>(sbits)[lane] = make_uint4(0, 0, 0, 0);
+            slo[lane] = 0;
+            __syncthreads();
+            X = seq_parse(stage, woff, W0, n, e, wend, sbits, slo, sum);
+            __syncthreads();
+            const uint4 v4 = reinterpret_cast<const uint4*>(sbits)[lane];
+            WL.b0 = v4.x; WL.b1 = v4.y; WL.b2 = v4.z; WL.b3 = v4.w;
+            WL.out = slo[lane];
+        } else if (wfl & WIN_BROKEN) {
+            X = SNAP_INVALID;
+        }
         if (X == SNAP_INVALID) { bad = true; break; }
-        __syncthreads();
-        reinterpret_cast<uint4*>(job.tokmap + size_t(w) * SNAP_WWORDS)[lane] = reinterpret_cast<const uint4*>(sbits)[lane];
-        LO[size_t(w) * 64 + lane] = slo[lane];
+        sum = wave_sum_sat(WL.out);
+        store_window(job.tokmap + size_t(w) * SNAP_WWORDS, LO + size_t(w) * 64, WL, lane);
         if (lane == 0) Wn[w] = SnapWin{e, X, sum, WM_DONE};
         e = X;
 #ifdef PF_STAMPS
