@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -230,28 +231,42 @@ int plan_snappy(pf_ctx* ctx) {
     ctx->pieces.clear();
     ctx->n_splits = 0;
     uint32_t n_win = 0;
-    for (size_t j = 0; j < ctx->jobs.size(); j++) {
-        SnappyJob& jb = ctx->jobs[j];
+    size_t tw = 0, tp = 0;
+    for (SnappyJob& jb : ctx->jobs) {
         jb.n_win = std::max<uint32_t>(1u, uint32_t((uint64_t(jb.src_len) + SNAP_WIN - 1) / SNAP_WIN));
-        jb.win_base = n_win;
-        for (uint32_t w = 0; w < jb.n_win; w++) ctx->wins.push_back(int2{int(j), int(w)});
-        n_win += jb.n_win;
         jb.n_pieces = std::max<uint32_t>(1u, uint32_t((uint64_t(jb.dst_len) + SNAP_BLOCK - 1) / SNAP_BLOCK));
-        jb.split_base = ctx->n_splits;
-        ctx->n_splits += jb.n_pieces;
-        for (uint32_t k = 0; k < jb.n_pieces; k++) ctx->pieces.push_back(int2{int(j), int(k)});
+        tw += jb.n_win;
+        tp += jb.n_pieces;
     }
+    ctx->wins.resize(tw);
+    ctx->pieces.resize(tp);
     // Dispatch the pieces with the most compressed bytes per 64 KiB of output first (more tokens per
     // piece -> more executor steps), so the longest pieces do not start last (k_snappy_exec alone
     // 1.50 -> 1.39 ms per launch on SF1). PF_PIECE_ORDER=0 keeps page order (A/B).
     static const bool lpt = [] { const char* e = std::getenv("PF_PIECE_ORDER"); return !(e && e[0] == '0'); }();
-    if (lpt) {
-        const auto cost = [&](const int2& p) {
-            const SnappyJob& jb = ctx->jobs[size_t(p.x)];
-            return uint64_t(jb.src_len) / jb.n_pieces;
-        };
-        std::stable_sort(ctx->pieces.begin(), ctx->pieces.end(),
-                         [&](const int2& a, const int2& b) { return cost(a) > cost(b); });
+    std::vector<uint64_t> keyed(lpt ? tp : 0);
+    size_t wi = 0, pi = 0;
+    for (size_t j = 0; j < ctx->jobs.size(); j++) {
+        SnappyJob& jb = ctx->jobs[j];
+        jb.win_base = n_win;
+        for (uint32_t w = 0; w < jb.n_win; w++) ctx->wins[wi++] = int2{int(j), int(w)};
+        n_win += jb.n_win;
+        jb.split_base = ctx->n_splits;
+        ctx->n_splits += jb.n_pieces;
+        const uint64_t cost = uint64_t(jb.src_len) / jb.n_pieces;   // compressed bytes per piece
+        for (uint32_t k = 0; k < jb.n_pieces; k++) {
+            if (lpt) keyed[pi] = (std::min<uint64_t>(cost, 0xffffffffull) << 32) | uint64_t(pi);
+            ctx->pieces[pi++] = int2{int(j), int(k)};
+        }
+    }
+    if (lpt) {   // descending cost, ties in page order
+        std::sort(keyed.begin(), keyed.end(), [](uint64_t a, uint64_t b) {
+            const uint64_t ca = a >> 32, cb = b >> 32;
+            return ca != cb ? ca > cb : uint32_t(a) < uint32_t(b);
+        });
+        std::vector<int2> sorted(tp);
+        for (size_t i = 0; i < tp; i++) sorted[i] = ctx->pieces[size_t(uint32_t(keyed[i]))];
+        ctx->pieces.swap(sorted);
     }
     const size_t tok_bytes = size_t(n_win) * SNAP_WWORDS * 4, lo_bytes = size_t(n_win) * 64 * 4;
     const size_t win_bytes = align_up(size_t(n_win) * sizeof(SnapWin), 256), ent_bytes = size_t(n_win) * 64 * sizeof(SnapEnt);
@@ -422,6 +437,13 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     if (ctx->pending) return fail(ctx, PF_ERR_STATE, "previous decode not waited for");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
+    // diagnostics: PF_DEBUG_PLAN=1 prints the host time of each planning phase (microseconds)
+    static const bool dbg_plan = [] { const char* e = std::getenv("PF_DEBUG_PLAN"); return e && e[0] == '1'; }();
+    using clk = std::chrono::steady_clock;
+    clk::time_point tp[8];
+    int ntp = 0;
+    auto mark = [&]() { if (dbg_plan && ntp < 8) tp[ntp++] = clk::now(); };
+    mark();
     ctx->n_chunks = n_chunks;
     ctx->chunks.assign(n_chunks, DevChunk{});
     ctx->pages.clear(); ctx->jobs.clear();
@@ -558,6 +580,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             if (cd.max_rep > 0) { op.def = take(out, entries); op.rep = take(out, entries); }
         }
     }
+    mark();
     // ---- PLAIN BYTE_ARRAY walk jobs: dictionary pages first, then PLAIN data pages ----
     ctx->bajobs.clear();
     ctx->ba_tiles.clear();
@@ -584,6 +607,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         }
         if (pass == 0) { ctx->n_ba_dict = int(ctx->bajobs.size()); ctx->n_ba_dict_tiles = int(ctx->ba_tiles.size()); }
     }
+    mark();
     // ---- allocate arenas ----
     size_t chars_cap = std::max<size_t>(size_t(2 * chars_hint) + (16u << 20), ctx->chars_need);
     if (ctx->copies_pending && (out > ctx->d_out.cap || bits > ctx->d_bits.cap || chars_cap > ctx->d_chars.cap))
@@ -677,11 +701,13 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         }
         ctx->l_decode.push_back(int(i));
     }
+    mark();
     // ---- Snappy tables: 8 KiB index windows, 64 KiB pieces ----
     {
         int rc = plan_snappy(ctx);
         if (rc) return rc;
     }
+    mark();
     // ---- metadata upload ----
     size_t m = 0;
     ctx->off_chunks = take(m, sizeof(DevChunk) * n_chunks);
@@ -704,8 +730,16 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     HIPCHK(ctx, ctx->h_res.ensure(align_up(sizeof(DevChunkResult) * n_chunks, 256) + sizeof(DevChunk) * n_chunks + 256));
     int rc = upload_meta(ctx);
     if (rc) return rc;
+    mark();
     rc = enqueue_kernels(ctx);
     if (rc) return rc;
+    mark();
+    if (dbg_plan) {
+        auto us = [&](int a, int b) { return long(std::chrono::duration_cast<std::chrono::microseconds>(tp[b] - tp[a]).count()); };
+        std::fprintf(stderr, "[pf plan] chunks %d pages %zu jobs %zu wins %zu | pages %ld ba %ld alloc+lists %ld snappy %ld meta %ld launch %ld us\n",
+                     n_chunks, ctx->pages.size(), ctx->jobs.size(), ctx->wins.size(), us(0, 1), us(1, 2), us(2, 3), us(3, 4),
+                     us(4, 5), us(5, 6));
+    }
     ctx->pending = true;
     ctx->tables_from_decode = true;
     return PF_OK;

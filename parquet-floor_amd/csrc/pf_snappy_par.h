@@ -10,6 +10,13 @@
 
 namespace pf {
 
+// Global-memory view of a pointer loaded from a descriptor: without it the loads/stores are flat_*,
+// which count against lgkmcnt as well and make the compiler drain vmcnt before LDS accesses.
+#define PF_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ PF_GLOBAL T* gptr(T* p) { return (PF_GLOBAL T*)(p); }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // 16-byte access (POD, any address space)
+
 constexpr uint32_t SNAP_RB = 128;                 // input bytes per lane region (index pass)
 constexpr uint32_t SNAP_WIN = 64 * SNAP_RB;       // 8 KiB of input per index window
 constexpr uint32_t SNAP_WSTAGE = SNAP_WIN + 96;   // staged window: + alignment shift (< 16) + 64-lane lookahead
@@ -77,10 +84,11 @@ __device__ __forceinline__ uint64_t lds_read8(const uint8_t* s, uint32_t a) {
 
 // 8 bytes from global memory at in[p], zero past n.
 __device__ __forceinline__ uint64_t glb_read8(const uint8_t* in, uint64_t n, uint64_t p) {
+    const PF_GLOBAL uint8_t* g = gptr(in);
     uint64_t v = 0;
     #pragma unroll
     for (int i = 0; i < 8; i++)
-        if (p + i < n) v |= uint64_t(in[p + i]) << (8 * i);
+        if (p + i < n) v |= uint64_t(g[p + i]) << (8 * i);
     return v;
 }
 
@@ -91,13 +99,13 @@ __device__ __forceinline__ uint32_t snap_stage(uint8_t* stage, const uint8_t* in
                                                uint32_t bytes, int lane) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(in + base);
     const uint32_t woff = uint32_t(a & 15u);
-    const uint4* src = reinterpret_cast<const uint4*>(a - woff);
+    const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(a - woff);
     const int64_t first = int64_t(base) - int64_t(woff);
     for (uint32_t c = uint32_t(lane); c < bytes / 16; c += 64) {
         const int64_t p = first + int64_t(c) * 16;
-        uint4 v = make_uint4(0, 0, 0, 0);
+        u32x4 v = {0u, 0u, 0u, 0u};
         if (p < int64_t(n)) v = src[c];
-        reinterpret_cast<uint4*>(stage)[c] = v;
+        reinterpret_cast<u32x4*>(stage)[c] = v;
     }
     return woff;
 }

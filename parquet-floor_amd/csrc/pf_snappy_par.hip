@@ -690,7 +690,7 @@ __device__ __forceinline__ uint32_t flush_slots(const uint8_t* ring, uint8_t* ds
         const uint32_t a0 = F + uint32_t(lane) * (XSLOT / 64);
         #pragma unroll
         for (uint32_t u = 0; u < XST; u++)
-            *reinterpret_cast<uint4*>(dst + a0 + 16 * u) = *reinterpret_cast<const uint4*>(ring + ((a0 + 16 * u) & XRMASK));
+            *(PF_GLOBAL u32x4*)(dst + a0 + 16 * u) = *reinterpret_cast<const u32x4*>(ring + ((a0 + 16 * u) & XRMASK));
         F += XSLOT;
         nsl += XST;
     }
@@ -1071,10 +1071,17 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
         for (uint32_t k2 = k + 1; k2 < job.n_pieces; k2++)
             if (sp[k2] != SNAP_INVALID) { out_end = k2 * SNAP_BLOCK; break; }
     }
-    const uint16_t* tm16 = reinterpret_cast<const uint16_t*>(job.tokmap);
+    const PF_GLOBAL uint16_t* tm16 = (const PF_GLOBAL uint16_t*)(job.tokmap);
+    const PF_GLOBAL uint8_t* gin = gptr(in);
+    PF_GLOBAL uint8_t* gdst = gptr(dst);
     uint32_t op = out_start, F = out_start;
     uint32_t nst = 0;   // store instructions issued by the last flush (still possibly in flight)
     bool bad = false;
+    XT_DECL;
+#ifdef PF_STAMPS
+    const unsigned long long xt0 = xt_;
+    if (lane == 0) STAMP_ADD(13, 1);
+#endif
     while (op < out_end && !bad) {
         if (ip >= n) { bad = true; break; }
         const uint32_t I = ip & ~15u;
@@ -1096,6 +1103,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
         }
         nst = 0;   // the bitmap loads above waited for every earlier store
         __syncthreads();
+        XT(7);
         if (T == 0) { bad = true; break; }
         uint32_t sb = 0;
         while (sb < T && op < out_end) {
@@ -1127,6 +1135,8 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
                                                               (farc && frank >= XFAR)));
             const uint32_t cut = cutm ? uint32_t(__ffsll(cutm) - 1) : uint32_t(nt);
             uint32_t used, btot;
+            XT(1);
+            if (lane == 0) STAMP_ADD(0, 1);
             if (cut == 0) {
                 // one literal, from HBM (copies are <= 64 bytes, so only a literal gets here)
                 const uint32_t L0 = __builtin_amdgcn_readfirstlane(ol);
@@ -1139,7 +1149,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
                     if (b0 < c) {
                         uint8_t by[16];
                         #pragma unroll
-                        for (int u = 0; u < 16; u++) by[u] = b0 + u < c ? in[s0 + d0 + b0 + u] : uint8_t(0);
+                        for (int u = 0; u < 16; u++) by[u] = b0 + u < c ? gin[s0 + d0 + b0 + u] : uint8_t(0);
                         #pragma unroll
                         for (int u = 0; u < 16; u++)
                             if (b0 + u < c) ring[(op + d0 + b0 + u) & XRMASK] = by[u];
@@ -1149,6 +1159,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
                 nst = fl_slots;
                 used = 1;
                 btot = L0;
+                XT(11);
             } else {
                 used = cut;
                 btot = __builtin_amdgcn_readlane(inc, cut - 1);
@@ -1162,7 +1173,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
                     if (nst == XST) wait_vmem_last_slot();   // all but the last slot's stores have landed
                     else wait_vmem();
                     if (far) {
-                        const uint32_t* fsrc = reinterpret_cast<const uint32_t*>(dst + (a & ~3u));
+                        const PF_GLOBAL uint32_t* fsrc = (const PF_GLOBAL uint32_t*)(gdst + (a & ~3u));
                         const uint32_t nwd = ((a & 3u) + ol + 3u) >> 2;
                         uint32_t fw[FBUF_W];
                         #pragma unroll
@@ -1173,6 +1184,8 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
                             if (uint32_t(u) < nwd) fl[u] = fw[u];
                     }
                 }
+                if (lane == 0 && __any(far)) STAMP_ADD(9, 1);
+                XT(3);
                 // packed token descriptor, read by the byte lanes with ds_bpermute:
                 //   d0 = rel (11 bits) | kind (1 bit, 11) | self-overlap (bit 12) | offset << 16
                 //   d1 = LDS byte address of the token's first source byte (literal / far copy) or the
@@ -1196,41 +1209,73 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
                     if (lane < int(XBATCH / 32)) wpre[lane] = e2;
                 }
                 __syncthreads();
-                for (uint32_t x0 = 0; x0 < btot; x0 += 64) {
-                    const uint32_t x = x0 + uint32_t(lane);
-                    const bool act = x < btot;
-                    const uint32_t xw = act ? x : btot - 1u;
-                    const uint32_t wd = xw >> 5;
-                    const uint32_t ti = wpre[wd] + __popc(sbits[wd] & ((2u << (xw & 31u)) - 1u)) - 1u;
-                    const uint32_t i0 = uint32_t(__builtin_amdgcn_ds_bpermute(int(ti << 2), int(d0)));
-                    const uint32_t i1 = uint32_t(__builtin_amdgcn_ds_bpermute(int(ti << 2), int(d1)));
-                    const uint32_t jj = xw - (i0 & 0x7ffu);
-                    uint32_t addr, pl = 0;
-                    bool pend = false;
-                    if (((i0 >> 11) & 1u) == X2_COPY) {
-                        const uint32_t r = (i0 & (1u << 12)) ? mod_small(jj, i0 >> 16) : jj;
-                        const uint32_t y = i1 + r;                    // absolute output position of the source byte
-                        const uint32_t s0 = op + x0;
-                        pend = y >= s0;                               // produced in this sub-step
-                        pl = y - s0;
-                        addr = y & XRMASK;
-                    } else {
-                        addr = i1 + jj;
+                XT(4);
+                // 256-byte windows: lane L owns bytes w0 + 64u + L (u < 4). A byte's word is its value
+                // (< 0x100) or 0x100 | p: "same as window byte p" (p < its own position).
+                for (uint32_t w0 = 0; w0 < btot; w0 += 256) {
+                    if (lane == 0) STAMP_ADD(8, 1);
+                    const uint32_t s0 = op + w0;
+                    // straight-line phases over the four slots (no branches: the compiler keeps the four
+                    // chains of LDS operations in flight together)
+                    uint32_t W[4], xw[4], ti[4], i0[4], i1[4], addr[4];
+                    bool act[4], pend[4];
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t x = w0 + 64u * uint32_t(u) + uint32_t(lane);
+                        act[u] = x < btot;
+                        xw[u] = act[u] ? x : btot - 1u;
                     }
-                    pend = pend && act;
-                    uint32_t val = (act && !pend) ? uint32_t(L[addr]) : 0u;
-                    while (__any(pend)) {
-                        const uint32_t w = val | (pend ? 0x100u : 0u) | (pl << 9);
-                        const uint32_t got = uint32_t(__builtin_amdgcn_ds_bpermute(int(pl << 2), int(w)));
-                        if (pend) {
-                            if (got & 0x100u) pl = (got >> 9) & 63u;
-                            else { val = got & 0xffu; pend = false; }
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t wd = xw[u] >> 5;
+                        ti[u] = wpre[wd] + __popc(sbits[wd] & ((2u << (xw[u] & 31u)) - 1u)) - 1u;
+                    }
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        i0[u] = uint32_t(__builtin_amdgcn_ds_bpermute(int(ti[u] << 2), int(d0)));
+                        i1[u] = uint32_t(__builtin_amdgcn_ds_bpermute(int(ti[u] << 2), int(d1)));
+                    }
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t jj = xw[u] - (i0[u] & 0x7ffu);
+                        const bool copy = ((i0[u] >> 11) & 1u) == X2_COPY;
+                        const uint32_t offv = max(i0[u] >> 16, 1u);
+                        const uint32_t r = (i0[u] & (1u << 12)) ? mod_small(jj & 63u, offv) : jj;
+                        const uint32_t y = i1[u] + r;                 // copy: absolute output position of the source byte
+                        pend[u] = act[u] && copy && y >= s0;          // produced in this window
+                        addr[u] = copy ? (y & XRMASK) : (i1[u] + jj);
+                        W[u] = 0x100u | ((y - s0) & 0xffu);
+                    }
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t v = uint32_t(L[addr[u]]);
+                        W[u] = pend[u] ? W[u] : (act[u] ? v : 0u);
+                    }
+                    // pointer jumping over the window's 256 bytes (a source always precedes its reader)
+                    while (__any(((W[0] | W[1] | W[2] | W[3]) & 0x100u) != 0u)) {
+                        if (lane == 0) STAMP_ADD(5, 1);
+                        const uint32_t R01 = W[0] | (W[1] << 16), R23 = W[2] | (W[3] << 16);
+                        uint32_t G[4];
+                        #pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            const uint32_t pl = W[u] & 0xffu;
+                            const uint32_t g01 = uint32_t(__builtin_amdgcn_ds_bpermute(int((pl & 63u) << 2), int(R01)));
+                            const uint32_t g23 = uint32_t(__builtin_amdgcn_ds_bpermute(int((pl & 63u) << 2), int(R23)));
+                            const uint32_t sl = pl >> 6;
+                            const uint32_t g = sl < 2 ? g01 : g23;
+                            G[u] = (sl & 1u) ? (g >> 16) : (g & 0xffffu);
                         }
+                        #pragma unroll
+                        for (int u = 0; u < 4; u++) W[u] = (W[u] & 0x100u) ? G[u] : W[u];
                     }
-                    if (act) ring[(op + x) & XRMASK] = uint8_t(val);
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (act[u]) ring[(s0 + 64u * uint32_t(u) + uint32_t(lane)) & XRMASK] = uint8_t(W[u]);
                 }
+                XT(2);
                 const uint32_t sl = flush_slots(ring, dst, F, op + btot, lane);
                 if (sl) nst = sl;
+                XT(6);
             }
             op += btot;
             ip = __builtin_amdgcn_readlane(endp, int(used) - 1);
@@ -1241,10 +1286,13 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
         if (lane == 0) atomicMax(&fb[j], whole ? FB_SERIAL : FB_REDO);
         return;
     }
+#ifdef PF_STAMPS
+    if (lane == 0) STAMP_ADD(12, __builtin_amdgcn_s_memtime() - xt0);
+#endif
     // tail: bytes [F, op)
     for (uint32_t a = F + uint32_t(lane) * 16u; a + 16u <= op; a += 1024u)
-        *reinterpret_cast<uint4*>(dst + a) = *reinterpret_cast<const uint4*>(ring + (a & XRMASK));
-    for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) dst[a] = ring[a & XRMASK];
+        *(PF_GLOBAL u32x4*)(gdst + a) = *reinterpret_cast<const u32x4*>(ring + (a & XRMASK));
+    for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) gdst[a] = ring[a & XRMASK];
 }
 
 #ifdef PF_STAMPS

@@ -10,5 +10,5 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_snappy.py tests/test_gpu_pa
 rc=$?; tail -2 "$OUT/pytest.log"; [ $rc -eq 0 ] || { tail -50 "$OUT/pytest.log"; exit 1; }
 for i in $(seq 1 $N); do
   timeout -k 10 300 python -u bench.py --steps 30 --warmup 3 --no-cpu-baseline --no-pmc --no-e2e "$@" > "$OUT/bench_$i.json" 2>> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
-  python -c "import json; d=json.load(open('$OUT/bench_$i.json')); print(d['ms_per_step'], d['roofline']['kernel'], d['roofline']['launch_ms'], {k: round(v,3) for k,v in d['stage_ms'].items()}, d['parity']['bit_exact'])"
+  python -c "import json; d=json.load(open('$OUT/bench_$i.json')); print(d['ms_per_step'], d.get('host_enqueue_ms_per_batch'), d['roofline']['kernel'], d['roofline']['launch_ms'], {k: round(v,3) for k,v in d['stage_ms'].items()}, d['parity']['bit_exact'])"
 done

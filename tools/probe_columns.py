@@ -11,28 +11,26 @@ from pfloor import _native  # noqa: E402
 from pfloor.decoder import GpuDecoder  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-d = "/tmp/pfloor_bench"
-os.makedirs(d, exist_ok=True)
-path = os.path.join(d, f"lineitem_{bench.SF1_ROWS}_seed{bench.SEED}_rg{bench.RG_ROWS}.parquet")
-if not os.path.exists(path):
-    bench.make_input(path, bench.SF1_ROWS)
-pf, items, host, descs = bench.plan_file(path)
+import argparse  # noqa: E402
+from pfloor.decoder import ParquetFile  # noqa: E402
+args = argparse.Namespace(workload="sf1", data_dir="/tmp/pfloor_bench")
+path = bench.make_input(args)
+pf = ParquetFile(path)
 dec = GpuDecoder(0)
-L = _native.lib()
-d_in = C.c_void_p()
-_native.check(L.pf_device_alloc(dec.h, host.nbytes, C.byref(d_in)), dec.h, "alloc")
-_native.check(L.pf_memcpy_h2d(dec.h, d_in, host.ctypes.data, host.nbytes), dec.h, "h2d")
 tot = {}
 for col in range(pf.num_columns):
-    dd = [descs[i] for i, it in enumerate(items) if it[1] == col]
+    bi = bench.BatchInput(pf, [(g, g, [col]) for g in range(pf.num_row_groups)], dec.h)
+    bi.upload(dec)
+    dd = bi.descs
     st = bench.page_stats(dd)
     acc = {}
     for r in range(reps + 1):
-        dec.decode(dd, d_in.value, host.nbytes, on_device=True)
+        dec.decode(dd, bi.dev.value, bi.nbytes, on_device=True)
         assert dec.wait() == 0, dec.error()
         if r:
             for k, v in dec.timing().items():
                 acc[k] = acc.get(k, 0.0) + v / reps
+    bi.free(dec)
     for k, v in acc.items():
         tot[k] = tot.get(k, 0.0) + v
     s = " ".join(f"{k}={v:.3f}" for k, v in acc.items() if k != "h2d" and v >= 0.005)

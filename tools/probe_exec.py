@@ -22,8 +22,9 @@ st = L.pf_debug_stamps
 st.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
 buf = (C.c_ulonglong * 16)()
 dec = GpuDecoder(0)
-names = ["steps", "decode", "A", "far+cls", "lvl1", "serial", "flush", "stage", "ser_tok", "far_steps",
-         "lvl1_tok", "longlit", "total", "waves"]
+# executor v2 slots (k_snappy_exec2); PF_EXEC=1 selects v1, whose slots differ (see its XT() marks)
+names = ["steps", "decode", "windows_cyc", "far_cyc", "bitmap_cyc", "jump_rounds", "flush", "stage", "windows256",
+         "far_steps", "-", "longlit", "total", "waves"]
 with ParquetFile(path) as pf:
     for col in range(pf.num_columns):
         cname = pf.columns[col].path[0] if hasattr(pf, "columns") else str(col)
