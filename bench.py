@@ -492,7 +492,12 @@ def main():
 
     # HBM traffic of the roofline kernels: rocprofv3 child processes, before this process touches the GPU
     pmc = None
-    if world == 1 and not args.no_pmc:
+    # never start rocprofv3 from a process that is itself being profiled: the profiler's preload has
+    # already initialised the GPU here, and a GPU-initialised process must not exec another program
+    profiled = any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", "")
+    if profiled:
+        pmc = {"error": "skipped: bench.py is running under a profiler"}
+    elif world == 1 and not args.no_pmc:
         try:
             pmc = measure_pmc(args, "k_snappy_exec|k_snappy_index|k_snappy_chain|k_flat")
         except Exception as e:

@@ -24,10 +24,11 @@
 
 namespace pf {
 void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, const int2*, int, uint32_t*,
-                   int*, DevChunkResult*, hipStream_t);
-void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, int*,
+                   uint2*, int*, DevChunkResult*, hipStream_t);
+void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, uint2*, int*,
                          hipStream_t);
-void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*, DevChunkResult*, hipStream_t);
+void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, const uint2*, int*, DevChunkResult*, hipStream_t);
+int snappy_exec_mode();
 void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
@@ -119,6 +120,7 @@ struct pf_ctx {
     size_t bits_bytes = 0;
     size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
     size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0, off_bajobs = 0, off_batiles = 0;
+    size_t off_subsplits = 0;
     uint64_t chars_need = 0;
     const uint8_t* d_bytes = nullptr;
     int reruns = 0;
@@ -175,21 +177,23 @@ int enqueue_kernels(pf_ctx* ctx) {
     uint32_t* d_splits = reinterpret_cast<uint32_t*>(meta + ctx->off_splits);
     int* d_fallback = reinterpret_cast<int*>(meta + ctx->off_fallback);
     const int2* d_wins = reinterpret_cast<const int2*>(meta + ctx->off_wins);
+    uint2* d_subsplits = reinterpret_cast<uint2*>(meta + ctx->off_subsplits);
 
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
     launch_snappy_parse(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent,
-                        ctx->d_lane_out, d_splits, d_fallback, st);
+                        ctx->d_lane_out, d_splits, d_subsplits, d_fallback, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
     if (ctx->exec_stream) {
         HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->exec_stream, ctx->ev_fork, 0));
-        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res,
-                           ctx->exec_stream);
+        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_subsplits,
+                           d_fallback, d_res, ctx->exec_stream);
         HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->exec_stream));
         HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_join, 0));
     } else {
-        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res, st);
+        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_subsplits,
+                           d_fallback, d_res, st);
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], st));
     BaJob* d_bajobs = reinterpret_cast<BaJob*>(meta + ctx->off_bajobs);
@@ -288,6 +292,7 @@ int upload_meta(pf_ctx* ctx) {
     std::memcpy(h + ctx->off_jobs, ctx->jobs.data(), sizeof(SnappyJob) * ctx->jobs.size());
     std::memcpy(h + ctx->off_pieces, ctx->pieces.data(), sizeof(int2) * ctx->pieces.size());
     std::memset(h + ctx->off_splits, 0xff, sizeof(uint32_t) * ctx->n_splits);
+    std::memset(h + ctx->off_subsplits, 0xff, sizeof(uint2) * size_t(ctx->n_splits) * (SNAP_SUBS - 1));
     std::memcpy(h + ctx->off_wins, ctx->wins.data(), sizeof(int2) * ctx->wins.size());
     {   // data-page walks report their chars into the page record
         BaJob* bj = reinterpret_cast<BaJob*>(h + ctx->off_bajobs);
@@ -466,7 +471,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->d_bytes = d_bytes;
 
     // ---- plan: sizes of scratch / outputs ----
-    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; };
+    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; uint64_t cell_off; };
+    const bool sub_exec = snappy_exec_mode() == 3;   // the sub-piece executor keeps 16-bit cells per output byte
     std::vector<PagePlan> pplan;
     size_t scratch = 0, out = 0, bits = 0;
     uint64_t chars_hint = 0;
@@ -514,10 +520,12 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     hs = PF_ERR_CORRUPT_PAGE; break;
                 }
                 bool compressed = cd.codec == PF_CODEC_SNAPPY && (!v2 || pd.is_compressed);
-                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull};
+                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull, ~0ull};
                 if (v2) { pg.lvl = src; pg.rep_len = uint32_t(pd.rep_bytes); pg.def_len = uint32_t(pd.def_bytes); }
                 if (compressed) {
                     pp.scratch_off = take(scratch, pd.uncompressed_size - lvl, 16);
+                    if (sub_exec && pd.uncompressed_size - lvl > SNAP_SUB)
+                        pp.cell_off = take(scratch, 2ull * (pd.uncompressed_size - lvl) + 16, 16);
                     pg.flags |= PG_COMPRESSED;
                     pg.body_len = pd.uncompressed_size - lvl;
                     SnappyJob j{};
@@ -629,7 +637,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             if (pg.flags & PG_COMPRESSED) {
                 pg.body = S + pp.scratch_off;
                 while (ji < ctx->jobs.size() && ctx->jobs[ji].page != int(i)) ji++;
-                if (ji < ctx->jobs.size()) ctx->jobs[ji].dst = S + pp.scratch_off;
+                if (ji < ctx->jobs.size()) {
+                    ctx->jobs[ji].dst = S + pp.scratch_off;
+                    ctx->jobs[ji].cells = pp.cell_off == ~0ull ? nullptr : reinterpret_cast<uint16_t*>(S + pp.cell_off);
+                }
             }
             if (pp.aux_off != ~0ull) {
                 pg.aux = reinterpret_cast<uint32_t*>(S + pp.aux_off);
@@ -719,6 +730,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_res = take(m, sizeof(DevChunkResult) * n_chunks);
     ctx->off_pieces = take(m, sizeof(int2) * ctx->pieces.size());
     ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);
+    ctx->off_subsplits = take(m, sizeof(uint2) * size_t(ctx->n_splits) * (SNAP_SUBS - 1));
     ctx->off_fallback = take(m, sizeof(int) * ctx->jobs.size());
     ctx->off_wins = take(m, sizeof(int2) * ctx->wins.size());
     ctx->off_bajobs = take(m, sizeof(BaJob) * ctx->bajobs.size());
@@ -909,11 +921,13 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     ctx->info.clear();
     ctx->tables_from_decode = false;   // d_meta now holds this call's layout
     HIPCHK(ctx, ctx->d_in.ensure(std::max<size_t>(n, 1)));
-    HIPCHK(ctx, ctx->d_scratch.ensure(std::max<size_t>(ulen, 1) + 16));
+    const size_t cells_at = align_up(std::max<size_t>(ulen, 1) + 16, 256);
+    HIPCHK(ctx, ctx->d_scratch.ensure(cells_at + 2 * std::max<size_t>(ulen, 1) + 16));
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
     SnappyJob job{};
     job.src = static_cast<const uint8_t*>(ctx->d_in.p);
     job.dst = static_cast<uint8_t*>(ctx->d_scratch.p);
+    job.cells = reinterpret_cast<uint16_t*>(static_cast<uint8_t*>(ctx->d_scratch.p) + cells_at);
     job.src_len = uint32_t(n);
     job.dst_len = uint32_t(ulen);
     ctx->jobs.assign(1, job);
@@ -926,6 +940,7 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     size_t o_job = take(m, sizeof(SnappyJob)), o_pc = take(m, sizeof(int2) * ctx->pieces.size());
     size_t o_sp = take(m, 4 * ctx->pieces.size()), o_fb = take(m, 4), o_wn = take(m, sizeof(int2) * ctx->wins.size());
     size_t o_res = take(m, sizeof(DevChunkResult));
+    size_t o_ss = take(m, sizeof(uint2) * ctx->pieces.size() * (SNAP_SUBS - 1));
     m = align_up(m, 256);
     HIPCHK(ctx, ctx->d_meta.ensure(m));
     HIPCHK(ctx, ctx->h_meta.ensure(m));
@@ -934,13 +949,15 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     std::memcpy(h + o_job, ctx->jobs.data(), sizeof(SnappyJob));
     std::memcpy(h + o_pc, ctx->pieces.data(), sizeof(int2) * ctx->pieces.size());
     std::memset(h + o_sp, 0xff, 4 * ctx->pieces.size());
+    std::memset(h + o_ss, 0xff, sizeof(uint2) * ctx->pieces.size() * (SNAP_SUBS - 1));
     std::memcpy(h + o_wn, ctx->wins.data(), sizeof(int2) * ctx->wins.size());
     uint8_t* d = static_cast<uint8_t*>(ctx->d_meta.p);
     HIPCHK(ctx, hipMemcpyAsync(d, h, m, hipMemcpyHostToDevice, st));
     ctx->d_last_splits = reinterpret_cast<const uint32_t*>(d + o_sp);
     launch_snappy(reinterpret_cast<const SnappyJob*>(d + o_job), 1, reinterpret_cast<const int2*>(d + o_wn),
                   int(ctx->wins.size()), ctx->d_win, ctx->d_ent, ctx->d_lane_out, reinterpret_cast<const int2*>(d + o_pc),
-                  int(ctx->pieces.size()), reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb),
+                  int(ctx->pieces.size()), reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<uint2*>(d + o_ss),
+                  reinterpret_cast<int*>(d + o_fb),
                   reinterpret_cast<DevChunkResult*>(d + o_res), st);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, ctx->h_res.ensure(512));

@@ -11,6 +11,6 @@ cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 240 rocprofv3 --pmc $C --kernel-include-regex 'k_snappy_exec|k_flat|k_snappy_index' \
         --output-format csv -d "$OUT/$C" -o run -- \
-        python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --streams 1 > "$OUT/$C.log" 2>&1 || exit 1
+        python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-pmc --no-e2e --no-parity --streams 1 > "$OUT/$C.log" 2>&1 || exit 1
 done
 exit 0
