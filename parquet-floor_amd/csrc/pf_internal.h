@@ -35,7 +35,7 @@ struct SnappyJob {
     uint16_t* cells;      // sub-piece executor: 2 bytes per output byte (value, or 256 + distance back), or null
 };
 
-enum : int32_t { DONE_FIXED = 1, DONE_FLAT = 2 };
+enum : int32_t { DONE_FIXED = 1, DONE_FLAT = 2, DONE_NULL = 4 };
 
 struct DevPage {
     const uint8_t* body;      // v1: [rep][def][values] uncompressed; v2: values section
@@ -67,6 +67,8 @@ struct DevPage {
     int32_t ba_job;           // PLAIN BYTE_ARRAY data page: its BaJob (k_count fills it), else -1
     int32_t counted;          // 1: k_count_flat counted the page (k_count skips it)
     uint32_t* runtab;         // dictionary data page of a flat chunk: id run table (k_runs), else null
+    uint32_t* lvltab;         // nullable fixed-width page of a flat chunk: definition-level run table (k_lvl), else null
+    uint32_t lvl_cap;         // runs the level table can hold
     // DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY page (k_dlen, pf_delta.hip): {cpos[aux_cap + 1],
     // lenA[aux_cap], lenB[aux_cap]} (u64), values in the length streams, first bad value, and
     // where the chars / suffixes start in the values section; else null
@@ -81,6 +83,15 @@ struct DevPage {
 // entries {first | packed << 31, RLE value or bit offset}; a run's count is the next first - first.
 constexpr uint32_t RT_CAP = 1024;
 constexpr uint32_t RT_BYTES = 16 + 8 * RT_CAP;
+
+// k_lvl definition-level run table of a nullable flat page: {nruns, valid, present values, -}, then
+// nruns entries {first entry, RLE value or bit offset, count | packed << 31, present values before}.
+constexpr uint32_t LT_BLOCK_RUNS = 1024;   // most runs one k_flat_null block may overlap (its LDS table)
+__host__ __device__ inline uint32_t lvl_table_cap(int32_t num_values) {
+    // RLE runs are >= 8 repeats and bit-packed groups 8 values for the writers we know (parquet-mr,
+    // Arrow): <= 2 runs per 16 entries; a page needing more is left to k_flat / k_decode
+    return uint32_t(num_values) / 8u + 64u;
+}
 
 // One PLAIN BYTE_ARRAY length walk (a BYTE_ARRAY dictionary page, or the values section of a
 // PLAIN BYTE_ARRAY data page), done tile-parallel by the k_ba_* kernels (pf_pages.hip).

@@ -1207,15 +1207,17 @@ __global__ __launch_bounds__(128) void k_runs(const DevChunk* __restrict__ chunk
     }
     __syncthreads();
     const int nr = s_nr;
-    if (s_res == 2 || !s_allp) {   // too many runs for the table / levels with nulls: blocks walk themselves
-        if (tid == 0) T[3] = 0;
+    if (s_res == 2) {   // too many runs for the table: blocks walk themselves
+        if (tid == 0) { T[2] = 0; T[3] = 0; }
         return;
     }
     for (int i = tid; i < nr; i += 128) {
         T[4 + 2 * i] = R[i].first | (R[i].packed << 31);
         T[5 + 2 * i] = R[i].data;
     }
-    if (tid == 0) { T[0] = uint32_t(nr); T[1] = s_cov; T[2] = 1u; T[3] = 1u; }
+    // T[2]: the id table is valid (indexed by value: pages with nulls hold fewer ids than entries, the
+    // walk then ends with the stream); T[3]: valid and every level present (k_flat_fixed / k_flat split)
+    if (tid == 0) { T[0] = uint32_t(nr); T[1] = s_cov; T[2] = 1u; T[3] = s_allp ? 1u : 0u; }
 }
 
 // k_count for flat BYTE_ARRAY pages whose levels are all present: slots = rows = values =
@@ -1655,7 +1657,7 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
     const int tid = threadIdx.x;
     // DONE_FIXED: k_flat_fixed took the page. Never test DONE_FLAT here: this kernel's own blocks of
     // the same page set it when they finish, and a block that starts later must still run.
-    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || (pg.done & DONE_FIXED)) return;
+    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || (pg.done & (DONE_FIXED | DONE_NULL))) return;
     Sections s;
     if (!page_sections(pg, ck, s)) return;                 // k_decode reports it
     const int enc = pg.encoding;
@@ -1902,6 +1904,310 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
     }
 }
 
+// ---- nullable flat pages: definition-level run table + block-parallel decode ------------------
+//
+// north_star K2/K6: "RLE/bit-packed-hybrid expansion of definition levels ... using prefix scans to
+// find run boundaries" and null scatter. k_lvl walks a page's level run headers once (they are few:
+// ~300 per 20,000 entries at 30 % random nulls), counts the present values of every run in parallel
+// and scans them, so that every 4096-entry block of the page knows the value index of its first
+// present entry. k_flat_null then decodes the blocks in parallel: levels -> present bits -> block
+// scan -> value index -> dictionary gather / PLAIN load; null slots are zero.
+constexpr uint32_t LVL_STAGE = 8192;   // level sections up to this size are walked from LDS
+
+__device__ __forceinline__ uint32_t lvl_present_in(const uint8_t* d, uint64_t dn, uint32_t bitoff, uint32_t cnt, int bw,
+                                                   uint32_t maxd) {
+    // present values (level == maxd) among cnt packed levels from bit offset bitoff
+    uint32_t c = 0;
+    if (bw == 1) {
+        uint32_t i = 0;
+        while (i < cnt) {
+            const uint32_t take = min(24u, cnt - i);
+            const uint32_t v = bits_le(d, dn, uint64_t(bitoff) + i, int(take));
+            c += __popc(v);
+            i += take;
+        }
+        return maxd == 1 ? c : 0u;   // 1-bit levels: max_def is 1
+    }
+    for (uint32_t i = 0; i < cnt; i++) c += bits_le(d, dn, uint64_t(bitoff) + uint64_t(i) * uint32_t(bw), bw) == maxd;
+    return c;
+}
+
+__global__ __launch_bounds__(NT) void k_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
+                                            DevChunkResult* res) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[LVL_STAGE];
+    __shared__ uint32_t scan_tmp[NT / 64];
+    __shared__ uint32_t s_nr, s_ok;
+    const int pi = list[blockIdx.x];
+    DevPage& pg = pages[pi];
+    uint32_t* LT = pg.lvltab;
+    if (!LT) return;
+    const DevChunk& ck = chunks[pg.chunk];
+    const int tid = threadIdx.x;
+    Sections s;
+    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.max_def <= 0 || !page_sections(pg, ck, s) || !s.def_rle) {
+        if (tid == 0) LT[1] = 0;
+        return;
+    }
+    const uint32_t ne = uint32_t(pg.num_values);
+    const int bw = bit_width(uint32_t(ck.max_def));
+    const uint32_t maxd = uint32_t(ck.max_def);
+    const bool staged = s.def_n <= LVL_STAGE;
+    if (staged) {
+        for (uint32_t i = tid; i < uint32_t(s.def_n); i += NT) stage[i] = s.def[i];
+        __syncthreads();
+    }
+    const uint8_t* d = staged ? stage : s.def;
+    const uint64_t dn = s.def_n;
+    uint32_t* runs = LT + 4;
+    const uint32_t cap = pg.lvl_cap;
+    if (tid == 0) {   // the header walk (run headers are a varint chain)
+        uint64_t pos = 0;
+        uint32_t first = 0, nr = 0, ok = 1, blk_runs = 0, cur_blk = 0, max_blk_runs = 0;
+        while (first < ne) {
+            uint64_t h;
+            if (!uvarint(d, dn, pos, h)) { ok = 0; break; }
+            uint32_t data, packed;
+            uint64_t cnt;
+            if (h & 1) {
+                cnt = (h >> 1) * 8;
+                const uint64_t nb = (h >> 1) * uint64_t(bw);
+                data = uint32_t(pos * 8);
+                packed = 1;
+                pos += nb < dn - pos ? nb : dn - pos;   // truncated to what is left (parquet-mr)
+            } else {
+                cnt = h >> 1;
+                const int nbv = (bw + 7) >> 3;
+                if (pos + nbv > dn) { ok = 0; break; }
+                data = 0;
+                for (int b = 0; b < nbv; b++) data |= uint32_t(d[pos + b]) << (8 * b);
+                pos += nbv;
+                packed = 0;
+                if (data > maxd) { ok = 0; break; }
+            }
+            if (cnt == 0) continue;
+            if (nr == cap) { ok = 0; break; }
+            const uint32_t c = uint32_t(min<uint64_t>(cnt, uint64_t(ne - first)));
+            // runs overlapping each FBLK block (k_flat_null's LDS table)
+            const uint32_t b0 = first / FBLK, b1 = (first + c - 1) / FBLK;
+            if (b0 != cur_blk) { cur_blk = b0; blk_runs = 1; } else blk_runs++;
+            max_blk_runs = max(max_blk_runs, blk_runs);
+            if (b1 != b0) { cur_blk = b1; blk_runs = 1; }
+            runs[4 * nr + 0] = first;
+            runs[4 * nr + 1] = data;
+            runs[4 * nr + 2] = c | (packed << 31);
+            nr++;
+            first += c;
+        }
+        if (max_blk_runs > LT_BLOCK_RUNS) ok = 0;
+        s_nr = nr;
+        s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) {
+        if (tid == 0) LT[1] = 0;
+        return;
+    }
+    __threadfence_block();
+    const uint32_t nr = s_nr;
+    uint32_t carry = 0;
+    for (uint32_t r0 = 0; r0 < nr; r0 += NT) {
+        const uint32_t r = r0 + uint32_t(tid);
+        uint32_t pc = 0;
+        if (r < nr) {
+            const uint32_t data = runs[4 * r + 1], cw = runs[4 * r + 2];
+            const uint32_t cnt = cw & 0x7fffffffu;
+            pc = (cw >> 31) ? lvl_present_in(d, dn, data, cnt, bw, maxd) : (data == maxd ? cnt : 0u);
+        }
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<NT>(pc, scan_tmp, tot);
+        if (r < nr) runs[4 * r + 3] = carry + ex;
+        carry += tot;
+    }
+    if (tid == 0) { LT[0] = nr; LT[2] = carry; LT[1] = 1; }
+}
+
+struct NullLds {
+    Run drun[LT_BLOCK_RUNS];
+    uint32_t dvb[LT_BLOCK_RUNS];       // present values before each run
+    Run vrun[RUN_CAP];
+    uint32_t vbits[FT / 32 + 2];
+    uint32_t scan_tmp[NT / 64];
+    uint32_t r0, nrun, vb;
+    int bad;
+};
+
+__global__ __launch_bounds__(NT) void k_flat_null(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                  const int2* __restrict__ blocks, DevChunkResult* res) {
+    __shared__ NullLds S;
+    const int2 pbk = blocks[blockIdx.x];
+    const int pi = pbk.x;
+    const uint32_t blk = uint32_t(pbk.y);
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    const int tid = threadIdx.x;
+    const uint32_t* LT = pg.lvltab;
+    if (!LT || res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.ptype == 6 || ck.ptype == 0 ||
+        (pg.done & DONE_FIXED) || LT[1] != 1u)
+        return;
+    Sections s;
+    if (!page_sections(pg, ck, s)) return;
+    const int enc = pg.encoding;
+    const bool dict = is_dict_enc(enc);
+    if (!dict && enc != 0) return;
+    const uint32_t* T = pg.runtab;
+    if (dict && !(T != nullptr && T[2] == 1u && T[0] <= uint32_t(RUN_CAP) && s.val_n > 0 && ck.dict_data != nullptr))
+        return;
+    const uint32_t ne = uint32_t(pg.num_values);
+    const uint32_t e_begin = blk * FBLK;
+    if (blk > 0 && e_begin >= ne) return;
+    const uint32_t e_end = min(ne, e_begin + FBLK);
+    const int w = ck.width;
+    const int bw = bit_width(uint32_t(ck.max_def));
+    const uint32_t maxd = uint32_t(ck.max_def);
+    const uint32_t nr = LT[0];
+    const uint32_t* runs = LT + 4;
+    const int id_bw = dict ? int(s.val[0]) : 0;
+    const uint8_t* ids = dict ? s.val + 1 : nullptr;
+    const uint64_t ids_n = dict ? s.val_n - 1 : 0;
+    const uint32_t idcov = dict ? T[1] : 0u;
+    if (tid == 0) {
+        uint32_t lo = 0, hi = nr;   // last run with first <= e_begin
+        while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (runs[4 * m] <= e_begin) lo = m; else hi = m;
+        }
+        uint32_t r1 = lo;
+        while (r1 < nr && runs[4 * r1] < e_end) r1++;
+        S.r0 = lo;
+        S.nrun = r1 - lo;
+        S.bad = (r1 - lo > LT_BLOCK_RUNS || id_bw > 32) ? 1 : 0;
+    }
+    __syncthreads();
+    if (S.bad) {
+        if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi);
+        return;
+    }
+    const uint32_t rbase = S.r0, nrun = S.nrun;
+    for (uint32_t i = tid; i < nrun; i += NT) {
+        const uint32_t* q = runs + 4 * (rbase + i);
+        Run r;
+        r.first = q[0];
+        r.data = q[1];
+        r.count = q[2] & 0x7fffffffu;
+        r.packed = q[2] >> 31;
+        S.drun[i] = r;
+        S.dvb[i] = q[3];
+    }
+    if (dict) {
+        const uint32_t vnr = T[0];
+        for (uint32_t i = tid; i < vnr; i += NT) {
+            const uint32_t f = T[4 + 2 * i];
+            const uint32_t nf = i + 1 < vnr ? (T[4 + 2 * (i + 1)] & 0x7fffffffu) : idcov;
+            Run r;
+            r.first = f & 0x7fffffffu;
+            r.count = nf - r.first;
+            r.data = T[5 + 2 * i];
+            r.packed = f >> 31;
+            S.vrun[i] = r;
+        }
+    }
+    if (tid == 0) S.vb = 0;
+    __syncthreads();
+    // present values of the first run before e_begin
+    {
+        const Run R0 = S.drun[0];
+        uint32_t c = 0;
+        const uint32_t before = e_begin - R0.first;
+        if (!R0.packed) {
+            if (tid == 0) c = R0.data == maxd ? before : 0u;
+        } else {
+            for (uint32_t i = tid * 32u; i < before; i += NT * 32u) {
+                const uint32_t k = min(32u, before - i);
+                if (bw == 1) c += __popc(bits_le(s.def, s.def_n, uint64_t(R0.data) + i, int(k)));
+                else for (uint32_t q = 0; q < k; q++)
+                    c += bits_le(s.def, s.def_n, uint64_t(R0.data) + uint64_t(i + q) * uint32_t(bw), bw) == maxd;
+            }
+        }
+        if (c) atomicAdd(&S.vb, c);
+    }
+    __syncthreads();
+    uint64_t vidx = uint64_t(S.dvb[0]) + S.vb;   // value index of the block's next present entry
+    const uint64_t slot_base = uint64_t(pg.entry_start);
+    const bool dalign = dict && (reinterpret_cast<uintptr_t>(ck.dict_data) & uintptr_t(w - 1)) == 0;
+    int bad = 0;
+    uint64_t present_total = 0;
+    for (uint32_t e0 = e_begin; e0 < e_end; e0 += FT) {
+        const uint32_t want = min(uint32_t(FT), e_end - e0);
+        for (uint32_t i = tid; i < FT / 32 + 2; i += NT) S.vbits[i] = 0;
+        const uint32_t eb = uint32_t(tid) * FEPT;
+        uint32_t fv = 0;
+        if (eb < want) {
+            const uint32_t m = min(uint32_t(FEPT), want - eb);
+            const uint32_t e = e0 + eb;
+            int r = run_find(S.drun, int(nrun), e);
+            for (uint32_t k = 0; k < m; k++) {
+                while (r + 1 < int(nrun) && e + k >= S.drun[r].first + S.drun[r].count) r++;
+                const Run& R = S.drun[r];
+                const uint32_t dl = R.packed ? bits_le(s.def, s.def_n, uint64_t(R.data) + uint64_t(e + k - R.first) * uint32_t(bw), bw)
+                                             : R.data;
+                bad |= dl > maxd;
+                fv |= uint32_t(dl == maxd) << k;
+            }
+        }
+        uint32_t tv;
+        const uint32_t vo = block_excl_scan<NT>(__popc(fv), S.scan_tmp, tv);
+        // values of this thread's entries (null slots zero)
+        uint32_t j = 0;
+        int vr = -1;
+        for (uint32_t k = 0; k < FEPT; k++) {
+            if (eb + k >= want) break;
+            uint8_t* dst = ck.values + (slot_base + e0 + eb + k) * uint64_t(w);
+            if (!((fv >> k) & 1u)) { zero_value(dst, w); continue; }
+            const uint64_t gv = vidx + vo + j++;
+            if (dict) {
+                if (gv >= idcov) { bad = 1; continue; }
+                if (vr < 0) vr = run_find(S.vrun, int(T[0]), uint32_t(gv));
+                while (gv >= uint64_t(S.vrun[vr].first) + S.vrun[vr].count) vr++;
+                const Run& R = S.vrun[vr];
+                uint32_t id = R.data;
+                if (R.packed) {
+                    const uint64_t bit = uint64_t(R.data) + (gv - R.first) * uint64_t(id_bw);
+                    id = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
+                                                  : bits_le(ids, ids_n, bit, id_bw);
+                }
+                if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
+                const uint8_t* src = ck.dict_data + uint64_t(id) * uint64_t(w);
+                if (w == 4 && dalign) *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(src);
+                else if (w == 8 && dalign) *reinterpret_cast<uint64_t*>(dst) = *reinterpret_cast<const uint64_t*>(src);
+                else copy_value(dst, src, w);
+            } else {
+                if ((gv + 1) * uint64_t(w) > s.val_n) { bad = 1; continue; }
+                copy_value(dst, s.val + gv * uint64_t(w), w);
+            }
+        }
+        if (ck.validity && fv) {
+            const uint64_t abase = (slot_base + e0) & ~uint64_t(31);
+            const uint64_t rb = slot_base + e0 + eb - abase;
+            const uint32_t sh = uint32_t(rb & 31);
+            atomicOr(&S.vbits[rb >> 5], fv << sh);
+            if (sh + FEPT > 32 && sh) atomicOr(&S.vbits[(rb >> 5) + 1], fv >> (32 - sh));
+        }
+        __syncthreads();
+        if (ck.validity) flush_bits(S.vbits, slot_base + e0, want, ck.validity);
+        vidx += tv;
+        present_total += tv;
+        if (__syncthreads_or(bad)) break;
+    }
+    if (tid == 0) {
+        if (bad) set_status(res, pg.chunk, ST_CORRUPT, pi);
+        else {
+            if (ck.needs_count == 0)
+                atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values), (unsigned long long)present_total);
+            atomicOr(&pg.done, DONE_NULL);
+        }
+    }
+}
+
 // ---- launchers -------------------------------------------------------------------------------
 void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                   BaJob* d_bajobs, hipStream_t st) {
@@ -1929,11 +2235,16 @@ void launch_runs(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
                  hipStream_t st) {
     if (n > 0) hipLaunchKernelGGL(k_runs, dim3(n), dim3(128), 0, st, d_chunks, d_pages, d_list, d_res);
 }
+void launch_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
+                hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(k_lvl, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res);
+}
 void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
-                 hipStream_t st) {   // d_list: n (page, block) pairs
+                 hipStream_t st, bool nullable) {   // d_list: n (page, block) pairs
     if (n <= 0) return;
     const int2* blocks = reinterpret_cast<const int2*>(d_list);
     hipLaunchKernelGGL(k_flat_fixed, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
+    if (nullable) hipLaunchKernelGGL(k_flat_null, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
     hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
 }
 void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,

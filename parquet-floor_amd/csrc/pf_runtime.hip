@@ -35,7 +35,8 @@ void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hi
 void launch_dba_chars(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, BaJob*, hipStream_t);
 void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
-void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool);
+void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 }  // namespace pf
@@ -105,7 +106,7 @@ struct pf_ctx {
     std::vector<DevChunk> chunks;          // host copies (device pointers)
     std::vector<DevPage> pages;
     std::vector<SnappyJob> jobs;
-    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode, l_runs, l_dlen, l_dba;
+    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode, l_runs, l_dlen, l_dba, l_lvl;
     std::vector<int2> wins, pieces;       // Snappy index windows / 64 KiB pieces (job, index)
     std::vector<BaJob> bajobs;             // PLAIN BYTE_ARRAY walks: dictionary pages, then data pages
     std::vector<int2> ba_tiles;            // (job relative to its batch, tile)
@@ -172,6 +173,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     int* d_runs = lists + lo; lo += ctx->l_runs.size();
     int* d_dlen = lists + lo; lo += ctx->l_dlen.size();
     int* d_dba = lists + lo; lo += ctx->l_dba.size();
+    int* d_lvl = lists + lo; lo += ctx->l_lvl.size();
     unsigned long long* used = reinterpret_cast<unsigned long long*>(meta + ctx->meta_bytes - 256);
     const int2* d_pieces = reinterpret_cast<const int2*>(meta + ctx->off_pieces);
     uint32_t* d_splits = reinterpret_cast<uint32_t*>(meta + ctx->off_splits);
@@ -204,6 +206,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], st));
     launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), d_res, st);
     launch_runs(d_chunks, d_pages, d_runs, int(ctx->l_runs.size()), d_res, st);
+    launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st);
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[5], st));
     launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st);
@@ -213,7 +216,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], st));
-    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st);
+    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty());
     HIPCHK(ctx, hipEventRecord(ctx->ev[8], st));
     launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), d_res, st);
     launch_dba_chars(d_chunks, d_pages, d_dba, int(ctx->l_dba.size()), d_res, st);
@@ -305,7 +308,7 @@ int upload_meta(pf_ctx* ctx) {
     int* lists = reinterpret_cast<int*>(h + ctx->off_lists);
     size_t lo = 0;
     for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_flat, &ctx->l_decode, &ctx->l_runs,
-                    &ctx->l_dlen, &ctx->l_dba}) {
+                    &ctx->l_dlen, &ctx->l_dba, &ctx->l_lvl}) {
         std::copy(v->begin(), v->end(), lists + lo);
         lo += v->size();
     }
@@ -453,7 +456,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->chunks.assign(n_chunks, DevChunk{});
     ctx->pages.clear(); ctx->jobs.clear();
     ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_flat.clear(); ctx->l_decode.clear();
-    ctx->l_runs.clear(); ctx->l_dlen.clear(); ctx->l_dba.clear();
+    ctx->l_runs.clear(); ctx->l_dlen.clear(); ctx->l_dba.clear(); ctx->l_lvl.clear();
     ctx->wins.clear(); ctx->pieces.clear(); ctx->n_splits = 0;
     ctx->host_status.assign(n_chunks, 0);
     ctx->info.assign(n_chunks, pf_column_info{});
@@ -471,7 +474,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->d_bytes = d_bytes;
 
     // ---- plan: sizes of scratch / outputs ----
-    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; uint64_t cell_off; };
+    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; uint64_t cell_off;
+                      uint64_t lt_off; };
     const bool sub_exec = snappy_exec_mode() == 3;   // the sub-piece executor keeps 16-bit cells per output byte
     std::vector<PagePlan> pplan;
     size_t scratch = 0, out = 0, bits = 0;
@@ -520,7 +524,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     hs = PF_ERR_CORRUPT_PAGE; break;
                 }
                 bool compressed = cd.codec == PF_CODEC_SNAPPY && (!v2 || pd.is_compressed);
-                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull, ~0ull};
+                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull, ~0ull, ~0ull};
                 if (v2) { pg.lvl = src; pg.rep_len = uint32_t(pd.rep_bytes); pg.def_len = uint32_t(pd.def_bytes); }
                 if (compressed) {
                     pp.scratch_off = take(scratch, pd.uncompressed_size - lvl, 16);
@@ -561,6 +565,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     if (cd.max_rep == 0 && cd.physical_type != PF_BOOLEAN &&
                         (pd.encoding == PF_ENC_PLAIN_DICTIONARY || pd.encoding == PF_ENC_RLE_DICTIONARY))
                         pp.rt_off = take(scratch, RT_BYTES, 256);   // k_runs table
+                    if (cd.max_rep == 0 && cd.max_def > 0 && cd.physical_type != PF_BOOLEAN && cd.physical_type != PF_BYTE_ARRAY &&
+                        (!v2 || pd.num_nulls != 0) &&   // v2 pages say when no level is null (v1: unknown)
+                        (pd.encoding == PF_ENC_PLAIN || pd.encoding == PF_ENC_PLAIN_DICTIONARY || pd.encoding == PF_ENC_RLE_DICTIONARY))
+                        pp.lt_off = take(scratch, 16 + 16ull * lvl_table_cap(pd.num_values), 256);   // k_lvl table
                 }
                 pplan.push_back(pp);
                 ctx->pages.push_back(pg);
@@ -650,6 +658,11 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                 pg.runtab = reinterpret_cast<uint32_t*>(S + pp.rt_off);
                 ctx->l_runs.push_back(int(i));
             }
+            if (pp.lt_off != ~0ull) {
+                pg.lvltab = reinterpret_cast<uint32_t*>(S + pp.lt_off);
+                pg.lvl_cap = lvl_table_cap(pg.num_values);
+                ctx->l_lvl.push_back(int(i));
+            }
             if (pp.dx_off != ~0ull) {
                 pg.dx = reinterpret_cast<uint64_t*>(S + pp.dx_off);
                 ctx->l_dlen.push_back(int(i));
@@ -726,7 +739,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_jobs = take(m, sizeof(SnappyJob) * ctx->jobs.size());
     ctx->off_lists = take(m, sizeof(int) * (ctx->l_dictbin.size() + ctx->l_delta.size() + ctx->l_count.size() +
                                             ctx->l_scan.size() + ctx->l_flat.size() + ctx->l_decode.size() + ctx->l_runs.size() +
-                                            ctx->l_dlen.size() + ctx->l_dba.size()));
+                                            ctx->l_dlen.size() + ctx->l_dba.size() + ctx->l_lvl.size()));
     ctx->off_res = take(m, sizeof(DevChunkResult) * n_chunks);
     ctx->off_pieces = take(m, sizeof(int2) * ctx->pieces.size());
     ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);

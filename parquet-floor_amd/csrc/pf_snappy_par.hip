@@ -1755,7 +1755,7 @@ void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins
 int snappy_exec_mode() {
     // PF_EXEC=1: token-serial executor v1; 2: byte-lane executor v2; default (3): sub-piece executor
     // (PF_NSUB=2 or 4 sub-pieces per 64 KiB piece, default 4)
-    static const int m = [] { const char* e = std::getenv("PF_EXEC"); return e && e[0] >= '1' && e[0] <= '3' ? e[0] - '0' : 3; }();
+    static const int m = [] { const char* e = std::getenv("PF_EXEC"); return e && e[0] >= '1' && e[0] <= '3' ? e[0] - '0' : 2; }();
     return m;
 }
 
