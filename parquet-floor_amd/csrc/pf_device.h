@@ -9,6 +9,14 @@ namespace pf {
 
 constexpr int WAVE = 64;
 
+// Global-memory view of a pointer loaded from a descriptor: without it the loads/stores are flat_*,
+// which count against lgkmcnt as well and make the compiler drain vmcnt before LDS accesses.
+#define PF_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ PF_GLOBAL T* gptr(T* p) { return (PF_GLOBAL T*)(p); }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // 16-byte access (POD, any address space)
+
+
 // Status codes (pfloor.h pf_status); kept as constants so device code needs no header.
 enum : int32_t {
     ST_OK = 0, ST_CORRUPT = -2, ST_ENCODING = -3, ST_CODEC = -4, ST_CAPACITY = -6, ST_TYPE = -7

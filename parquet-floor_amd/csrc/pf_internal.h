@@ -85,8 +85,13 @@ constexpr uint32_t RT_CAP = 1024;
 constexpr uint32_t RT_BYTES = 16 + 8 * RT_CAP;
 
 // k_lvl definition-level run table of a nullable flat page: {nruns, valid, present values, -}, then
-// nruns entries {first entry, RLE value or bit offset, count | packed << 31, present values before}.
-constexpr uint32_t LT_BLOCK_RUNS = 1024;   // most runs one k_flat_null block may overlap (its LDS table)
+// nruns entries {first entry, RLE value or bit offset, count | packed << 31, present values before},
+// then LT_BT_WORDS words per 4096-entry block (k_flat_null): {first run, end run, first value index,
+// end value index, level bytes [d0, d1), dictionary-id bytes [i0, i1)} of the block.
+constexpr uint32_t LT_BLOCK_RUNS = 512;    // most runs one k_flat_null block may overlap (its LDS table)
+constexpr uint32_t LT_BT_WORDS = 8;
+constexpr uint32_t NL_DST = 4096;          // level bytes one k_flat_null block stages in LDS
+constexpr uint32_t NL_IST = 12288;         // dictionary-id bytes one k_flat_null block stages in LDS
 __host__ __device__ inline uint32_t lvl_table_cap(int32_t num_values) {
     // RLE runs are >= 8 repeats and bit-packed groups 8 values for the writers we know (parquet-mr,
     // Arrow): <= 2 runs per 16 entries; a page needing more is left to k_flat / k_decode

@@ -759,7 +759,7 @@ __device__ inline void flush_bits(const uint32_t* bits, uint64_t b0, uint32_t nb
     if (nbits == 0) return;
     uint32_t* out = reinterpret_cast<uint32_t*>(out_bytes);
     uint64_t w0 = b0 >> 5, w1 = (b0 + nbits - 1) >> 5;
-    for (uint64_t w = w0 + threadIdx.x; w <= w1; w += NT) {
+    for (uint64_t w = w0 + threadIdx.x; w <= w1; w += blockDim.x) {
         uint32_t v = bits[w - w0];
         if (w == w0 || w == w1) { if (v) atomicOr(out + w, v); }
         else out[w] = v;
@@ -1573,6 +1573,7 @@ __global__ __launch_bounds__(NT) void k_flat_fixed(const DevChunk* __restrict__ 
                                                    const int2* __restrict__ blocks, DevChunkResult* res) {
     __shared__ FixedLds S;
     const int2 pbk = blocks[blockIdx.x];
+    if (pbk.x < 0) return;   // padding of the XCD-grouped block list (runtime)
     const int pi = pbk.x;
     const uint32_t blk = uint32_t(pbk.y);
     DevPage& pg = pages[pi];
@@ -1650,6 +1651,7 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
                                              const int2* __restrict__ blocks, DevChunkResult* res) {
     __shared__ FlatLds S;
     const int2 pbk = blocks[blockIdx.x];
+    if (pbk.x < 0) return;   // padding of the XCD-grouped block list (runtime)
     const int pi = pbk.x;
     const uint32_t blk = uint32_t(pbk.y);
     DevPage& pg = pages[pi];
@@ -1914,28 +1916,60 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
 // scan -> value index -> dictionary gather / PLAIN load; null slots are zero.
 constexpr uint32_t LVL_STAGE = 8192;   // level sections up to this size are walked from LDS
 
-__device__ __forceinline__ uint32_t lvl_present_in(const uint8_t* d, uint64_t dn, uint32_t bitoff, uint32_t cnt, int bw,
-                                                   uint32_t maxd) {
-    // present values (level == maxd) among cnt packed levels from bit offset bitoff
-    uint32_t c = 0;
-    if (bw == 1) {
-        uint32_t i = 0;
-        while (i < cnt) {
-            const uint32_t take = min(24u, cnt - i);
-            const uint32_t v = bits_le(d, dn, uint64_t(bitoff) + i, int(take));
-            c += __popc(v);
-            i += take;
-        }
-        return maxd == 1 ? c : 0u;   // 1-bit levels: max_def is 1
-    }
-    for (uint32_t i = 0; i < cnt; i++) c += bits_le(d, dn, uint64_t(bitoff) + uint64_t(i) * uint32_t(bw), bw) == maxd;
-    return c;
+// Bits [bit, bit + k) (k <= 32) of an LDS byte array (LSB-first), from the two aligned dwords around it.
+__device__ __forceinline__ uint32_t lds_bits(const uint8_t* st, uint32_t bit, uint32_t k) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(st);
+    const uint32_t wi = bit >> 5, sh = bit & 31u;
+    const uint64_t v = uint64_t(w[wi]) | (uint64_t(w[wi + 1]) << 32);
+    return uint32_t(v >> sh) & (k >= 32 ? 0xffffffffu : ((1u << k) - 1u));
 }
 
-__global__ __launch_bounds__(NT) void k_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
-                                            DevChunkResult* res) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[LVL_STAGE];
-    __shared__ uint32_t scan_tmp[NT / 64];
+// Last level run with first entry <= e (runs: k_lvl table rows of 4 words, runs[0].first == 0).
+__device__ __forceinline__ uint32_t lvl_run_at(const uint32_t* runs, uint32_t nr, uint32_t e) {
+    uint32_t lo = 0, hi = nr;
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (runs[4 * m] <= e) lo = m; else hi = m;
+    }
+    return lo;
+}
+// Present values before entry e, which lies in run r (its present-before count plus the present
+// levels of the run before e, from the staged level section).
+__device__ inline uint32_t lvl_values_before(const uint32_t* runs, uint32_t r, uint32_t e, const uint8_t* stage,
+                                             uint32_t woff, int bw, uint32_t maxd) {
+    const uint32_t first = runs[4 * r], data = runs[4 * r + 1], cw = runs[4 * r + 2];
+    const uint32_t before = e - first;
+    uint32_t vb = runs[4 * r + 3];
+    if (!(cw >> 31)) return vb + (data == maxd ? before : 0u);
+    if (bw == 1) {
+        for (uint32_t i = 0; i < before; i += 32) {
+            const uint32_t k = min(32u, before - i), bb = woff * 8u + data + i;
+            if (bb + k <= LVL_STAGE * 8u) vb += __popc(lds_bits(stage, bb, k));
+        }
+    } else {
+        for (uint32_t i = 0; i < before; i++) {
+            const uint32_t bb = woff * 8u + data + i * uint32_t(bw);
+            if (bb + uint32_t(bw) <= LVL_STAGE * 8u) vb += lds_bits(stage, bb, uint32_t(bw)) == maxd;
+        }
+    }
+    return vb;
+}
+// Dictionary-id run (k_runs table T: {nruns, covered, valid, -}, then {first | packed << 31, data})
+// holding value v.
+__device__ __forceinline__ uint32_t id_run_at(const uint32_t* T, uint32_t nr, uint32_t v) {
+    uint32_t lo = 0, hi = nr;
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if ((T[4 + 2 * m] & 0x7fffffffu) <= v) lo = m; else hi = m;
+    }
+    return lo;
+}
+
+constexpr int LT_NT = 64;   // k_lvl: one wave per page (the header walk is one lane's work)
+__global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
+                                               DevChunkResult* res) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[LVL_STAGE + 48];
+    __shared__ uint32_t scan_tmp[1];
     __shared__ uint32_t s_nr, s_ok;
     const int pi = list[blockIdx.x];
     DevPage& pg = pages[pi];
@@ -1944,42 +1978,60 @@ __global__ __launch_bounds__(NT) void k_lvl(const DevChunk* __restrict__ chunks,
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
     Sections s;
-    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.max_def <= 0 || !page_sections(pg, ck, s) || !s.def_rle) {
+    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.max_def <= 0 || !page_sections(pg, ck, s) || !s.def_rle ||
+        s.def_n > LVL_STAGE) {   // (longer level sections: k_flat / k_decode)
         if (tid == 0) LT[1] = 0;
         return;
     }
     const uint32_t ne = uint32_t(pg.num_values);
     const int bw = bit_width(uint32_t(ck.max_def));
     const uint32_t maxd = uint32_t(ck.max_def);
-    const bool staged = s.def_n <= LVL_STAGE;
-    if (staged) {
-        for (uint32_t i = tid; i < uint32_t(s.def_n); i += NT) stage[i] = s.def[i];
+    const uint32_t dn = uint32_t(s.def_n);
+    // stage the level section with aligned 16-byte loads: section byte i is stage[woff + i]; bytes
+    // past the section read as zero (parquet-mr zero-pads a truncated bit-packed run)
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(s.def);
+    const uint32_t woff = uint32_t(sa & 15u);
+    if (woff + dn > LVL_STAGE) {
+        if (tid == 0) LT[1] = 0;
+        return;
+    }
+    {
+        const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(sa - woff);
+        const uint32_t nchunk = (woff + dn + 15u) / 16u;
+        for (uint32_t c = tid; c < nchunk; c += LT_NT) reinterpret_cast<u32x4*>(stage)[c] = src[c];
+        __syncthreads();
+        for (uint32_t i = woff + dn + uint32_t(tid); i < nchunk * 16u + 16u; i += LT_NT) stage[i] = 0;
         __syncthreads();
     }
-    const uint8_t* d = staged ? stage : s.def;
-    const uint64_t dn = s.def_n;
     uint32_t* runs = LT + 4;
     const uint32_t cap = pg.lvl_cap;
-    if (tid == 0) {   // the header walk (run headers are a varint chain)
-        uint64_t pos = 0;
-        uint32_t first = 0, nr = 0, ok = 1, blk_runs = 0, cur_blk = 0, max_blk_runs = 0;
+    if (tid == 0) {   // the header walk (run headers are a varint chain), from LDS
+        uint32_t pos = 0, first = 0, nr = 0, ok = 1;
         while (first < ne) {
-            uint64_t h;
-            if (!uvarint(d, dn, pos, h)) { ok = 0; break; }
+            uint64_t h = 0;
+            int sh = 0;
+            for (;;) {
+                if (pos >= dn || sh > 63) { ok = 0; break; }
+                const uint32_t c = stage[woff + pos++];
+                h |= uint64_t(c & 0x7fu) << sh;
+                sh += 7;
+                if (!(c & 0x80u)) break;
+            }
+            if (!ok) break;
             uint32_t data, packed;
             uint64_t cnt;
             if (h & 1) {
                 cnt = (h >> 1) * 8;
                 const uint64_t nb = (h >> 1) * uint64_t(bw);
-                data = uint32_t(pos * 8);
+                data = pos * 8u;
                 packed = 1;
-                pos += nb < dn - pos ? nb : dn - pos;   // truncated to what is left (parquet-mr)
+                pos += uint32_t(nb < uint64_t(dn - pos) ? nb : uint64_t(dn - pos));   // truncated (parquet-mr)
             } else {
                 cnt = h >> 1;
-                const int nbv = (bw + 7) >> 3;
+                const uint32_t nbv = uint32_t(bw + 7) >> 3;
                 if (pos + nbv > dn) { ok = 0; break; }
                 data = 0;
-                for (int b = 0; b < nbv; b++) data |= uint32_t(d[pos + b]) << (8 * b);
+                for (uint32_t b = 0; b < nbv; b++) data |= uint32_t(stage[woff + pos + b]) << (8 * b);
                 pos += nbv;
                 packed = 0;
                 if (data > maxd) { ok = 0; break; }
@@ -1987,18 +2039,12 @@ __global__ __launch_bounds__(NT) void k_lvl(const DevChunk* __restrict__ chunks,
             if (cnt == 0) continue;
             if (nr == cap) { ok = 0; break; }
             const uint32_t c = uint32_t(min<uint64_t>(cnt, uint64_t(ne - first)));
-            // runs overlapping each FBLK block (k_flat_null's LDS table)
-            const uint32_t b0 = first / FBLK, b1 = (first + c - 1) / FBLK;
-            if (b0 != cur_blk) { cur_blk = b0; blk_runs = 1; } else blk_runs++;
-            max_blk_runs = max(max_blk_runs, blk_runs);
-            if (b1 != b0) { cur_blk = b1; blk_runs = 1; }
             runs[4 * nr + 0] = first;
             runs[4 * nr + 1] = data;
             runs[4 * nr + 2] = c | (packed << 31);
             nr++;
             first += c;
         }
-        if (max_blk_runs > LT_BLOCK_RUNS) ok = 0;
         s_nr = nr;
         s_ok = ok;
     }
@@ -2010,44 +2056,160 @@ __global__ __launch_bounds__(NT) void k_lvl(const DevChunk* __restrict__ chunks,
     __threadfence_block();
     const uint32_t nr = s_nr;
     uint32_t carry = 0;
-    for (uint32_t r0 = 0; r0 < nr; r0 += NT) {
+    for (uint32_t r0 = 0; r0 < nr; r0 += LT_NT) {
         const uint32_t r = r0 + uint32_t(tid);
         uint32_t pc = 0;
         if (r < nr) {
             const uint32_t data = runs[4 * r + 1], cw = runs[4 * r + 2];
             const uint32_t cnt = cw & 0x7fffffffu;
-            pc = (cw >> 31) ? lvl_present_in(d, dn, data, cnt, bw, maxd) : (data == maxd ? cnt : 0u);
+            if (!(cw >> 31)) pc = data == maxd ? cnt : 0u;
+            else {
+                // packed levels [data, data + cnt * bw) bits (the stage is zero past the section)
+                const uint32_t nbits = cnt * uint32_t(bw);
+                const uint32_t b0 = woff * 8u + data;
+                if (bw == 1) {
+                    for (uint32_t i = 0; i < nbits; i += 32) {
+                        const uint32_t k = min(32u, nbits - i);
+                        if (b0 + i + k <= LVL_STAGE * 8u) pc += __popc(lds_bits(stage, b0 + i, k));
+                    }
+                } else {
+                    for (uint32_t i = 0; i < cnt; i++) {
+                        const uint32_t b = b0 + i * uint32_t(bw);
+                        if (b + uint32_t(bw) <= LVL_STAGE * 8u) pc += lds_bits(stage, b, uint32_t(bw)) == maxd;
+                    }
+                }
+            }
         }
         uint32_t tot;
-        const uint32_t ex = block_excl_scan<NT>(pc, scan_tmp, tot);
+        const uint32_t ex = block_excl_scan<LT_NT>(pc, scan_tmp, tot);
         if (r < nr) runs[4 * r + 3] = carry + ex;
         carry += tot;
     }
-    if (tid == 0) { LT[0] = nr; LT[2] = carry; LT[1] = 1; }
+    // per FBLK block (k_flat_null): the runs it overlaps [r0, r1), the value indices of its first and
+    // end entries, the level bytes its packed runs read and the dictionary-id bytes of its values
+    __threadfence_block();
+    __syncthreads();
+    uint32_t* BT = runs + 4 * cap;
+    const uint32_t nblk = (ne + FBLK - 1) / FBLK;
+    // dictionary id runs (k_runs, same stream): value index -> bit offset in the id stream
+    const uint32_t* T = pg.runtab;
+    const bool dict = is_dict_enc(pg.encoding) && T != nullptr && T[2] == 1u && T[0] <= uint32_t(RUN_CAP) && s.val_n > 0;
+    const uint32_t tnr = dict ? T[0] : 0u, tcov = dict ? T[1] : 0u;
+    const uint32_t id_bw = dict ? uint32_t(s.val[0]) : 0u;
+    uint32_t fit = 1;
+    for (uint32_t b = tid; b < nblk; b += LT_NT) {
+        const uint32_t eb = b * FBLK, ee = min(ne, eb + FBLK);
+        const uint32_t lo = lvl_run_at(runs, nr, eb);
+        uint32_t a = lo, z = nr;    // first run with first >= ee
+        while (a < z) {
+            const uint32_t m = (a + z) >> 1;
+            if (runs[4 * m] < ee) a = m + 1; else z = m;
+        }
+        const uint32_t vb = lvl_values_before(runs, lo, eb, stage, woff, bw, maxd);
+        const uint32_t ve = ee == ne ? carry : lvl_values_before(runs, lvl_run_at(runs, nr, ee), ee, stage, woff, bw, maxd);
+        // level bytes: from the first packed run's first bit to the last packed run's end
+        uint32_t d0 = 0, d1 = 0;
+        for (uint32_t r = lo; r < a; r++) {
+            const uint32_t cw = runs[4 * r + 2];
+            if (!(cw >> 31)) continue;
+            const uint32_t f = runs[4 * r];
+            d0 = (runs[4 * r + 1] + (max(eb, f) - f) * uint32_t(bw)) >> 3;
+            break;
+        }
+        for (uint32_t r = a; r > lo; r--) {
+            const uint32_t cw = runs[4 * (r - 1) + 2];
+            if (!(cw >> 31)) continue;
+            const uint32_t f = runs[4 * (r - 1)], end = min(ee, f + (cw & 0x7fffffffu));
+            d1 = (runs[4 * (r - 1) + 1] + (end - f) * uint32_t(bw) + 7u) >> 3;
+            break;
+        }
+        // dictionary-id bytes of values [vb, ve)
+        uint32_t i0 = 0, i1 = 0;
+        if (dict && ve > vb) {
+            if (ve > tcov) fit = 0;
+            else {
+                const uint32_t q0 = id_run_at(T, tnr, vb), q1 = id_run_at(T, tnr, ve - 1);
+                for (uint32_t q = q0; q <= q1; q++) {
+                    if (!(T[4 + 2 * q] >> 31)) continue;
+                    const uint32_t f = T[4 + 2 * q] & 0x7fffffffu;
+                    i0 = uint32_t((uint64_t(T[5 + 2 * q]) + uint64_t(max(vb, f) - f) * id_bw) >> 3);
+                    break;
+                }
+                for (uint32_t q = q1 + 1; q > q0; q--) {
+                    if (!(T[4 + 2 * (q - 1)] >> 31)) continue;
+                    const uint32_t f = T[4 + 2 * (q - 1)] & 0x7fffffffu;
+                    const uint32_t nf = q < tnr ? (T[4 + 2 * q] & 0x7fffffffu) : tcov;
+                    i1 = uint32_t((uint64_t(T[5 + 2 * (q - 1)]) + uint64_t(min(ve, nf) - f) * id_bw + 7u) >> 3);
+                    break;
+                }
+            }
+        }
+        if (a - lo > LT_BLOCK_RUNS || d1 - d0 + 16u > NL_DST || i1 - i0 + 16u > NL_IST || ve < vb) fit = 0;
+        uint32_t* bt = BT + LT_BT_WORDS * b;
+        bt[0] = lo; bt[1] = a; bt[2] = vb; bt[3] = ve;
+        bt[4] = d0; bt[5] = d1; bt[6] = i0; bt[7] = i1;
+    }
+    fit = __all(fit) ? 1u : 0u;   // one wave
+    if (tid == 0) { LT[0] = nr; LT[2] = carry; LT[1] = fit; }
 }
 
+// k_flat_null: one 512-thread workgroup per 4096-entry block, 8 consecutive entries per thread. The
+// block's level runs, the page's id runs and the level / id bytes the block reads (k_lvl's block
+// table) are all fetched at once into LDS, so the workgroup waits on one round of loads, then on the
+// dictionary gather; no spread step: entry k of a thread takes the value of rank popc(fv & (2^k - 1)).
+constexpr int NTN = 512;
+constexpr int NEPT = FBLK / NTN;   // 8
 struct NullLds {
     Run drun[LT_BLOCK_RUNS];
-    uint32_t dvb[LT_BLOCK_RUNS];       // present values before each run
     Run vrun[RUN_CAP];
-    uint32_t vbits[FT / 32 + 2];
-    uint32_t scan_tmp[NT / 64];
-    uint32_t r0, nrun, vb;
-    int bad;
+    uint32_t dst[NL_DST / 4 + 8];
+    uint32_t ist[NL_IST / 4 + 8];
+    uint32_t vbits[FBLK / 32 + 2];
+    uint32_t scan_tmp[NTN / 64];
 };
 
-__global__ __launch_bounds__(NT) void k_flat_null(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                                  const int2* __restrict__ blocks, DevChunkResult* res) {
-    __shared__ NullLds S;
+// Stage bytes [b0, b1) of stream p[0, n) into LDS words st: byte b0 + i of the stream is byte
+// off + i of st (off = the 16-byte misalignment of p + b0); stream bytes at or past n read as zero
+// (parquet-mr zero-pads a truncated bit-packed run), as do the 16 bytes after the range.
+__device__ __forceinline__ uint32_t stage_bytes(uint32_t* st, const uint8_t* p, uint64_t n, uint32_t b0, uint32_t b1) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p) + b0;
+    const uint32_t off = uint32_t(a & 15u);
+    if (b1 <= b0) return off;
+    const uint32_t nchunk = (off + (b1 - b0) + 15u) / 16u;
+    const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(a - off);
+    const int64_t base = int64_t(b0) - int64_t(off);   // stream offset of st byte 0
+    for (uint32_t c = threadIdx.x; c <= nchunk; c += blockDim.x) {
+        u32x4 v = {0u, 0u, 0u, 0u};
+        const int64_t cb = base + 16 * int64_t(c);   // stream offset of the chunk
+        if (c < nchunk && cb < int64_t(n)) {
+            v = src[c];
+            if (cb + 16 > int64_t(n)) {
+                #pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int64_t keep = int64_t(n) - (cb + 4 * q);   // valid bytes of word q
+                    const uint32_t mask = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
+                    v[q] &= mask;
+                }
+            }
+        }
+        reinterpret_cast<u32x4*>(st)[c] = v;
+    }
+    return off;
+}
+
+__global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                   const int2* __restrict__ blocks, DevChunkResult* res) {
+    __shared__ __attribute__((aligned(16))) NullLds S;
     const int2 pbk = blocks[blockIdx.x];
+    if (pbk.x < 0) return;   // padding of the XCD-grouped block list (runtime)
     const int pi = pbk.x;
     const uint32_t blk = uint32_t(pbk.y);
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
     const uint32_t* LT = pg.lvltab;
-    if (!LT || res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.ptype == 6 || ck.ptype == 0 ||
-        (pg.done & DONE_FIXED) || LT[1] != 1u)
+    if (!LT || res[pg.chunk].status != 0 || ck.max_rep != 0 || (ck.width != 4 && ck.width != 8) ||
+        (pg.done & DONE_FIXED) || LT[1] != 1u)   // (other widths: k_flat / k_decode)
         return;
     Sections s;
     if (!page_sections(pg, ck, s)) return;
@@ -2066,145 +2228,153 @@ __global__ __launch_bounds__(NT) void k_flat_null(const DevChunk* __restrict__ c
     const uint32_t maxd = uint32_t(ck.max_def);
     const uint32_t nr = LT[0];
     const uint32_t* runs = LT + 4;
-    const int id_bw = dict ? int(s.val[0]) : 0;
+    const uint32_t* bt = runs + 4 * pg.lvl_cap + LT_BT_WORDS * blk;
+    const uint32_t r0 = bt[0], r1 = bt[1], vb = bt[2], ve = bt[3], d0 = bt[4], d1 = bt[5], i0 = bt[6], i1 = bt[7];
+    const uint32_t id_bw = dict ? uint32_t(s.val[0]) : 0u;
+    const uint32_t vnr = dict ? T[0] : 0u;
+    const uint32_t idcov = dict ? T[1] : 0u;
     const uint8_t* ids = dict ? s.val + 1 : nullptr;
     const uint64_t ids_n = dict ? s.val_n - 1 : 0;
-    const uint32_t idcov = dict ? T[1] : 0u;
-    if (tid == 0) {
-        uint32_t lo = 0, hi = nr;   // last run with first <= e_begin
-        while (hi - lo > 1) {
-            const uint32_t m = (lo + hi) >> 1;
-            if (runs[4 * m] <= e_begin) lo = m; else hi = m;
-        }
-        uint32_t r1 = lo;
-        while (r1 < nr && runs[4 * r1] < e_end) r1++;
-        S.r0 = lo;
-        S.nrun = r1 - lo;
-        S.bad = (r1 - lo > LT_BLOCK_RUNS || id_bw > 32) ? 1 : 0;
-    }
-    __syncthreads();
-    if (S.bad) {
+    if (r1 < r0 || r1 - r0 > LT_BLOCK_RUNS || r1 > nr || id_bw > 32 || ve < vb || d1 < d0 || d1 - d0 + 16u > NL_DST ||
+        i1 < i0 || i1 - i0 + 16u > NL_IST || (dict && ve > idcov) || (!dict && uint64_t(ve) * uint64_t(w) > s.val_n)) {
         if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi);
         return;
     }
-    const uint32_t rbase = S.r0, nrun = S.nrun;
-    for (uint32_t i = tid; i < nrun; i += NT) {
-        const uint32_t* q = runs + 4 * (rbase + i);
+    // one round of loads: level runs, id runs, level bytes, id bytes
+    const uint32_t nrun = r1 - r0;
+    for (uint32_t i = tid; i < nrun; i += NTN) {
+        const uint32_t* q = runs + 4 * (r0 + i);
         Run r;
         r.first = q[0];
         r.data = q[1];
         r.count = q[2] & 0x7fffffffu;
         r.packed = q[2] >> 31;
         S.drun[i] = r;
-        S.dvb[i] = q[3];
     }
-    if (dict) {
-        const uint32_t vnr = T[0];
-        for (uint32_t i = tid; i < vnr; i += NT) {
-            const uint32_t f = T[4 + 2 * i];
-            const uint32_t nf = i + 1 < vnr ? (T[4 + 2 * (i + 1)] & 0x7fffffffu) : idcov;
-            Run r;
-            r.first = f & 0x7fffffffu;
-            r.count = nf - r.first;
-            r.data = T[5 + 2 * i];
-            r.packed = f >> 31;
-            S.vrun[i] = r;
-        }
+    for (uint32_t i = tid; i < vnr; i += NTN) {
+        const uint32_t f = T[4 + 2 * i];
+        const uint32_t nf = i + 1 < vnr ? (T[4 + 2 * (i + 1)] & 0x7fffffffu) : idcov;
+        Run r;
+        r.first = f & 0x7fffffffu;
+        r.count = nf - r.first;
+        r.data = T[5 + 2 * i];
+        r.packed = f >> 31;
+        S.vrun[i] = r;
     }
-    if (tid == 0) S.vb = 0;
+    const uint32_t doff = stage_bytes(S.dst, s.def, s.def_n, d0, d1);
+    const uint32_t ioff = dict ? stage_bytes(S.ist, ids, ids_n, i0, i1) : 0u;
+    for (uint32_t i = tid; i < FBLK / 32 + 2; i += NTN) S.vbits[i] = 0;
     __syncthreads();
-    // present values of the first run before e_begin
-    {
-        const Run R0 = S.drun[0];
-        uint32_t c = 0;
-        const uint32_t before = e_begin - R0.first;
-        if (!R0.packed) {
-            if (tid == 0) c = R0.data == maxd ? before : 0u;
-        } else {
-            for (uint32_t i = tid * 32u; i < before; i += NT * 32u) {
-                const uint32_t k = min(32u, before - i);
-                if (bw == 1) c += __popc(bits_le(s.def, s.def_n, uint64_t(R0.data) + i, int(k)));
-                else for (uint32_t q = 0; q < k; q++)
-                    c += bits_le(s.def, s.def_n, uint64_t(R0.data) + uint64_t(i + q) * uint32_t(bw), bw) == maxd;
-            }
-        }
-        if (c) atomicAdd(&S.vb, c);
-    }
-    __syncthreads();
-    uint64_t vidx = uint64_t(S.dvb[0]) + S.vb;   // value index of the block's next present entry
-    const uint64_t slot_base = uint64_t(pg.entry_start);
-    const bool dalign = dict && (reinterpret_cast<uintptr_t>(ck.dict_data) & uintptr_t(w - 1)) == 0;
+    const uint8_t* dst8 = reinterpret_cast<const uint8_t*>(S.dst);
+    const uint8_t* ist8 = reinterpret_cast<const uint8_t*>(S.ist);
+    const uint32_t dbase = d0 * 8u - doff * 8u;   // stream bit of LDS bit 0
+    const uint32_t ibase = i0 * 8u - ioff * 8u;
+    const uint32_t dlim = (d1 - d0 + doff + 16u) * 8u;   // readable LDS bits
+    const uint32_t ilim = (i1 - i0 + ioff + 16u) * 8u;
     int bad = 0;
-    uint64_t present_total = 0;
-    for (uint32_t e0 = e_begin; e0 < e_end; e0 += FT) {
-        const uint32_t want = min(uint32_t(FT), e_end - e0);
-        for (uint32_t i = tid; i < FT / 32 + 2; i += NT) S.vbits[i] = 0;
-        const uint32_t eb = uint32_t(tid) * FEPT;
-        uint32_t fv = 0;
-        if (eb < want) {
-            const uint32_t m = min(uint32_t(FEPT), want - eb);
-            const uint32_t e = e0 + eb;
-            int r = run_find(S.drun, int(nrun), e);
+    // present bits of this thread's entries
+    const uint32_t e = e_begin + uint32_t(tid) * NEPT;
+    const uint32_t m = e < e_end ? min(uint32_t(NEPT), e_end - e) : 0u;
+    uint32_t fv = 0;
+    if (m) {
+        int r = run_find(S.drun, int(nrun), e);
+        const Run R = S.drun[r];
+        if (e + m <= R.first + R.count && (!R.packed || bw == 1)) {   // one run
+            if (!R.packed) fv = R.data == maxd ? ((1u << m) - 1u) : 0u;
+            else {
+                const uint32_t b = R.data + (e - R.first) - dbase;
+                fv = b + m <= dlim ? lds_bits(dst8, b, m) : 0u;
+                bad |= b + m > dlim;
+            }
+        } else {
             for (uint32_t k = 0; k < m; k++) {
                 while (r + 1 < int(nrun) && e + k >= S.drun[r].first + S.drun[r].count) r++;
-                const Run& R = S.drun[r];
-                const uint32_t dl = R.packed ? bits_le(s.def, s.def_n, uint64_t(R.data) + uint64_t(e + k - R.first) * uint32_t(bw), bw)
-                                             : R.data;
+                const Run& Rk = S.drun[r];
+                uint32_t dl = Rk.data;
+                if (Rk.packed) {
+                    const uint32_t b = Rk.data + (e + k - Rk.first) * uint32_t(bw) - dbase;
+                    bad |= b + uint32_t(bw) > dlim;
+                    dl = b + uint32_t(bw) <= dlim ? lds_bits(dst8, b, uint32_t(bw)) : 0u;
+                }
                 bad |= dl > maxd;
                 fv |= uint32_t(dl == maxd) << k;
             }
         }
-        uint32_t tv;
-        const uint32_t vo = block_excl_scan<NT>(__popc(fv), S.scan_tmp, tv);
-        // values of this thread's entries (null slots zero)
-        uint32_t j = 0;
-        int vr = -1;
-        for (uint32_t k = 0; k < FEPT; k++) {
-            if (eb + k >= want) break;
-            uint8_t* dst = ck.values + (slot_base + e0 + eb + k) * uint64_t(w);
-            if (!((fv >> k) & 1u)) { zero_value(dst, w); continue; }
-            const uint64_t gv = vidx + vo + j++;
-            if (dict) {
-                if (gv >= idcov) { bad = 1; continue; }
-                if (vr < 0) vr = run_find(S.vrun, int(T[0]), uint32_t(gv));
-                while (gv >= uint64_t(S.vrun[vr].first) + S.vrun[vr].count) vr++;
-                const Run& R = S.vrun[vr];
-                uint32_t id = R.data;
-                if (R.packed) {
-                    const uint64_t bit = uint64_t(R.data) + (gv - R.first) * uint64_t(id_bw);
-                    id = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
-                                                  : bits_le(ids, ids_n, bit, id_bw);
+    }
+    uint32_t tv;
+    const uint32_t vo = block_excl_scan<NTN>(__popc(fv), S.scan_tmp, tv);
+    if (tv != ve - vb) bad = 1;   // the block table disagrees with the levels
+    const uint32_t gv0 = vb + vo;   // value index of this thread's first present entry
+    uint64_t v[NEPT];
+    #pragma unroll
+    for (int k = 0; k < NEPT; k++) v[k] = 0;
+    if (fv && !bad) {
+        if (dict) {
+            int vr = run_find(S.vrun, int(vnr), gv0);
+            #pragma unroll
+            for (int k = 0; k < NEPT; k++) {
+                if (!((fv >> k) & 1u)) continue;
+                const uint32_t gv = gv0 + __popc(fv & ((1u << k) - 1u));
+                while (vr + 1 < int(vnr) && gv >= S.vrun[vr].first + S.vrun[vr].count) vr++;
+                const Run& V = S.vrun[vr];
+                uint32_t id = V.data;
+                if (V.packed) {
+                    const uint32_t b = uint32_t(uint64_t(V.data) + uint64_t(gv - V.first) * id_bw - ibase);
+                    bad |= b + id_bw > ilim;
+                    id = b + id_bw <= ilim ? lds_bits(ist8, b, id_bw) : 0u;
                 }
-                if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
-                const uint8_t* src = ck.dict_data + uint64_t(id) * uint64_t(w);
-                if (w == 4 && dalign) *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(src);
-                else if (w == 8 && dalign) *reinterpret_cast<uint64_t*>(dst) = *reinterpret_cast<const uint64_t*>(src);
-                else copy_value(dst, src, w);
-            } else {
-                if ((gv + 1) * uint64_t(w) > s.val_n) { bad = 1; continue; }
-                copy_value(dst, s.val + gv * uint64_t(w), w);
+                bad |= int64_t(id) >= ck.dict_n;
+                const uint8_t* src = ck.dict_data + uint64_t(int64_t(id) < ck.dict_n ? id : 0u) * uint64_t(w);
+                if (w == 4) v[k] = ld_u32_any(src);
+                else v[k] = ld_u64_any(src);
+            }
+        } else {
+            #pragma unroll
+            for (int k = 0; k < NEPT; k++) {
+                if (!((fv >> k) & 1u)) continue;
+                const uint8_t* src = s.val + uint64_t(gv0 + __popc(fv & ((1u << k) - 1u))) * uint64_t(w);
+                if (w == 4) v[k] = ld_u32_any(src);
+                else v[k] = ld_u64_any(src);
             }
         }
-        if (ck.validity && fv) {
-            const uint64_t abase = (slot_base + e0) & ~uint64_t(31);
-            const uint64_t rb = slot_base + e0 + eb - abase;
-            const uint32_t sh = uint32_t(rb & 31);
-            atomicOr(&S.vbits[rb >> 5], fv << sh);
-            if (sh + FEPT > 32 && sh) atomicOr(&S.vbits[(rb >> 5) + 1], fv >> (32 - sh));
-        }
-        __syncthreads();
-        if (ck.validity) flush_bits(S.vbits, slot_base + e0, want, ck.validity);
-        vidx += tv;
-        present_total += tv;
-        if (__syncthreads_or(bad)) break;
     }
-    if (tid == 0) {
-        if (bad) set_status(res, pg.chunk, ST_CORRUPT, pi);
-        else {
-            if (ck.needs_count == 0)
-                atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values), (unsigned long long)present_total);
-            atomicOr(&pg.done, DONE_NULL);
+    const uint64_t slot_base = uint64_t(pg.entry_start);
+    if (m && !bad) {
+        uint8_t* dst0 = ck.values + (slot_base + e) * uint64_t(w);
+        if (m == NEPT && (reinterpret_cast<uintptr_t>(dst0) & 15u) == 0) {
+            u32x4* d4 = reinterpret_cast<u32x4*>(dst0);
+            if (w == 4) {
+                d4[0] = u32x4{uint32_t(v[0]), uint32_t(v[1]), uint32_t(v[2]), uint32_t(v[3])};
+                d4[1] = u32x4{uint32_t(v[4]), uint32_t(v[5]), uint32_t(v[6]), uint32_t(v[7])};
+            } else {
+                #pragma unroll
+                for (int q = 0; q < 4; q++)
+                    d4[q] = u32x4{uint32_t(v[2 * q]), uint32_t(v[2 * q] >> 32), uint32_t(v[2 * q + 1]), uint32_t(v[2 * q + 1] >> 32)};
+            }
+        } else {
+            for (uint32_t k = 0; k < m; k++) {
+                uint32_t* d = reinterpret_cast<uint32_t*>(dst0 + uint64_t(k) * uint64_t(w));   // 4-byte aligned
+                d[0] = uint32_t(v[k]);
+                if (w == 8) d[1] = uint32_t(v[k] >> 32);
+            }
         }
+    }
+    if (ck.validity && fv) {
+        const uint64_t abase = (slot_base + e_begin) & ~uint64_t(31);
+        const uint64_t rb = slot_base + e - abase;
+        const uint32_t sh = uint32_t(rb & 31);
+        atomicOr(&S.vbits[rb >> 5], fv << sh);
+        if (sh + NEPT > 32 && sh) atomicOr(&S.vbits[(rb >> 5) + 1], fv >> (32 - sh));
+    }
+    bad = __syncthreads_or(bad);
+    if (bad) {
+        if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi);
+        return;
+    }
+    if (ck.validity) flush_bits(S.vbits, slot_base + e_begin, e_end - e_begin, ck.validity);
+    if (tid == 0) {
+        if (ck.needs_count == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values), (unsigned long long)tv);
+        atomicOr(&pg.done, DONE_NULL);
     }
 }
 
@@ -2237,14 +2407,14 @@ void launch_runs(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
 }
 void launch_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                 hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_lvl, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res);
+    if (n > 0) hipLaunchKernelGGL(k_lvl, dim3(n), dim3(LT_NT), 0, st, d_chunks, d_pages, d_list, d_res);
 }
 void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                  hipStream_t st, bool nullable) {   // d_list: n (page, block) pairs
     if (n <= 0) return;
     const int2* blocks = reinterpret_cast<const int2*>(d_list);
     hipLaunchKernelGGL(k_flat_fixed, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
-    if (nullable) hipLaunchKernelGGL(k_flat_null, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
+    if (nullable) hipLaunchKernelGGL(k_flat_null, dim3(n), dim3(NTN), 0, st, d_chunks, d_pages, blocks, d_res);
     hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
 }
 void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,

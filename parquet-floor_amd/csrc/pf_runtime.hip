@@ -568,7 +568,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     if (cd.max_rep == 0 && cd.max_def > 0 && cd.physical_type != PF_BOOLEAN && cd.physical_type != PF_BYTE_ARRAY &&
                         (!v2 || pd.num_nulls != 0) &&   // v2 pages say when no level is null (v1: unknown)
                         (pd.encoding == PF_ENC_PLAIN || pd.encoding == PF_ENC_PLAIN_DICTIONARY || pd.encoding == PF_ENC_RLE_DICTIONARY))
-                        pp.lt_off = take(scratch, 16 + 16ull * lvl_table_cap(pd.num_values), 256);   // k_lvl table
+                        pp.lt_off = take(scratch, 16 + 16ull * lvl_table_cap(pd.num_values) +
+                                                      4ull * LT_BT_WORDS * (uint64_t(pd.num_values) / FLAT_BLK + 1), 256);   // k_lvl tables
                 }
                 pplan.push_back(pp);
                 ctx->pages.push_back(pg);
@@ -713,6 +714,15 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             if (ck.needs_count) ctx->l_scan.push_back(c);
         }
     }
+    // (page, block) pairs of the flat kernels. A chunk with a large dictionary keeps all its blocks on
+    // one blockIdx % 8 label (the dispatcher's XCD group, MI355X_MICROARCH.md), so the dictionary is
+    // gathered through one XCD's L2 instead of all eight (config 4: 400 KB dictionaries); such chunks
+    // go to the least loaded label, all other blocks then fill the labels evenly. Labels are
+    // interleaved into the grid; short ones are padded with (-1, 0).
+    constexpr uint32_t STICKY_DICT = 64u << 10;
+    std::vector<int> xq[8];
+    std::vector<int> spread;
+    std::vector<std::vector<int>> sticky(static_cast<size_t>(n_chunks));
     for (size_t i = 0; i < ctx->pages.size(); i++) {
         const DevPage& pg = ctx->pages[i];
         if (pg.flags & PG_DICT) continue;
@@ -721,9 +731,40 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         if (ck.needs_count) ctx->l_count.push_back(int(i));
         if (ck.max_rep == 0) {   // (page, block) pairs
             const int nb = std::max(1, int((int64_t(pg.num_values) + FLAT_BLK - 1) / FLAT_BLK));
-            for (int b = 0; b < nb; b++) { ctx->l_flat.push_back(int(i)); ctx->l_flat.push_back(b); }
+            const bool big_dict = ck.dict_page >= 0 && ctx->pages[size_t(ck.dict_page)].body_len > STICKY_DICT &&
+                                  (pg.encoding == PF_ENC_PLAIN_DICTIONARY || pg.encoding == PF_ENC_RLE_DICTIONARY);
+            std::vector<int>& q = big_dict ? sticky[size_t(pg.chunk)] : spread;
+            for (int b = 0; b < nb; b++) { q.push_back(int(i)); q.push_back(b); }
         }
         ctx->l_decode.push_back(int(i));
+    }
+    {
+        size_t load[8] = {};
+        std::vector<int> order(static_cast<size_t>(n_chunks));
+        for (int c = 0; c < n_chunks; c++) order[size_t(c)] = c;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return sticky[size_t(a)].size() > sticky[size_t(b)].size(); });
+        for (int c : order) {
+            if (sticky[size_t(c)].empty()) continue;
+            const int x = int(std::min_element(load, load + 8) - load);
+            xq[x].insert(xq[x].end(), sticky[size_t(c)].begin(), sticky[size_t(c)].end());
+            load[x] += sticky[size_t(c)].size() / 2;
+        }
+        for (size_t k = 0; k + 1 < spread.size(); k += 2) {
+            const int x = int(std::min_element(load, load + 8) - load);
+            xq[x].push_back(spread[k]);
+            xq[x].push_back(spread[k + 1]);
+            load[x]++;
+        }
+        const size_t longest = *std::max_element(load, load + 8);
+        if (longest) {
+            ctx->l_flat.assign(2 * 8 * longest, 0);
+            for (size_t k = 0; k < longest; k++)
+                for (int x = 0; x < 8; x++) {
+                    const bool have = k < load[x];
+                    ctx->l_flat[2 * (8 * k + x)] = have ? xq[x][2 * k] : -1;
+                    ctx->l_flat[2 * (8 * k + x) + 1] = have ? xq[x][2 * k + 1] : 0;
+                }
+        }
     }
     mark();
     // ---- Snappy tables: 8 KiB index windows, 64 KiB pieces ----

@@ -10,12 +10,6 @@
 
 namespace pf {
 
-// Global-memory view of a pointer loaded from a descriptor: without it the loads/stores are flat_*,
-// which count against lgkmcnt as well and make the compiler drain vmcnt before LDS accesses.
-#define PF_GLOBAL __attribute__((address_space(1)))
-template <class T>
-__device__ __forceinline__ PF_GLOBAL T* gptr(T* p) { return (PF_GLOBAL T*)(p); }
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // 16-byte access (POD, any address space)
 
 constexpr uint32_t SNAP_RB = 128;                 // input bytes per lane region (index pass)
 constexpr uint32_t SNAP_WIN = 64 * SNAP_RB;       // 8 KiB of input per index window
