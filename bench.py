@@ -35,6 +35,7 @@ import ctypes as C
 import glob
 import json
 import os
+import re
 import shutil
 import socket
 import subprocess
@@ -52,6 +53,11 @@ RG_ROWS = 1 << 20
 SEED = 42
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PCIE_GBS = 63.0         # MI355X_MICROARCH.md: PCIe Gen5 x16 per direction
+# kernels of each stage (rocprof names), for the PMC traffic and the label of the roofline object
+STAGE_KERNELS = {"snappy_exec": r"k_snappy_exec", "snappy_parse": r"k_snappy_(index|chain)$",
+                 "flat": r"k_flat(_fixed|_null)?$", "decode": r"k_decode$"}
+STAGE_LABEL = {"snappy_exec": "k_snappy_exec2 (Snappy executor stage)", "snappy_parse": "k_snappy_index + k_snappy_chain",
+               "flat": "flat stage: k_flat_fixed + k_flat_null + k_flat", "decode": "k_decode"}
 ROOF_PASSES = 3         # isolated decodes of context 0's first batch for the roofline kernel time
 E2E_PASSES = 2
 METRIC = "decoded GB/s + rows/s (node), lineitem-shape Snappy+dict, 1/2/4/8 GPUs"
@@ -499,7 +505,7 @@ def main():
         pmc = {"error": "skipped: bench.py is running under a profiler"}
     elif world == 1 and not args.no_pmc:
         try:
-            pmc = measure_pmc(args, "k_snappy_exec|k_snappy_index|k_snappy_chain|k_flat")
+            pmc = measure_pmc(args, "k_snappy_exec|k_snappy_index|k_snappy_chain|k_flat|k_decode")
         except Exception as e:
             pmc = {"error": repr(e)}
 
@@ -603,10 +609,8 @@ def main():
     traffic, traffic_detail = None, None
     if pmc and "error" not in pmc:
         traffic_detail = pmc_traffic_per_kernel(pmc)
-        kmap = {"snappy_exec": ["k_snappy_exec"], "snappy_parse": ["k_snappy_index", "k_snappy_chain"],
-                "flat": ["k_flat", "k_flat_fixed"]}
-        names = kmap.get(dom, [])
-        if names and all(n in traffic_detail for n in names):
+        names = [n for n in traffic_detail if STAGE_KERNELS.get(dom) and re.match(STAGE_KERNELS[dom], n.split("<")[0])]
+        if names:
             traffic = sum(traffic_detail[n]["traffic_bytes"] for n in names)
     b_alg_step = None
     descs_all = [d for bl in batches for bi in bl for d in bi.descs]
@@ -649,7 +653,7 @@ def main():
                                   f"{S} decode streams per GPU"},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "host_enqueue_ms_per_batch": round(host_plan_ms, 4),
-        "roofline": {"bound": "hbm", "kernel": f"k_{dom}", "achieved": round(achieved, 2) if achieved else None,
+        "roofline": {"bound": "hbm", "kernel": STAGE_LABEL.get(dom, dom), "achieved": round(achieved, 2) if achieved else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": traffic,
                      "traffic_source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE per launch, measured in "

@@ -84,7 +84,9 @@ typedef struct pf_page_desc {
     int32_t  def_encoding;        /* v1 only: RLE or BIT_PACKED */
     int32_t  rep_encoding;        /* v1 only */
     int32_t  num_values;          /* level entries (data) / dictionary entries (dict) */
-    int32_t  num_nulls;           /* v2 only */
+    int32_t  num_nulls;           /* v2: header; v1: page statistics null_count, -1 if absent.
+                                     A routing hint (0 skips the null-page tables); results never
+                                     depend on it */
     int32_t  num_rows;            /* v2 only */
     int32_t  def_bytes;           /* v2 only: definition_levels_byte_length */
     int32_t  rep_bytes;           /* v2 only: repetition_levels_byte_length */

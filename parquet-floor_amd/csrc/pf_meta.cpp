@@ -7,6 +7,7 @@
 // exists in this image, so this C++ parser produces the same descriptors for the C++/Python
 // hosts and the tests. It reads Thrift compact protocol (parquet.thrift field ids) and
 // never touches the GPU.
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -246,6 +247,7 @@ void FileMeta::walk_pages(const uint8_t* chunk, size_t size, const ChunkMeta& m,
         ThriftReader r{chunk + off, chunk + size};
         pf_page_desc d{};
         d.is_compressed = 1;
+        d.num_nulls = -1;   // v1 without page statistics: unknown
         d.page_type = -1;
         int last = 0, id, t;
         while (r.field(last, id, t)) {
@@ -260,7 +262,15 @@ void FileMeta::walk_pages(const uint8_t* chunk, size_t size, const ChunkMeta& m,
                         else if (i2 == 2) d.encoding = int32_t(r.integer(t2));
                         else if (i2 == 3) d.def_encoding = int32_t(r.integer(t2));
                         else if (i2 == 4) d.rep_encoding = int32_t(r.integer(t2));
-                        else r.skip(t2);
+                        else if (i2 == 5 && t2 == 12) {   // Statistics: null_count (field 3), a routing hint
+                            int l3 = 0, i3, t3;
+                            while (r.field(l3, i3, t3)) {
+                                if (i3 == 3) {
+                                    const int64_t nn = r.integer(t3);
+                                    d.num_nulls = nn >= 0 && nn <= INT32_MAX ? int32_t(nn) : -1;
+                                } else r.skip(t3);
+                            }
+                        } else r.skip(t2);
                     } else if (id == 7) {   // DictionaryPageHeader
                         if (i2 == 1) d.num_values = int32_t(r.integer(t2));
                         else if (i2 == 2) d.encoding = int32_t(r.integer(t2));

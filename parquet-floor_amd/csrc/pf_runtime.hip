@@ -566,7 +566,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                         (pd.encoding == PF_ENC_PLAIN_DICTIONARY || pd.encoding == PF_ENC_RLE_DICTIONARY))
                         pp.rt_off = take(scratch, RT_BYTES, 256);   // k_runs table
                     if (cd.max_rep == 0 && cd.max_def > 0 && cd.physical_type != PF_BOOLEAN && cd.physical_type != PF_BYTE_ARRAY &&
-                        (!v2 || pd.num_nulls != 0) &&   // v2 pages say when no level is null (v1: unknown)
+                        pd.num_nulls != 0 &&   // v2 header / v1 page statistics say when no level is null (-1: unknown)
                         (pd.encoding == PF_ENC_PLAIN || pd.encoding == PF_ENC_PLAIN_DICTIONARY || pd.encoding == PF_ENC_RLE_DICTIONARY))
                         pp.lt_off = take(scratch, 16 + 16ull * lvl_table_cap(pd.num_values) +
                                                       4ull * LT_BT_WORDS * (uint64_t(pd.num_values) / FLAT_BLK + 1), 256);   // k_lvl tables
