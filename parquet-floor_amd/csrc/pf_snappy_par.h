@@ -70,6 +70,19 @@ __device__ __forceinline__ SnapTok snap_tok(uint64_t v) {
     return t;
 }
 
+// Token lengths from the tag byte alone (literals with a length field, tag_long, need snap_tok).
+__device__ __forceinline__ uint32_t tag_tl(uint32_t tag) {   // input bytes (branch-free)
+    const uint32_t kind = tag & 3u;
+    const uint32_t lit = uint32_t(int32_t(kind - 1u) >> 31);        // all ones for a literal
+    return ((0x05030200u >> (kind << 3)) & 0xffu) | (((tag >> 2) + 2u) & lit);
+}
+__device__ __forceinline__ uint32_t tag_ol(uint32_t tag) {   // output bytes (branch-free)
+    const uint32_t L = tag >> 2;
+    const uint32_t c1 = uint32_t(-int32_t((tag & 3u) == 1u));     // all ones for a 1-byte-offset copy
+    return ((4u + (L & 7u)) & c1) | ((L + 1u) & ~c1);
+}
+__device__ __forceinline__ bool tag_long(uint32_t tag) { return (tag & 3u) == 0u && tag >= 240u; }
+
 // 8 bytes from LDS at byte offset a (two aligned dword reads; a + 8 + 3 must be staged).
 __device__ __forceinline__ uint64_t lds_read8(const uint8_t* s, uint32_t a) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(s + (a & ~3u));

@@ -88,8 +88,60 @@ __device__ __forceinline__ bool bit_get(const WinLane& L, uint32_t i) {
     return (v >> (i & 31u)) & 1u;
 }
 
+// ---- padded window stage: lane region k (input bytes [W0 + 128k, W0 + 128k + 140)) sits at
+// sp + 140k, so 64 lanes reading the same offset of their own regions hit 64 different LDS banks
+// (140 B = 35 dwords, odd) and an 8-byte token read at any region offset < 128 stays in the copy.
+constexpr uint32_t SNAP_PB = 140;
+constexpr uint32_t SNAP_PSTAGE = 64 * SNAP_PB;
+constexpr uint32_t XS_SAT = 0x7fffu;       // saturated region exit (a literal longer than ~32 KiB)
+
+// n >= 1. Dwords holding no stream byte are never read (zero instead).
+__device__ void stage_pad(uint8_t* sp, const uint8_t* in, uint64_t n, uint32_t W0, int lane) {
+    const uintptr_t base = reinterpret_cast<uintptr_t>(in);
+    const uintptr_t lastw = (base + n - 1) & ~uintptr_t(3);
+    for (uint32_t idx = uint32_t(lane); idx < SNAP_PSTAGE / 4; idx += 64) {
+        const uint32_t k = idx / (SNAP_PB / 4), jd = idx - k * (SNAP_PB / 4);
+        const uintptr_t a = base + W0 + k * SNAP_RB + jd * 4;
+        const uintptr_t a0 = a & ~uintptr_t(3);
+        const uint32_t lo = a0 <= lastw ? *(const PF_GLOBAL uint32_t*)a0 : 0u;
+        const uint32_t hi = a0 + 4 <= lastw ? *(const PF_GLOBAL uint32_t*)(a0 + 4) : 0u;
+        reinterpret_cast<uint32_t*>(sp)[idx] = __builtin_amdgcn_alignbyte(hi, lo, uint32_t(a & 3u));
+    }
+}
+
+// 8 stream bytes from window offset r (< 8 KiB) of a padded stage.
+__device__ __forceinline__ uint64_t pad_read8(const uint8_t* sp, uint32_t r) {
+    return lds_read8(sp, (r >> 7) * SNAP_PB + (r & 127u));
+}
+
+// Input / output bytes of the token at window offset r of a padded stage.
+__device__ __forceinline__ uint64_t pad_tok(const uint8_t* sp, uint32_t r, uint32_t& ol) {
+    const uint32_t a = (r >> 7) * SNAP_PB + (r & 127u);
+    const uint32_t tag = (*reinterpret_cast<const uint32_t*>(sp + (a & ~3u)) >> (8u * (a & 3u))) & 0xffu;
+    if (!tag_long(tag)) {
+        ol = tag_ol(tag);
+        return tag_tl(tag);
+    }
+    const SnapTok t = snap_tok(lds_read8(sp, a));
+    ol = t.ol;
+    return t.tl;
+}
+
 constexpr int WIN_ROUNDS = 66;       // lane-region fixed-point rounds: each fixes at least the first wrong lane,
                                      // so 64 + 1 always converge (seq_parse stays as a guard)
+
+// Input / output bytes of the token at stage offset a (linear stage; tag decode unless a literal
+// carries a length field).
+__device__ __forceinline__ uint64_t stage_tok(const uint8_t* stage, uint32_t a, uint32_t& ol) {
+    const uint32_t tag = stage[a];
+    if (!tag_long(tag)) {
+        ol = tag_ol(tag);
+        return tag_tl(tag);
+    }
+    const SnapTok t = snap_tok(lds_read8(stage, a));
+    ol = t.ol;
+    return t.tl;
+}
 
 // Walk the chain from c while positions stay below re (bits relative to rs).
 __device__ void lane_walk(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t rs, uint32_t re,
@@ -100,29 +152,36 @@ __device__ void lane_walk(const uint8_t* stage, uint32_t woff, uint32_t W0, uint
     uint64_t p = c;
     bool bad = false;
     while (p < re) {
-        const SnapTok t = snap_tok(lds_read8(stage, woff + uint32_t(p - W0)));
+        uint32_t ol;
+        const uint64_t tl = stage_tok(stage, woff + uint32_t(p - W0), ol);
         bit_set(L, uint32_t(p) - rs);
-        const uint32_t o = L.out + t.ol;
+        const uint32_t o = L.out + ol;
         L.out = o < L.out ? 0xffffffffu : o;
-        p += t.tl;
+        p += tl;
         if (p > n) { bad = true; break; }
     }
     L.x = bad ? SNAP_INVALID : uint32_t(p);
 }
 
-// Parse one window whose chain enters at `entry` (W0 <= entry < min(W0 + SNAP_WIN, n)). All 64
-// lanes. Returns the window exit; flags = WIN_BROKEN if the chain runs past the stream end.
-__device__ uint32_t win_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t entry, WinLane& L,
-                              uint32_t& flags, int max_rounds = WIN_ROUNDS) {
+// Speculative parse of one window whose chain enters at `entry` (W0 <= entry < min(W0 + SNAP_WIN,
+// n)), all 64 lanes, linear stage. Each lane walks the chain of its 128-byte region from the region
+// start (a guess: chains started anywhere usually meet the true one within a few tokens); a scalar
+// walk then follows the chain lane to lane from the entry, and a lane whose true entry is not on
+// its guessed chain re-walks from it, until consistent (each round fixes at least the first wrong
+// lane). Returns the window exit; flags = WIN_BROKEN if the chain runs past the stream end,
+// WIN_NOCONV if max_rounds did not converge.
+__device__ uint32_t win_parse_spec(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t entry,
+                                   WinLane& L, uint32_t& flags, int max_rounds = WIN_ROUNDS) {
     const int lane = threadIdx.x & 63;
     const uint32_t rs = W0 + uint32_t(lane) * SNAP_RB;
     const uint32_t re = uint32_t(min(uint64_t(rs) + SNAP_RB, n));
-    const int L0 = int((entry - W0) / SNAP_RB);
+    entry = __builtin_amdgcn_readfirstlane(entry);
+    const uint32_t L0 = (entry - W0) / SNAP_RB;
     L.b0 = L.b1 = L.b2 = L.b3 = 0;
     L.out = 0;
     L.c = rs;
     L.x = SNAP_INVALID;
-    if (lane >= L0 && uint64_t(rs) < n) lane_walk(stage, woff, W0, n, rs, re, lane == L0 ? entry : rs, L);
+    if (uint32_t(lane) >= L0 && uint64_t(rs) < n) lane_walk(stage, woff, W0, n, rs, re, uint32_t(lane) == L0 ? entry : rs, L);
     uint32_t ent = SNAP_INVALID, X = SNAP_INVALID;
     bool converged = false;
     flags = 0;
@@ -130,14 +189,13 @@ __device__ uint32_t win_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, 
         // follow the chain lane to lane (uniform scalar loop)
         ent = SNAP_INVALID;
         flags = 0;
-        int k = L0;
-        uint32_t e = entry;
+        uint32_t k = L0, e = entry;
         for (;;) {
-            if (lane == k) ent = e;
-            const uint32_t x = __builtin_amdgcn_readlane(L.x, k);
+            ent = uint32_t(lane) == k ? e : ent;
+            const uint32_t x = __builtin_amdgcn_readlane(L.x, int(k));
             if (x == SNAP_INVALID) { flags = WIN_BROKEN; X = SNAP_INVALID; break; }
             if (uint64_t(x) >= n || x >= W0 + SNAP_WIN) { X = x; break; }
-            k = int((x - W0) / SNAP_RB);
+            k = (x - W0) / SNAP_RB;
             e = x;
         }
         const bool need = ent != SNAP_INVALID && ent != L.c && !(ent > L.c && bit_get(L, ent - rs));
@@ -152,10 +210,11 @@ __device__ uint32_t win_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, 
     } else if (ent > L.c) {
         uint32_t p = L.c;
         while (p < ent) {
-            const SnapTok t = snap_tok(lds_read8(stage, woff + (p - W0)));
+            uint32_t ol;
+            const uint64_t tl = stage_tok(stage, woff + (p - W0), ol);
             bit_clr(L, p - rs);
-            L.out -= t.ol;
-            p += uint32_t(t.tl);
+            L.out -= ol;
+            p += uint32_t(tl);
         }
         L.c = ent;
     }
@@ -175,32 +234,37 @@ __device__ __forceinline__ SnapEnt mk_ent(uint32_t pos, uint32_t flag, uint32_t 
 // MERGE: pos = meeting point m, out = (true chain output in [e, m)) - (window chain output in
 // [W0, m)). NOMERGE: the chain from e leaves the window first: pos = its exit, out = its output.
 // SLOW: not resolved within ENT_STEPS tokens. BAD: the chain from e runs past the stream end.
-template <class BitF, class TokF>
-__device__ SnapEnt ent_walk(uint32_t e, uint32_t W0, uint64_t wend, uint64_t n, BitF bit, TokF tok) {
+// Linear stage; sb = the window chain's token-start bits, pre[r] = its output before lane region r.
+__device__ SnapEnt ent_walk(uint32_t e, uint32_t W0, uint64_t wend, uint64_t n, const uint8_t* stage, uint32_t woff,
+                            const uint32_t* sb, const uint32_t* pre) {
     uint64_t q = e;
     uint32_t acc = 0;
     int steps = 0;
     for (;;) {
         if (q >= wend) return mk_ent(uint32_t(q), ENT_NOMERGE, acc);
-        if (bit(uint32_t(q))) break;
+        const uint32_t r = uint32_t(q) - W0;
+        if ((sb[r >> 5] >> (r & 31u)) & 1u) break;
         if (steps == ENT_STEPS) return mk_ent(e, ENT_SLOW, 0);
-        const SnapTok t = tok(uint32_t(q));
-        acc += t.ol;
-        q += t.tl;
+        uint32_t ol;
+        const uint64_t tl = stage_tok(stage, woff + r, ol);
+        acc += ol;
+        q += tl;
         steps++;
         if (q > n) return mk_ent(e, ENT_BAD, 0);
     }
-    uint64_t p = W0;
-    uint32_t g = 0;
-    steps = 0;
-    while (p < q) {
-        if (steps == ENT_STEPS) return mk_ent(e, ENT_SLOW, 0);
-        const SnapTok t = tok(uint32_t(p));
-        g += t.ol;
-        p += t.tl;
-        steps++;
+    const uint32_t rel = uint32_t(q) - W0, rq = rel / SNAP_RB;
+    uint32_t g = pre[rq];
+    for (uint32_t b = rq * SNAP_RB; b < rel; b += 32) {
+        const uint32_t hi = rel - b >= 32 ? 0xffffffffu : ((1u << (rel - b)) - 1u);
+        uint32_t mm = sb[b >> 5] & hi;
+        while (mm) {
+            const uint32_t i = b + uint32_t(__ffs(mm) - 1);
+            mm &= mm - 1;
+            uint32_t ol;
+            stage_tok(stage, woff + i, ol);
+            g += ol;
+        }
     }
-    if (p != q) return mk_ent(e, ENT_SLOW, 0);
     return mk_ent(uint32_t(q), ENT_MERGE, acc - g);
 }
 
@@ -264,6 +328,143 @@ __device__ uint32_t seq_parse(const uint8_t* stage, uint32_t woff, uint32_t W0, 
     return uint32_t(cur);
 }
 
+// Exact parse of the 8 KiB window at W0 whose chain enters at `entry` (W0 <= entry < min(W0 + 8 KiB,
+// n)), all 64 lanes, lane k owning input region k. (1) Every offset i of the region is decoded as
+// if a token started there: xs[i][k] = i + token length when that is inside the region, else the
+// tagged offset the token ends at. (2) A backward pass turns this into the region exit of the
+// chain from every offset (tokens are >= 2 bytes, so offsets i and i-1 never depend on each other:
+// two per LDS round trip). Offsets at or past the stream end stop every chain (a chain stepping
+// over n is broken). (3) The true chain crosses the regions with one lookup per region (offsets
+// < 8 from registers). (4) Each lane walks the true chain through its region: token-start bits and
+// output bytes. Returns the window exit (SNAP_INVALID: broken); a saturated exit falls back to the
+// exact whole-wave parse on a linear stage (xs reused). sp must be staged (stage_pad) and synced.
+__device__ uint32_t win_parse(const uint8_t* in, uint64_t n, uint32_t W0, uint32_t entry, const uint8_t* sp,
+                              uint16_t* xs, uint32_t* sbits, uint32_t* slo, WinLane& L) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t rs = W0 + uint32_t(lane) * SNAP_RB;
+    const int64_t nrel = int64_t(n) - int64_t(rs);
+    const uint8_t* mine = sp + uint32_t(lane) * SNAP_PB;
+#ifdef PF_STAMPS
+    unsigned long long pt0 = __builtin_amdgcn_s_memtime();
+#define PT(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (lane == 0) CSTAMP(i, t_ - pt0); pt0 = t_; } while (0)
+#else
+#define PT(i) ((void)0)
+#endif
+    // (1) + (2), 8 offsets at a time from the region end: their tags (and literal length fields)
+    // come from 4 LDS dwords; an exit inside the group is resolved in registers, one beyond it is
+    // read from xs (final already)
+    uint32_t c[8];
+    for (int g = SNAP_RB / 8 - 1; g >= 0; g--) {
+        const uint32_t* mw = reinterpret_cast<const uint32_t*>(mine) + 2 * g;
+        const uint32_t d[4] = {mw[0], mw[1], mw[2], mw[3]};
+        uint32_t tl[8];
+        bool any_long = false;
+        #pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const uint32_t tag = (d[jj >> 2] >> (8 * (jj & 3))) & 0xffu;
+            tl[jj] = tag_tl(tag);
+            any_long |= tag_long(tag);
+        }
+        if (__any(any_long)) {
+            #pragma unroll
+            for (int jj = 0; jj < 8; jj++) {
+                const uint32_t tag = (d[jj >> 2] >> (8 * (jj & 3))) & 0xffu;
+                const int q = (jj + 1) >> 2, sh = (jj + 1) & 3;
+                const uint32_t b1 = __builtin_amdgcn_alignbyte(d[q + 1], d[q], uint32_t(sh));
+                const uint32_t nb = (tag >> 2) - 59u;
+                const uint32_t len = b1 & (nb >= 4u ? 0xffffffffu : (1u << (8u * nb)) - 1u);
+                if (tag_long(tag)) tl[jj] = len >= XS_SAT ? XS_SAT : 2u + nb + len;
+            }
+        }
+        uint32_t res[8];   // 0x8000 | exit offset, or an offset beyond the group to take the exit of
+        #pragma unroll
+        for (int jj = 7; jj >= 0; jj--) {
+            const uint32_t i = uint32_t(8 * g + jj);
+            const uint32_t nx = i + tl[jj];
+            uint32_t r = nx >= SNAP_RB ? (0x8000u | min(nx, XS_SAT)) : nx;
+            #pragma unroll
+            for (int m = jj + 2; m < 8; m++) r = nx == uint32_t(8 * g + m) ? res[m] : r;
+            if (int64_t(i) >= nrel) r = 0x8000u | i;
+            res[jj] = r;
+        }
+        uint32_t rd[8];
+        #pragma unroll
+        for (int jj = 0; jj < 8; jj++) rd[jj] = xs[((res[jj] & 0x8000u) ? uint32_t(8 * g + jj) : res[jj]) * 64 + lane];
+        #pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            c[jj] = (res[jj] & 0x8000u) ? (res[jj] & 0x7fffu) : rd[jj];
+            xs[(8 * g + jj) * 64 + lane] = uint16_t(c[jj]);
+        }
+    }
+    PT(21);
+    PT(22);
+    // (3)
+    uint32_t ent = SNAP_INVALID;
+    uint32_t e = __builtin_amdgcn_readfirstlane(entry);   // the chain walk is uniform (scalar)
+    uint64_t X;
+    bool sat = false;
+    for (;;) {
+        const uint32_t k = (e - W0) >> 7, d = e - W0 - (k << 7);
+        uint32_t x;
+        if (d < 8) {
+            uint32_t r[8];
+            #pragma unroll
+            for (int q = 0; q < 8; q++) r[q] = __builtin_amdgcn_readlane(c[q], int(k));
+            x = r[0];
+            #pragma unroll
+            for (int q = 1; q < 8; q++) x = d == uint32_t(q) ? r[q] : x;
+        } else {
+            x = __builtin_amdgcn_readfirstlane(uint32_t(xs[d * 64 + k]));
+        }
+        ent = uint32_t(lane) == k ? e : ent;
+        if (x == XS_SAT) { sat = true; X = 0; break; }
+        const uint64_t ex = uint64_t(W0) + (k << 7) + x;
+        if (ex >= n || ex >= uint64_t(W0) + SNAP_WIN) { X = ex; break; }
+        e = uint32_t(ex);
+    }
+    PT(23);
+    L.b0 = L.b1 = L.b2 = L.b3 = 0;
+    L.out = 0;
+    if (sat) {   // exact whole-wave parse on a linear stage
+        __syncthreads();
+        const uint32_t woff = snap_stage(reinterpret_cast<uint8_t*>(xs), in, n, W0, SNAP_WSTAGE, lane);
+        reinterpret_cast<uint4*>(sbits)[lane] = make_uint4(0, 0, 0, 0);
+        slo[lane] = 0;
+        __syncthreads();
+        uint32_t sum;
+        const uint64_t wend = min(uint64_t(W0) + SNAP_WIN, n);
+        const uint32_t Xs = seq_parse(reinterpret_cast<const uint8_t*>(xs), woff, W0, n, entry, wend, sbits, slo, sum);
+        __syncthreads();
+        const uint4 v = reinterpret_cast<const uint4*>(sbits)[lane];
+        L.b0 = v.x; L.b1 = v.y; L.b2 = v.z; L.b3 = v.w;
+        L.out = slo[lane];
+        return Xs;
+    }
+    if (X > n) return SNAP_INVALID;
+    // (4)
+    if (ent != SNAP_INVALID) {
+        const uint32_t re = uint32_t(min<uint64_t>(uint64_t(rs) + SNAP_RB, n));
+        uint32_t p = ent;
+        while (p < re) {
+            const uint32_t o = p - rs;
+            const uint32_t tag = (*reinterpret_cast<const uint32_t*>(mine + (o & ~3u)) >> (8u * (o & 3u))) & 0xffu;
+            uint32_t tl = tag_tl(tag), ol = tag_ol(tag);
+            if (tag_long(tag)) {   // < 2^15 past the region (the exits are not saturated)
+                const SnapTok t = snap_tok(lds_read8(mine, o));
+                tl = uint32_t(t.tl);
+                ol = t.ol;
+            }
+            bit_set(L, o);
+            const uint32_t s2 = L.out + ol;
+            L.out = s2 < L.out ? 0xffffffffu : s2;
+            p += tl;
+        }
+    }
+    PT(24);
+    return uint32_t(X);
+#undef PT
+}
+
 __device__ __forceinline__ void store_window(uint32_t* tm, uint32_t* lo, const WinLane& L, int lane) {
     reinterpret_cast<uint4*>(tm)[lane] = make_uint4(L.b0, L.b1, L.b2, L.b3);
     lo[lane] = L.out;
@@ -306,7 +507,7 @@ __global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict
     const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
     __syncthreads();
     uint32_t flags;
-    uint32_t X = win_parse(stage, woff, W0, n, entry, L, flags);
+    uint32_t X = win_parse_spec(stage, woff, W0, n, entry, L, flags);
 #ifdef PF_STAMPS
     { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (lane == 0) { CSTAMP(0, 1); CSTAMP(1, t_ - it0); if (flags & WIN_NOCONV) CSTAMP(2, 1); } it0 = t_; }
 #endif
@@ -333,12 +534,19 @@ __global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict
     // entry table: lane d follows the chain from W0 + d until it meets this window's chain
     __syncthreads();
     reinterpret_cast<uint4*>(sbits)[lane] = make_uint4(L.b0, L.b1, L.b2, L.b3);
+    {   // exclusive prefix of the lane-region outputs (wrapping: only differences are used)
+        uint32_t x = L.out;
+        #pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t y = __shfl_up(x, dd, 64);
+            if (lane >= dd) x += y;
+        }
+        slo[lane] = x - L.out;
+    }
     __syncthreads();
     SnapEnt T = mk_ent(0, ENT_SLOW, 0);
     if (!(flags & WIN_BROKEN) && uint64_t(W0) + lane < wend)
-        T = ent_walk(W0 + uint32_t(lane), W0, wend, n,
-                     [&](uint32_t q) { return (sbits[(q - W0) >> 5] >> ((q - W0) & 31u)) & 1u; },
-                     [&](uint32_t q) { return snap_tok(lds_read8(stage, woff + (q - W0))); });
+        T = ent_walk(W0 + uint32_t(lane), W0, wend, n, stage, woff, sbits, slo);
     ent[size_t(wi) * 64 + lane] = T;
 #ifdef PF_STAMPS
     {
@@ -384,24 +592,67 @@ extern "C" int pf_debug_trace(uint32_t* out, int n, int reset) {
 // ======================================================================== chain pass
 
 constexpr int FIX_MAXW = 1024;       // pages up to 8 MiB compressed (larger: serial fallback)
-constexpr int CHAIN_BLK = 32;        // windows whose records + tables the chain pass stages at once
 
 __device__ __forceinline__ bool tm_get(const uint32_t* tm, uint32_t i) { return (tm[i >> 5] >> (i & 31u)) & 1u; }
 
-// One wave per page. Window 0's entry is exact (after the varint); window w's true entry is
-// window w-1's true exit. For an entry within the first 64 bytes of a window the index pass
-// already knows where that chain meets the window's own chain (SnapEnt table); deeper entries
-// (after a long literal) walk from the bitmap in HBM; windows the table cannot resolve are parsed
-// exactly from the true entry by the whole wave. One table lookup per window. The result replaces
-// the window's SnapWin: {true entry, merge point / exit, true output bytes, WM_* mode}.
+// Entry deeper than 64 bytes into window w (after a long literal): follow the chain from e in HBM
+// until it meets the window's own chain (bitmap) or leaves the window. The window chain's output in
+// [W0, m) is the lane-region counts before m's region plus the tokens of m's region below m.
+__device__ SnapEnt deep_walk(const SnappyJob& job, uint32_t w, uint32_t e, uint64_t wend, const uint32_t* LOw) {
+    const uint64_t n = job.src_len;
+    const uint32_t W0 = w * SNAP_WIN;
+    const uint32_t* tm = job.tokmap + size_t(w) * SNAP_WWORDS;
+    uint64_t q = e;
+    uint32_t acc = 0;
+    int steps = 0;
+    for (;;) {
+        if (q >= wend) return mk_ent(uint32_t(q), ENT_NOMERGE, acc);
+        if (tm_get(tm, uint32_t(q) - W0)) break;
+        if (steps == ENT_STEPS) return mk_ent(e, ENT_SLOW, 0);
+        const SnapTok t = snap_tok(glb_read8(job.src, n, q));
+        acc += t.ol;
+        q += t.tl;
+        steps++;
+        if (q > n) return mk_ent(e, ENT_BAD, 0);
+    }
+    const uint32_t rel = uint32_t(q) - W0, rq = rel / SNAP_RB;
+    uint32_t g = 0;
+    for (uint32_t r = 0; r < rq; r++) g += LOw[r];
+    for (uint32_t b = rq * SNAP_RB; b < rel; b += 32) {
+        const uint32_t hi = rel - b >= 32 ? 0xffffffffu : ((1u << (rel - b)) - 1u);
+        uint32_t mm = tm[b >> 5] & hi;
+        while (mm) {
+            const uint32_t i = b + uint32_t(__ffs(mm) - 1);
+            mm &= mm - 1;
+            g += snap_tok(glb_read8(job.src, n, W0 + i)).ol;
+        }
+    }
+    return mk_ent(uint32_t(q), ENT_MERGE, acc - g);
+}
+
+// One wave per page, lanes over windows. Window 0's entry is exact (after the varint); window w's
+// true entry is window w-1's true exit. Every window's exit as a function of its entry is known
+// from the index pass for entries that merge with the window's own chain (exit = the window's own
+// exit) or that leave it first (the entry table); so all windows are evaluated at once from a
+// guessed entry (the previous window's own exit) and re-evaluated where the previous exit
+// changed, until the entries are consistent: the fixed point of e_w = exit_{w-1}(e_{w-1}) with
+// e_1 exact is unique, so a consistent assignment is the true chain. Usually two rounds, each one
+// table load per window. A window the table cannot resolve (entry not within ENT_STEPS tokens of
+// the chain) stops the propagation; the first such window is parsed exactly by the whole wave
+// once its entry is final, and the rounds continue behind it. The result replaces each window's
+// SnapWin: {true entry, merge point / exit, true output bytes, WM_* mode}.
 __global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict__ jobs, SnapWin* __restrict__ win,
                                                      const SnapEnt* __restrict__ ent, uint32_t* __restrict__ lane_out,
                                                      int* __restrict__ fb) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[SNAP_WSTAGE];
+    __shared__ __attribute__((aligned(16))) uint8_t sp[SNAP_PSTAGE];
+    __shared__ __attribute__((aligned(16))) uint16_t xs[SNAP_RB * 64];
     __shared__ __attribute__((aligned(16))) uint32_t sbits[SNAP_WWORDS];
     __shared__ uint32_t slo[64];
-    __shared__ SnapWin s_win[CHAIN_BLK];
-    __shared__ __attribute__((aligned(16))) SnapEnt s_tab[CHAIN_BLK * 64];
+    __shared__ uint32_t s_e[FIX_MAXW];     // current entry of window w
+    __shared__ uint32_t s_x[FIX_MAXW];     // exit given that entry (unresolved: the window's own exit)
+    __shared__ uint32_t s_pos[FIX_MAXW];   // merge point / exit (SnapWin.exit)
+    __shared__ uint32_t s_out[FIX_MAXW];   // true output bytes
+    __shared__ uint32_t s_mode[FIX_MAXW];  // 0 entry changed, 1 unresolved, else WM_* (WM_DONE: final)
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
     const SnappyJob job = jobs[j];
@@ -416,92 +667,100 @@ __global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict
         return;
     }
     const SnapWin w0 = Wn[0];
-    uint32_t e = w0.exit;
-    if (lane == 0) Wn[0] = SnapWin{w0.entry, w0.exit, w0.out, WM_KEEP};
+    if (lane == 0) {
+        Wn[0] = SnapWin{w0.entry, w0.exit, w0.out, WM_KEEP};
+        s_x[0] = w0.exit;
+        s_mode[0] = WM_KEEP;
+    }
+    for (uint32_t w = 1 + lane; w < nw; w += 64) {   // first guess: the previous window's own exit
+        s_e[w] = w == 1 ? w0.exit : Wn[w - 1].exit;
+        s_mode[w] = 0;
+    }
+    __syncthreads();
 #ifdef PF_STAMPS
     const unsigned long long cstart = __builtin_amdgcn_s_memtime();
     if (lane == 0) { CSTAMP(17, 1); CSTAMP(18, nw); }
 #endif
     bool bad = false;
-    for (uint32_t w = 1; w < nw; w++) {
-        const uint32_t W0 = w * SNAP_WIN;
-        const uint64_t wend = min(uint64_t(W0) + SNAP_WIN, n);
-        const uint32_t cb = (w - 1) % CHAIN_BLK;
-        if (cb == 0) {   // stage the next block of window records and entry tables
+    uint32_t base = 1;       // windows before base are final
+    bool dirty_all = true;   // first round: evaluate every window
+    while (base < nw) {
+        // fixed-point rounds over [base, nw): re-evaluate windows whose entry changed (mode 0).
+        // An unresolved window (mode 1) passes its own exit on as the guess for the next entry.
+        for (;;) {
+            for (uint32_t w = base + lane; w < nw; w += 64) {
+                if (s_mode[w] == WM_DONE || (!dirty_all && s_mode[w] != 0)) continue;
+                const uint32_t e = s_e[w];
+                const uint32_t W0 = w * SNAP_WIN;
+                const uint64_t wend = min(uint64_t(W0) + SNAP_WIN, n);
+                uint32_t x, pos = 0, out = 0, mode;
+                if (uint64_t(e) >= wend) {   // inside a literal that started earlier: no token here
+                    x = e; pos = e; mode = WM_SKIP;
+                } else {
+                    const SnapWin sw = Wn[w];
+                    SnapEnt T = mk_ent(e, ENT_SLOW, 0);
+                    const uint32_t d = e - W0;
+                    if (!(sw.flags & WIN_BROKEN)) {
+#ifdef PF_STAMPS
+                        const unsigned long long dt0 = __builtin_amdgcn_s_memtime();
+#endif
+                        T = d < 64 ? E[size_t(w) * 64 + d] : deep_walk(job, w, e, wend, LO + size_t(w) * 64);
+#ifdef PF_STAMPS
+                        if (d >= 64) { CSTAMP(11, 1); CSTAMP(12, __builtin_amdgcn_s_memtime() - dt0); }
+#endif
+                    }
+                    const uint32_t fl = T.pos >> 30, tp = T.pos & ENT_POS;
+                    x = sw.exit; mode = 1u;
+                    if (fl == ENT_MERGE) { pos = tp; out = sw.out + T.out; mode = WM_MERGE; }
+                    else if (fl == ENT_NOMERGE) { x = tp; pos = tp; out = T.out; mode = WM_FULL; }
+                }
+                s_x[w] = x; s_pos[w] = pos; s_out[w] = out; s_mode[w] = mode;
+            }
+            dirty_all = false;
+            if (lane == 0) CSTAMP(13, 1);
             __syncthreads();
-            const uint32_t nb = min(uint32_t(CHAIN_BLK), nw - w);
-            if (uint32_t(lane) < nb) s_win[lane] = Wn[w + lane];
-            const uint4* src = reinterpret_cast<const uint4*>(E + size_t(w) * 64);
-            for (uint32_t i = lane; i < nb * 32; i += 64) reinterpret_cast<uint4*>(s_tab)[i] = src[i];
+            bool changed = false;
+            for (uint32_t w = base + lane; w < nw; w += 64) {   // window base - 1 is final
+                const uint32_t ne = s_x[w - 1];
+                if (ne != s_e[w]) { s_e[w] = ne; s_mode[w] = 0; changed = true; }
+            }
             __syncthreads();
+            if (!__any(changed)) break;
         }
-        if (uint64_t(e) >= wend) {   // inside a literal that started earlier: no token here
-            if (lane == 0) { Wn[w] = SnapWin{e, e, 0, WM_SKIP}; CSTAMP(10, 1); }
-            continue;
-        }
-        const SnapWin sw = s_win[cb];
-        const uint32_t d = e - W0;
-        const uint32_t* tm = job.tokmap + size_t(w) * SNAP_WWORDS;
-        SnapEnt T;
+        // the first unresolved window: its entry is final now, parse it exactly
+        uint32_t u = nw;
+        for (uint32_t w = base + lane; w < nw; w += 64)
+            if (s_mode[w] == 1u) { u = w; break; }
+        #pragma unroll
+        for (int dd = 32; dd >= 1; dd >>= 1) u = min(u, uint32_t(__shfl_xor(u, dd, 64)));
+        if (u >= nw) break;
 #ifdef PF_STAMPS
-        const unsigned long long ct0 = __builtin_amdgcn_s_memtime();
+        const unsigned long long xt0 = __builtin_amdgcn_s_memtime();
 #endif
-        if (sw.flags & WIN_BROKEN) T = mk_ent(e, ENT_SLOW, 0);
-        else if (d < 64) T = s_tab[cb * 64 + d];
-        else {
-            T = ent_walk(e, W0, wend, n, [&](uint32_t q) { return tm_get(tm, q - W0); },
-                         [&](uint32_t q) { return snap_tok(glb_read8(job.src, n, q)); });
-#ifdef PF_STAMPS
-            if (lane == 0) { CSTAMP(11, 1); CSTAMP(12, __builtin_amdgcn_s_memtime() - ct0); }
-#endif
-        }
-#ifdef PF_STAMPS
-        if (lane == 0) { CSTAMP(13, 1); if ((T.pos >> 30) == ENT_SLOW) CSTAMP(14, 1); if ((T.pos >> 30) == ENT_NOMERGE) CSTAMP(15, 1); }
-#endif
-        const uint32_t fl = T.pos >> 30, pos = T.pos & ENT_POS;
-        if (fl == ENT_BAD) { bad = true; break; }
-        if (fl == ENT_MERGE) {
-            if (lane == 0) Wn[w] = SnapWin{e, pos, sw.out + T.out, WM_MERGE};
-            e = sw.exit;
-            continue;
-        }
-        if (fl == ENT_NOMERGE) {   // the true chain crosses the window without meeting its chain
-            if (lane == 0) Wn[w] = SnapWin{e, pos, T.out, WM_FULL};
-            e = pos;
-            continue;
-        }
-        // unresolved: exact parse of the window from its true entry (lane regions + fixed point)
-        __syncthreads();
-        const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
+        const uint32_t e = s_e[u];
+        const uint32_t W0 = u * SNAP_WIN;
+        stage_pad(sp, job.src, n, W0, lane);
         __syncthreads();
         WinLane WL{};
-        uint32_t wfl;
-        uint32_t X = win_parse(stage, woff, W0, n, e, WL, wfl);
-        uint32_t sum;
-        if (wfl & WIN_NOCONV) {   // guard (cannot happen within WIN_ROUNDS): exact whole-wave parse
-            reinterpret_cast<uint4*>(sbits)[lane] = make_uint4(0, 0, 0, 0);
-            slo[lane] = 0;
-            __syncthreads();
-            X = seq_parse(stage, woff, W0, n, e, wend, sbits, slo, sum);
-            __syncthreads();
-            const uint4 v4 = reinterpret_cast<const uint4*>(sbits)[lane];
-            WL.b0 = v4.x; WL.b1 = v4.y; WL.b2 = v4.z; WL.b3 = v4.w;
-            WL.out = slo[lane];
-        } else if (wfl & WIN_BROKEN) {
-            X = SNAP_INVALID;
-        }
+        const uint32_t X = win_parse(job.src, n, W0, e, sp, xs, sbits, slo, WL);
         if (X == SNAP_INVALID) { bad = true; break; }
-        sum = wave_sum_sat(WL.out);
-        store_window(job.tokmap + size_t(w) * SNAP_WWORDS, LO + size_t(w) * 64, WL, lane);
-        if (lane == 0) Wn[w] = SnapWin{e, X, sum, WM_DONE};
-        e = X;
+        const uint32_t sum = wave_sum_sat(WL.out);
+        store_window(job.tokmap + size_t(u) * SNAP_WWORDS, LO + size_t(u) * 64, WL, lane);
+        __syncthreads();
+        if (lane == 0) {
+            s_x[u] = X; s_pos[u] = X; s_out[u] = sum; s_mode[u] = WM_DONE;
+        }
+        __syncthreads();
+        base = u + 1;
 #ifdef PF_STAMPS
-        if (lane == 0) CSTAMP(16, __builtin_amdgcn_s_memtime() - ct0);
+        if (lane == 0) { CSTAMP(14, 1); CSTAMP(16, __builtin_amdgcn_s_memtime() - xt0); }
 #endif
     }
-    if (bad || uint64_t(e) != n) {
-        if (lane == 0) fb[j] = FB_SERIAL;
+    if (!bad) {
+        bad = uint64_t(s_x[nw - 1]) != n;
+        for (uint32_t w = 1 + lane; w < nw && !bad; w += 64) Wn[w] = SnapWin{s_e[w], s_pos[w], s_out[w], s_mode[w]};
     }
+    if (bad && lane == 0) fb[j] = FB_SERIAL;
 #ifdef PF_STAMPS
     if (lane == 0) { const unsigned long long dt_ = __builtin_amdgcn_s_memtime() - cstart; CSTAMP(19, dt_); atomicMax(&pf_cstamps[20], dt_); }
 #endif
@@ -1741,6 +2000,8 @@ void launch_snappy_serial(const SnappyJob*, int, const int*, DevChunkResult*, hi
 
 // Parse stage (token-start bitmaps, chain, 64 KiB split points) and execute stage, separately so
 // the runtime can time them apart.
+int snappy_exec_mode();
+
 void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
                          SnapEnt* d_ent, uint32_t* d_lane_out, uint32_t* d_splits, uint2* d_subsplits, int* d_fb,
                          hipStream_t s) {
@@ -1748,8 +2009,9 @@ void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins
     hipLaunchKernelGGL(k_snappy_index, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, d_win, d_ent, d_lane_out, d_fb);
     hipLaunchKernelGGL(k_snappy_chain, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_win, (const SnapEnt*)d_ent, d_lane_out, d_fb);
     hipLaunchKernelGGL(k_snappy_repair, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, (const SnapWin*)d_win, d_lane_out, d_fb);
+    // sub-piece boundaries only for the sub-piece executor (PF_EXEC=3)
     hipLaunchKernelGGL(k_snappy_splits, dim3(n_jobs), dim3(64), 0, s, d_jobs, (const SnapWin*)d_win,
-                       (const uint32_t*)d_lane_out, d_splits, d_subsplits, d_fb);
+                       (const uint32_t*)d_lane_out, d_splits, snappy_exec_mode() == 3 ? d_subsplits : nullptr, d_fb);
 }
 
 int snappy_exec_mode() {

@@ -1,4 +1,4 @@
-"""Diagnostic (stamps build: PFLOOR_LIB_PATH=parquet-floor_amd/build/stamps/libpfloor_stamps.so):
+"""Diagnostic (stamps build: PFLOOR_LIB_PATH=parquet-floor_amd/diag/libpfloor_stamps.so):
 decompress the first PLAIN data page of some lineitem columns through pf_snappy_decompress and
 print the executor's per-phase s_memtime cycle sums per piece."""
 import ctypes as C
