@@ -398,12 +398,43 @@ __device__ uint32_t win_parse(const uint8_t* in, uint64_t n, uint32_t W0, uint32
     }
     PT(21);
     PT(22);
-    // (3)
+    // (3) region entries by a prefix over the lanes of entry maps: lane k's map sends an entry
+    // offset d < 8 to the offset its chain enters region k+1 at (8: not below 8 there, or it
+    // leaves otherwise). The chain is exact up to the first lane the maps lose it at; from there a
+    // scalar walk follows it region by region.
+    uint32_t e = __builtin_amdgcn_readfirstlane(entry);
+    const uint32_t L0 = (e - W0) >> 7, d0 = e - W0 - (L0 << 7);
     uint32_t ent = SNAP_INVALID;
-    uint32_t e = __builtin_amdgcn_readfirstlane(entry);   // the chain walk is uniform (scalar)
+    if (d0 < 8) {
+        uint32_t P = 0;
+        #pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t o = c[q] - SNAP_RB;
+            P |= (o < 8u ? o : 8u) << (4 * q);
+        }
+        if (uint32_t(lane) < L0) P = 0x76543210u;   // identity
+        #pragma unroll
+        for (int h = 1; h < 64; h <<= 1) {
+            uint32_t A = __shfl_up(P, h, 64);
+            if (lane < h) A = 0x76543210u;
+            uint32_t np = 0;
+            #pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint32_t a = (A >> (4 * q)) & 15u;
+                np |= (a >= 8u ? 8u : (P >> (4u * a)) & 15u) << (4 * q);
+            }
+            P = np;
+        }
+        const uint32_t Pp = __shfl_up(P, 1, 64);
+        const uint32_t off = uint32_t(lane) == L0 ? d0 : (uint32_t(lane) > L0 ? (Pp >> (4u * d0)) & 15u : 8u);
+        const uint64_t lost = __ballot(uint32_t(lane) > L0 && off == 8u);
+        const uint32_t j = lost ? uint32_t(__ffsll((unsigned long long)lost) - 1) : 64u;
+        if (uint32_t(lane) >= L0 && uint32_t(lane) < j) ent = rs + off;
+        e = __builtin_amdgcn_readlane(ent, int(j - 1));   // the last lane the maps resolved
+    }
     uint64_t X;
     bool sat = false;
-    for (;;) {
+    for (;;) {   // uniform (scalar) walk
         const uint32_t k = (e - W0) >> 7, d = e - W0 - (k << 7);
         uint32_t x;
         if (d < 8) {
@@ -595,6 +626,8 @@ constexpr int FIX_MAXW = 1024;       // pages up to 8 MiB compressed (larger: se
 
 __device__ __forceinline__ bool tm_get(const uint32_t* tm, uint32_t i) { return (tm[i >> 5] >> (i & 31u)) & 1u; }
 
+constexpr int DEEP_STEPS = 24;       // HBM token walks of the chain pass; longer: exact parse of the window
+
 // Entry deeper than 64 bytes into window w (after a long literal): follow the chain from e in HBM
 // until it meets the window's own chain (bitmap) or leaves the window. The window chain's output in
 // [W0, m) is the lane-region counts before m's region plus the tokens of m's region below m.
@@ -608,7 +641,7 @@ __device__ SnapEnt deep_walk(const SnappyJob& job, uint32_t w, uint32_t e, uint6
     for (;;) {
         if (q >= wend) return mk_ent(uint32_t(q), ENT_NOMERGE, acc);
         if (tm_get(tm, uint32_t(q) - W0)) break;
-        if (steps == ENT_STEPS) return mk_ent(e, ENT_SLOW, 0);
+        if (steps == DEEP_STEPS) return mk_ent(e, ENT_SLOW, 0);
         const SnapTok t = snap_tok(glb_read8(job.src, n, q));
         acc += t.ol;
         q += t.tl;
