@@ -208,6 +208,30 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
  * independent 64 KiB blocks, or corrupt), 0 if the block-parallel kernels decoded it. */
 int pf_snappy_last_fallback(pf_ctx* ctx);
 
+/* ---- GPU page-header scan (the per-page Thrift walk of ParquetFileReader.readNextRowGroup,
+ *      ParquetReader.java:183, moved to the device) with optional page CRC32 verification
+ *      (parquet-mr ParquetReadOptions.usePageChecksumVerification: a page whose PageHeader.crc,
+ *      field 4, differs from the CRC32 of its on-disk page bytes is rejected). Pages are read
+ *      until the chunk's num_values level entries have been seen; INDEX / unknown pages are
+ *      skipped; the descriptors are exactly what pf_file_chunk_desc (the host walk) produces. */
+typedef struct pf_scan_chunk {
+    uint64_t chunk_offset;        /* first byte of the chunk in `bytes` */
+    uint64_t chunk_size;          /* ColumnMetaData.total_compressed_size */
+    int64_t  num_values;          /* ColumnMetaData.num_values */
+    int32_t  page_base;           /* first slot of this chunk's descriptors in pages_out */
+    int32_t  page_cap;            /* slots available to it */
+} pf_scan_chunk;
+typedef struct pf_scan_result {
+    int32_t n_pages;              /* dictionary + data pages found */
+    int32_t status;               /* PF_OK, PF_ERR_CORRUPT_PAGE (header, bounds or CRC), PF_ERR_CAPACITY */
+    int32_t err_page;             /* chunk-relative page of the first error, -1 */
+    int32_t crc_pages;            /* pages whose CRC was verified (verify_crc, header has a crc) */
+} pf_scan_result;
+/* Synchronous. `bytes` is host memory (copied to the device) unless bytes_on_device != 0.
+ * pages_out has room for every chunk's [page_base, page_base + page_cap) slots; results has
+ * n_chunks entries. Returns the first chunk error (PF_OK if none). */
+int pf_scan_pages(pf_ctx* ctx, const pf_scan_chunk* chunks, int n_chunks, const uint8_t* bytes, size_t n_bytes,
+                  int bytes_on_device, int verify_crc, pf_page_desc* pages_out, pf_scan_result* results);
 /* ---- host-side metadata parse: the stand-in for the Java side's parquet-mr footer /
  *      PageHeader parse (ParquetFileReader.open + readNextRowGroup,
  *      ParquetReader.java:120, :183). Builds the descriptors above from a file. ---- */

@@ -610,6 +610,7 @@ static int delta_binary_decode(const uint8_t* p, size_t n, int is64, uint64_t* o
 typedef struct {
     int type; int32_t usize, csize;
     int32_t num_values, encoding, def_enc, rep_enc, num_nulls, num_rows, def_bytes, rep_bytes, is_compressed;
+    int has_crc; uint32_t crc;                 /* PageHeader.crc (field 4) */
     const uint8_t* body;
 } page_t;
 
@@ -620,6 +621,7 @@ static int parse_page_header(tr_t* r, page_t* pg) {
         if (id == 1) pg->type = (int)tr_int(r, t);
         else if (id == 2) pg->usize = (int32_t)tr_int(r, t);
         else if (id == 3) pg->csize = (int32_t)tr_int(r, t);
+        else if (id == 4 && t == 5) { pg->crc = (uint32_t)tr_int(r, t); pg->has_crc = 1; }
         else if ((id == 5 || id == 7 || id == 8) && t == 12) {
             int l2 = 0, t2, f2;
             while ((f2 = tr_field(r, &l2, &t2))) {
@@ -1004,4 +1006,59 @@ void pfo_free_column(pfo_column* c) {
     free(c->values); free(c->validity); free(c->offsets); free(c->chars);
     free(c->list_offsets); free(c->list_validity); free(c->def_levels); free(c->rep_levels);
     memset(c, 0, sizeof(*c));
+}
+
+/* ------------------------------------------------------------------ page walk + CRC32 (scan oracle) */
+/* CRC-32 of java.util.zip.CRC32 / zlib (reflected polynomial 0xEDB88320, init and final xor ~0),
+ * bit at a time. parquet-mr 1.12.2 ParquetFileReader.Chunk.verifyCrc compares it with PageHeader.crc
+ * over the page's on-disk (compressed) bytes. */
+uint32_t pfo_crc32(const uint8_t* p, size_t n) {
+    uint32_t c = 0xffffffffu;
+    for (size_t i = 0; i < n; i++) {
+        c ^= p[i];
+        for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xedb88320u : c >> 1;
+    }
+    return c ^ 0xffffffffu;
+}
+
+/* parquet-mr Chunk.readAllPages: PageHeaders until num_values level entries are seen (the loop of
+ * pfo_decode above); dictionary and data pages are listed, INDEX / unknown pages skipped. With
+ * verify_crc, a listed page whose header carries a crc must match pfo_crc32 of its bytes
+ * (usePageChecksumVerification). Returns the page count, or a negative status with *err_page. */
+int pfo_chunk_pages(pfo_file* f, int rg, int col, pfo_page* out, int cap, int verify_crc, int* err_page) {
+    *err_page = -1;
+    if (rg < 0 || rg >= f->nrg || col < 0 || col >= f->nleaves) return E_ARG;
+    const chunk_meta* m = &f->rgs[rg].cols[col];
+    int64_t start = m->data_page_offset;
+    if (m->has_dict_offset && m->dictionary_page_offset > 0 && m->dictionary_page_offset < start) start = m->dictionary_page_offset;
+    const int64_t end = start + m->total_compressed_size;
+    if (m->num_values == 0) return 0;
+    if (start < 4 || end > (int64_t)f->size || m->total_compressed_size < 0) return E_CORRUPT;
+    const uint8_t* base = f->data + start;
+    const uint8_t* p = base;
+    const uint8_t* e = f->data + end;
+    int64_t seen = 0;
+    int n = 0;
+    while (seen < m->num_values) {
+        if (p >= e) { *err_page = n; return E_CORRUPT; }
+        tr_t r = { p, e, 0 };
+        page_t pg;
+        if (parse_page_header(&r, &pg) || pg.csize < 0 || (int64_t)(e - r.p) < pg.csize) { *err_page = n; return E_CORRUPT; }
+        p = r.p + pg.csize;
+        if (pg.type != 0 && pg.type != 2 && pg.type != 3) continue;
+        if (pg.type == 2 && n > 0) { *err_page = n; return E_CORRUPT; }
+        if (pg.type != 2) {
+            if (pg.num_values < 0) { *err_page = n; return E_CORRUPT; }
+            seen += pg.num_values;
+        }
+        if (n >= cap) { *err_page = n; return E_CAP; }
+        pfo_page* o = &out[n];
+        o->offset = (uint64_t)(r.p - base);
+        o->compressed_size = pg.csize; o->uncompressed_size = pg.usize; o->page_type = pg.type;
+        o->encoding = pg.encoding; o->num_values = pg.num_values; o->has_crc = pg.has_crc; o->crc = pg.crc;
+        o->crc_ok = pg.has_crc ? pfo_crc32(r.p, (size_t)pg.csize) == pg.crc : 1;
+        if (verify_crc && !o->crc_ok) { *err_page = n; return E_CORRUPT; }
+        n++;
+    }
+    return n;
 }

@@ -56,6 +56,17 @@ void pfo_free_column(pfo_column* c);
 int64_t pfo_snappy_uncompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap);
 int64_t pfo_snappy_uncompressed_length(const uint8_t* in, size_t n);
 /* Test-vector generator: greedy Snappy compressor (mode 0 Google-style 64 KiB blocks, mode 1 cross-block). */
+/* Page-header walk + CRC32 of one chunk (oracle of pf_scan_pages). */
+typedef struct pfo_page {
+    uint64_t offset;              /* page body, relative to the chunk's first byte */
+    int32_t compressed_size, uncompressed_size, page_type, encoding, num_values;
+    int32_t has_crc;              /* PageHeader.crc present */
+    uint32_t crc;
+    int32_t crc_ok;               /* CRC32 of the page bytes == crc (1 without a crc) */
+} pfo_page;
+int pfo_chunk_pages(pfo_file* f, int rg, int col, pfo_page* out, int cap, int verify_crc, int* err_page);
+uint32_t pfo_crc32(const uint8_t* p, size_t n);
+
 int64_t pfo_snappy_compress(const uint8_t* in, size_t n, uint8_t* out, size_t cap, int mode);
 
 #ifdef __cplusplus

@@ -149,4 +149,28 @@ struct DevChunkResult {
     int32_t err_page;
 };
 
+// GPU page-header scan (pf_scan.hip, pf_scan_pages)
+struct ScanChunk {            // device copy of pf_scan_chunk
+    const uint8_t* base;      // chunk's first byte
+    uint64_t size;
+    int64_t num_values;
+    int32_t page_base;
+    int32_t page_cap;
+};
+
+struct ScanCrc {              // per page slot: header crc and the page bytes it covers
+    const uint8_t* body;
+    uint32_t len;
+    uint32_t crc;
+    int32_t has_crc;
+    int32_t chunk;
+};
+
+struct ScanResult {           // mirrors pf_scan_result
+    int32_t n_pages;
+    int32_t status;
+    int32_t err_page;
+    int32_t crc_pages;
+};
+
 }  // namespace pf

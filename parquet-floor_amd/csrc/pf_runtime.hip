@@ -39,6 +39,8 @@ void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hi
 void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_page_scan(const ScanChunk*, int, pf_page_desc*, ScanCrc*, ScanResult*, hipStream_t);
+void launch_page_crc(const ScanCrc*, const int*, int, ScanResult*, int32_t*, hipStream_t);
 }  // namespace pf
 
 using namespace pf;
@@ -96,6 +98,7 @@ struct pf_ctx {
     hipEvent_t ev[N_EVENTS] = {};
     std::string err;
     DevBuf d_in, d_scratch, d_out, d_bits, d_chars, d_meta, d_tokmap;
+    DevBuf d_scan_in, d_scan;              // pf_scan_pages: host chunk bytes, tables
     HostBuf h_meta, h_res;
     // last batch
     int n_chunks = 0;
@@ -395,7 +398,8 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->exec_stream) (void)hipStreamSynchronize(ctx->exec_stream);
-    for (DevBuf* b : {&ctx->d_in, &ctx->d_scratch, &ctx->d_out, &ctx->d_bits, &ctx->d_chars, &ctx->d_meta, &ctx->d_tokmap})
+    for (DevBuf* b : {&ctx->d_in, &ctx->d_scratch, &ctx->d_out, &ctx->d_bits, &ctx->d_chars, &ctx->d_meta, &ctx->d_tokmap,
+                      &ctx->d_scan_in, &ctx->d_scan})
         b->release();
     ctx->h_meta.release();
     ctx->h_res.release();
@@ -1022,6 +1026,92 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     const DevChunkResult* r = static_cast<const DevChunkResult*>(ctx->h_res.p);
     if (r->status != 0) return fail(ctx, r->status, "snappy: corrupt input");
     return PF_OK;
+}
+
+// GPU page-header scan (pfloor.h): k_page_scan per chunk, then k_page_crc over the pages found.
+int pf_scan_pages(pf_ctx* ctx, const pf_scan_chunk* chunks, int n_chunks, const uint8_t* bytes, size_t n_bytes,
+                  int bytes_on_device, int verify_crc, pf_page_desc* pages_out, pf_scan_result* results) {
+    if (!ctx || n_chunks < 0 || (n_chunks && (!chunks || !results || !pages_out)) || (!bytes && n_bytes))
+        return fail(ctx, PF_ERR_INVALID_ARG, "scan: null arg");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "previous decode not waited for");
+    if (n_chunks == 0) return PF_OK;
+    int64_t slots = 0;
+    for (int c = 0; c < n_chunks; c++) {
+        const pf_scan_chunk& k = chunks[c];
+        if (k.page_base < 0 || k.page_cap < 0 || k.chunk_offset > n_bytes || k.chunk_size > n_bytes - k.chunk_offset)
+            return fail(ctx, PF_ERR_INVALID_ARG, "scan: chunk " + std::to_string(c) + " outside the buffer / bad slots");
+        slots = std::max<int64_t>(slots, int64_t(k.page_base) + k.page_cap);
+    }
+    if (slots > (int64_t(1) << 30)) return fail(ctx, PF_ERR_INVALID_ARG, "scan: too many page slots");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    if (ctx->copies_pending) HIPCHK(ctx, hipStreamSynchronize(st));
+    ctx->copies_pending = false;
+    const uint8_t* d_bytes = bytes;
+    if (!bytes_on_device && n_bytes) {
+        HIPCHK(ctx, ctx->d_scan_in.ensure(n_bytes));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_scan_in.p, bytes, n_bytes, hipMemcpyHostToDevice, st));
+        d_bytes = static_cast<const uint8_t*>(ctx->d_scan_in.p);
+    }
+    size_t m = 0;
+    auto take = [](size_t& cursor, size_t sz) { size_t o = align_up(cursor, 256); cursor = o + sz; return o; };
+    const size_t ns = size_t(std::max<int64_t>(slots, 1));
+    const size_t o_ck = take(m, sizeof(ScanChunk) * n_chunks), o_pg = take(m, sizeof(pf_page_desc) * ns);
+    const size_t o_crc = take(m, sizeof(ScanCrc) * ns), o_res = take(m, sizeof(ScanResult) * n_chunks);
+    const size_t o_bad = take(m, 4 * size_t(n_chunks)), o_list = take(m, 4 * ns);
+    m = align_up(m, 256);
+    HIPCHK(ctx, ctx->d_scan.ensure(m));
+    HIPCHK(ctx, ctx->h_meta.ensure(m));
+    uint8_t* h = static_cast<uint8_t*>(ctx->h_meta.p);
+    uint8_t* d = static_cast<uint8_t*>(ctx->d_scan.p);
+    ScanChunk* hc = reinterpret_cast<ScanChunk*>(h + o_ck);
+    for (int c = 0; c < n_chunks; c++)
+        hc[c] = ScanChunk{d_bytes + chunks[c].chunk_offset, chunks[c].chunk_size, chunks[c].num_values, chunks[c].page_base,
+                          chunks[c].page_cap};
+    int32_t* hbad = reinterpret_cast<int32_t*>(h + o_bad);
+    for (int c = 0; c < n_chunks; c++) hbad[c] = INT32_MAX;
+    HIPCHK(ctx, hipMemcpyAsync(d + o_ck, h + o_ck, o_list - o_ck, hipMemcpyHostToDevice, st));
+    ScanResult* d_res = reinterpret_cast<ScanResult*>(d + o_res);
+    ScanCrc* d_crc = reinterpret_cast<ScanCrc*>(d + o_crc);
+    launch_page_scan(reinterpret_cast<const ScanChunk*>(d + o_ck), n_chunks, reinterpret_cast<pf_page_desc*>(d + o_pg),
+                     d_crc, d_res, st);
+    HIPCHK(ctx, hipGetLastError());
+    ScanResult* hr = reinterpret_cast<ScanResult*>(h + o_res);
+    HIPCHK(ctx, hipMemcpyAsync(hr, d_res, sizeof(ScanResult) * n_chunks, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    if (verify_crc) {
+        int32_t* hl = reinterpret_cast<int32_t*>(h + o_list);
+        int n = 0;
+        for (int c = 0; c < n_chunks; c++)
+            for (int i = 0; i < hr[c].n_pages; i++) hl[n++] = chunks[c].page_base + i;
+        if (n) {
+            HIPCHK(ctx, hipMemcpyAsync(d + o_list, hl, 4 * size_t(n), hipMemcpyHostToDevice, st));
+            launch_page_crc(d_crc, reinterpret_cast<const int*>(d + o_list), n, d_res, reinterpret_cast<int32_t*>(d + o_bad), st);
+            HIPCHK(ctx, hipGetLastError());
+            HIPCHK(ctx, hipMemcpyAsync(hr, d_res, sizeof(ScanResult) * n_chunks, hipMemcpyDeviceToHost, st));
+            HIPCHK(ctx, hipMemcpyAsync(hbad, d + o_bad, 4 * size_t(n_chunks), hipMemcpyDeviceToHost, st));
+        }
+    }
+    HIPCHK(ctx, hipMemcpyAsync(pages_out, d + o_pg, sizeof(pf_page_desc) * size_t(slots), hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    int rc = PF_OK;
+    for (int c = 0; c < n_chunks; c++) {
+        pf_scan_result& r = results[c];
+        r.n_pages = hr[c].n_pages;
+        r.status = hr[c].status;
+        r.err_page = hr[c].err_page;
+        r.crc_pages = hr[c].crc_pages;
+        if (r.status == PF_OK && verify_crc && hbad[c] != INT32_MAX) {
+            r.status = PF_ERR_CORRUPT_PAGE;
+            r.err_page = hbad[c] - chunks[c].page_base;
+        }
+        if (r.status != PF_OK && rc == PF_OK) {
+            rc = r.status;
+            fail(ctx, rc, "scan: chunk " + std::to_string(c) + " page " + std::to_string(r.err_page) +
+                              (hbad[c] != INT32_MAX && verify_crc ? ": CRC checksum verification failed" : ": corrupt page header"));
+        }
+    }
+    return rc;
 }
 
 // Test hook: which path decoded the last pf_snappy_decompress (1 = serial fallback).

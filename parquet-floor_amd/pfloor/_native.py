@@ -60,6 +60,15 @@ class ColumnMeta(C.Structure):
                 ("logical_type", C.c_int32), ("scale", C.c_int32), ("precision", C.c_int32)]
 
 
+class ScanChunk(C.Structure):
+    _fields_ = [("chunk_offset", C.c_uint64), ("chunk_size", C.c_uint64), ("num_values", C.c_int64),
+                ("page_base", C.c_int32), ("page_cap", C.c_int32)]
+
+
+class ScanResult(C.Structure):
+    _fields_ = [("n_pages", C.c_int32), ("status", C.c_int32), ("err_page", C.c_int32), ("crc_pages", C.c_int32)]
+
+
 class PfError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"{STATUS.get(code, code)}: {msg}")
@@ -99,6 +108,8 @@ def lib():
         "pf_last_timing": ([vp, C.POINTER(C.c_float), i32, C.POINTER(C.c_int)], C.c_int),
         "pf_snappy_decompress": ([vp, vp, sz, vp, sz, C.POINTER(C.c_size_t)], C.c_int),
         "pf_snappy_last_fallback": ([vp], C.c_int),
+        "pf_scan_pages": ([vp, C.POINTER(ScanChunk), i32, vp, sz, i32, i32, C.POINTER(PageDesc),
+                           C.POINTER(ScanResult)], C.c_int),
         "pf_file_open": ([C.c_char_p, C.POINTER(vp)], C.c_int),
         "pf_file_close": ([vp], C.c_int),
         "pf_file_num_row_groups": ([vp, C.POINTER(C.c_int)], C.c_int),

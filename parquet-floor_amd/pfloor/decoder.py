@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._native import ChunkDesc, ColumnInfo, ColumnMeta, ColumnOut, check, lib
+from ._native import ChunkDesc, ColumnInfo, ColumnMeta, ColumnOut, PageDesc, ScanChunk, ScanResult, check, lib
 
 CONVERTED_UTF8, CONVERTED_ENUM, CONVERTED_JSON = 0, 4, 19
 LOGICAL_STRING, LOGICAL_ENUM, LOGICAL_JSON = 1, 4, 12
@@ -195,6 +195,26 @@ class GpuDecoder:
         if rc != 0:
             return rc, None
         return dst[:out_len.value].tobytes(), L.pf_snappy_last_fallback(self.h)
+
+    def scan_pages(self, data, chunks, verify_crc=False, page_cap=4096):
+        """GPU page-header scan (pf_scan_pages) of column chunks in one host buffer.
+        chunks: [(chunk_offset, chunk_size, num_values)]. Returns (rc, [(status, err_page, crc_pages,
+        [page dicts])] per chunk)."""
+        L = lib()
+        buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+        n = len(chunks)
+        sc = (ScanChunk * max(n, 1))()
+        for i, (off, size, nv) in enumerate(chunks):
+            sc[i] = ScanChunk(off, size, nv, i * page_cap, page_cap)
+        pages = (PageDesc * max(1, n * page_cap))()
+        res = (ScanResult * max(n, 1))()
+        rc = L.pf_scan_pages(self.h, sc, n, buf.ctypes.data, len(data), 0, int(verify_crc), pages, res)
+        out = []
+        for i in range(n):
+            r = res[i]
+            pg = [{f: getattr(pages[i * page_cap + k], f) for f, _ in PageDesc._fields_} for k in range(r.n_pages)]
+            out.append((r.status, r.err_page, r.crc_pages, pg))
+        return rc, out
 
     def timing(self):
         buf = (C.c_float * 16)()

@@ -46,6 +46,10 @@ class Oracle:
         L.pfo_snappy_uncompressed_length.restype = C.c_int64
         L.pfo_snappy_compress.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int]
         L.pfo_snappy_compress.restype = C.c_int64
+        L.pfo_chunk_pages.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(PfoPage), C.c_int, C.c_int,
+                                      C.POINTER(C.c_int)]
+        L.pfo_crc32.argtypes = [C.c_char_p, C.c_size_t]
+        L.pfo_crc32.restype = C.c_uint32
 
     def snappy_compress(self, data: bytes, mode=0):
         """Test-vector generator: mode 0 Google-style 64 KiB blocks, mode 1 cross-block copies."""
@@ -65,8 +69,17 @@ class Oracle:
             return got
         return out.raw[:got]
 
+    def crc32(self, data: bytes):
+        return self.lib.pfo_crc32(data, len(data))
+
     def open(self, path=None, data=None):
         return OracleFile(self, path, data)
+
+
+class PfoPage(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("compressed_size", C.c_int32), ("uncompressed_size", C.c_int32),
+                ("page_type", C.c_int32), ("encoding", C.c_int32), ("num_values", C.c_int32), ("has_crc", C.c_int32),
+                ("crc", C.c_uint32), ("crc_ok", C.c_int32)]
 
 
 class OracleFile:
@@ -115,6 +128,14 @@ class OracleFile:
         self.o.lib.pfo_column_schema(self.h, c, a)
         return dict(zip(("type", "type_length", "max_def", "max_rep", "repeated_def", "list_null_def",
                          "converted_type"), list(a)))
+
+    def chunk_pages(self, rg, col, verify_crc=False, cap=100000):
+        """(status or page count, err_page, [page dicts]) of the oracle's PageHeader walk."""
+        out = (PfoPage * cap)()
+        err = C.c_int(-1)
+        n = self.o.lib.pfo_chunk_pages(self.h, rg, col, out, cap, int(verify_crc), C.byref(err))
+        pages = [{f: getattr(out[i], f) for f, _ in PfoPage._fields_} for i in range(max(n, 0))]
+        return n, err.value, pages
 
     def decode(self, rg, col):
         """Decoded chunk as a dict of numpy arrays in the canonical layout (pfloor.h)."""

@@ -78,7 +78,8 @@ def test_struct_layouts_match_header(native, tmp_path):
     import subprocess
     structs = {"pf_page_desc": native.PageDesc, "pf_chunk_desc": native.ChunkDesc,
                "pf_column_out": native.ColumnOut, "pf_column_info": native.ColumnInfo,
-               "pf_column_meta": native.ColumnMeta}
+               "pf_column_meta": native.ColumnMeta, "pf_scan_chunk": native.ScanChunk,
+               "pf_scan_result": native.ScanResult}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "pfloor.h"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
