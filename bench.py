@@ -122,6 +122,30 @@ def units_for_rank(args, pf, world, rank, S):
         g, p, _ = units[0]
         k = max(1, min(S, len(cols)))
         units = [(g, p, cols[i::k]) for i in range(k)] + units[1:]
+    elif getattr(args, "split", "rowgroups") == "columns" and units and S > 1 and WORKLOADS[args.workload]["batch"] <= 0:
+        # Each context decodes a few columns over the rank's row groups: a stage's latency is set by
+        # its slowest item (a heavy column's Snappy pieces, string blocks) more than by how many items
+        # it has, so heavy columns go to different contexts and their stage chains overlap instead
+        # of adding up. A column heavier than a context's fair share is cut into that many slices of
+        # its row groups; slices go longest-processing-time first (compressed bytes) to the least
+        # loaded context.
+        size = {(p, c): pf.chunk_range(p, c)[1] for _, p, _ in units for c in cols}
+        cost = {c: sum(size[(p, c)] for _, p, _ in units) for c in cols}
+        share = sum(cost.values()) / S
+        slices = []
+        for c in cols:
+            k = max(1, min(len(units), -(-cost[c] // max(1, int(share)))))
+            for j in range(k):
+                us = units[j::k]
+                slices.append((sum(size[(p, c)] for _, p, _ in us), c, [(g, p) for g, p, _ in us]))
+        load = [0] * S
+        per = [dict() for _ in range(S)]          # context -> {(g, p): [columns]}
+        for cst, c, gps in sorted(slices, key=lambda t: -t[0]):
+            k = min(range(S), key=lambda k: load[k])
+            load[k] += cst
+            for gp in gps:
+                per[k].setdefault(gp, []).append(c)
+        return [[[(g, p, sorted(cs)) for (g, p), cs in sorted(d.items())]] for d in per if d], n_log, mine
     S = max(1, min(S, len(units)))
     per_ctx = [units[k::S] for k in range(S)]
     bsz = WORKLOADS[args.workload]["batch"]
@@ -234,7 +258,7 @@ def measure_pmc(args, kernel_re):
         d = os.path.join(out, cnt)
         cmd = [prof, "--pmc", cnt, "--kernel-include-regex", kernel_re, "--output-format", "csv", "-d", d, "-o", "run",
                "--", sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
-               "--data-dir", args.data_dir, "--streams", str(args.streams)]
+               "--data-dir", args.data_dir, "--streams", str(args.streams), "--split", args.split]
         t0 = time.time()
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
         log(f"[bench] rocprofv3 --pmc {cnt}: rc {r.returncode} in {time.time() - t0:.1f}s")
@@ -471,6 +495,8 @@ def main():
     ap.add_argument("--data-dir", default=os.environ.get("PF_BENCH_DIR", "/tmp/pfloor_bench"))
     ap.add_argument("--streams", type=int, default=4,
                     help="decode contexts (HIP streams) per GPU; work units are dealt round-robin to them")
+    ap.add_argument("--split", choices=("columns", "rowgroups"), default="columns",
+                    help="sf1: give each context all row groups of a column subset (default) or whole row groups")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -650,7 +676,9 @@ def main():
                    "row_groups_per_rank": len(mine), "decoded_bytes_per_step": int(tot[0]),
                    "compressed_page_bytes_rank0": st_all["compressed"],
                    "parallelism": f"row groups sharded round-robin over {world} GPU(s) (pfloor.shard, no collective), "
-                                  f"{S} decode streams per GPU"},
+                                  f"{S} decode streams per GPU" +
+                                  (", each stream all row groups of a column subset (LPT on compressed bytes)"
+                                   if args.split == "columns" and args.workload == "sf1" and S > 1 else "")},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "host_enqueue_ms_per_batch": round(host_plan_ms, 4),
         "roofline": {"bound": "hbm", "kernel": STAGE_LABEL.get(dom, dom), "achieved": round(achieved, 2) if achieved else None,
