@@ -13,8 +13,8 @@ per = collections.defaultdict(list)
 for r in rows:
     n = r["Kernel_Name"].split("(")[0].replace("pf::", "")
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-    if n == "k_snappy_exec" and d < 100:
-        n = "k_snappy_exec_redo"
+    if n.startswith("k_snappy_exec") and d < 100:
+        n += "_redo"
     per[n].append(d)
 print(f"{'kernel':24s} {'launches':>8s} {'avg_us':>10s} {'avg_last%d_us' % passes:>14s}")
 for n, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
