@@ -1366,20 +1366,35 @@ __device__ inline void copy_chars_fast(const uint32_t* coff, const uint32_t* csr
                 continue;
             }
         }
-        const uint8_t* sp = sbase + (int64_t(csrc[v]) - int64_t(vb));
+        // the chunk spans values: one aligned 16-byte window per value piece, blended under a byte mask
+        // (dword loads that overlap the piece's source bytes only, so every load stays in the source)
         uint32_t word[4] = {0, 0, 0, 0};
-        #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int64_t r = r0 + k;
-            if (r >= 0 && r < int64_t(total)) {
-                while (uint32_t(r) >= vend) {
-                    v++;
-                    vb = coff[v];
-                    vend = v + 1 < nv ? coff[v + 1] : total;
-                    sp = sbase + (int64_t(csrc[v]) - int64_t(vb));
+        for (;;) {
+            const int64_t lo = max(max(r0, int64_t(vb)), int64_t(0)), hi = min(min(r0 + 16, int64_t(vend)), int64_t(total));
+            if (lo < hi) {
+                const uintptr_t need0 = reinterpret_cast<uintptr_t>(sbase) + csrc[v] + uint32_t(lo - vb);
+                const uintptr_t need1 = need0 + uintptr_t(hi - lo);            // source bytes [need0, need1)
+                const uintptr_t ws = need0 - uintptr_t(lo - r0);               // source of chunk byte 0
+                const uintptr_t wa = ws & ~uintptr_t(3);
+                const uint32_t sh = uint32_t(ws & 3u);
+                uint32_t d[5];
+                #pragma unroll
+                for (int k = 0; k < 5; k++) {
+                    const uintptr_t da = wa + 4u * k;
+                    d[k] = (da + 4 > need0 && da < need1) ? *reinterpret_cast<const uint32_t*>(da) : 0u;
                 }
-                word[k >> 2] |= uint32_t(sp[r]) << (8 * (k & 3));
+                const uint32_t bm = (0xffffu >> (16 - uint32_t(hi - r0))) & ~((1u << uint32_t(lo - r0)) - 1u);
+                #pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t w = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+                    const uint32_t m = (((bm >> (4 * k)) & 0xfu) * 0x00204081u & 0x01010101u) * 0xffu;
+                    word[k] = (word[k] & ~m) | (w & m);
+                }
             }
+            if (int64_t(vend) >= r0 + 16 || v + 1 >= nv) break;
+            v++;
+            vb = coff[v];
+            vend = v + 1 < nv ? coff[v + 1] : total;
         }
         if (r0 >= 0 && r0 + 16 <= int64_t(total)) {
             *reinterpret_cast<uint4*>(dst) = make_uint4(word[0], word[1], word[2], word[3]);

@@ -186,10 +186,18 @@ __device__ uint32_t win_parse_spec(const uint8_t* stage, uint32_t woff, uint32_t
     bool converged = false;
     flags = 0;
     for (int round = 0; round < max_rounds; round++) {
-        // follow the chain lane to lane (uniform scalar loop)
-        ent = SNAP_INVALID;
+        // follow the chain lane to lane. Fast-forward: while each lane's exit lands in the next lane's
+        // region the entries are just the previous lanes' exits (one shuffle); from the first lane
+        // where that fails, a uniform scalar walk.
         flags = 0;
-        uint32_t k = L0, e = entry;
+        const uint32_t xk = L.x;
+        const bool ok = uint32_t(lane) >= L0 && xk != SNAP_INVALID && uint64_t(xk) < n && xk < W0 + SNAP_WIN &&
+                        (xk - W0) / SNAP_RB == uint32_t(lane) + 1;
+        const uint64_t notok = ~__ballot(ok) & (~0ull << L0);
+        const uint32_t la = notok ? uint32_t(__ffsll((unsigned long long)notok) - 1) : 63u;
+        const uint32_t xprev = __shfl_up(xk, 1, 64);
+        ent = uint32_t(lane) == L0 ? entry : ((uint32_t(lane) > L0 && uint32_t(lane) <= la) ? xprev : SNAP_INVALID);
+        uint32_t k = la, e = __builtin_amdgcn_readlane(ent, int(la));
         for (;;) {
             ent = uint32_t(lane) == k ? e : ent;
             const uint32_t x = __builtin_amdgcn_readlane(L.x, int(k));
@@ -200,6 +208,11 @@ __device__ uint32_t win_parse_spec(const uint8_t* stage, uint32_t woff, uint32_t
         }
         const bool need = ent != SNAP_INVALID && ent != L.c && !(ent > L.c && bit_get(L, ent - rs));
         if (!__any(need)) { converged = true; break; }
+#ifdef PF_STAMPS
+        if (lane == 0) { CSTAMP(7, 1); CSTAMP(8, __popcll(__ballot(need))); }
+#else
+        (void)__ballot(need);
+#endif
         if (need) lane_walk(stage, woff, W0, n, rs, re, ent, L);
     }
     if (!converged) flags = WIN_NOCONV;

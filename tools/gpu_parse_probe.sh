@@ -15,5 +15,6 @@ for line in open(sys.argv[1]):
     calls = w + d.get('ch_exact', 0)
     print(f"{line.split()[0]:16s} win {w:5d} idx_parse/w {d.get('idx_parse_cyc', 0) // w:7d} table/w {d.get('idx_table_cyc', 0) // w:6d} "
           + " ".join(f"{k[3:-4]}={d[k] // calls}" for k in d if k.startswith('wp_'))
+          + f" rounds/w {d.get('idx_rounds', 0) / w:.2f} rewalks/w {d.get('idx_rewalks', 0) / w:.1f}"
           + f" ch_max {d.get('ch_max_cyc', 0)} ch_exact {d.get('ch_exact', 0)}")
 PY

@@ -22,7 +22,7 @@ st.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
 buf = (C.c_ulonglong * 32)()
 dec = GpuDecoder(0)
 names = {0: "idx_windows", 1: "idx_parse_cyc", 2: "idx_noconv", 3: "idx_seq_store_cyc", 4: "idx_table_cyc",
-         5: "idx_windows_with_slow", 6: "idx_slow_lanes", 11: "ch_deep_walks", 12: "ch_deep_cyc",
+         5: "idx_windows_with_slow", 6: "idx_slow_lanes", 7: "idx_rounds", 8: "idx_rewalks", 11: "ch_deep_walks", 12: "ch_deep_cyc",
          13: "ch_rounds", 14: "ch_exact", 16: "ch_exact_cyc", 17: "ch_pages", 18: "ch_nw",
          19: "ch_total_cyc", 20: "ch_max_cyc", 21: "wp_decode_cyc", 22: "wp_exits_cyc", 23: "wp_chain_cyc",
          24: "wp_walk_cyc"}
