@@ -157,6 +157,14 @@ const char* pf_last_error(pf_ctx* ctx);           /* ctx may be NULL: thread-loc
 int pf_device_count(int* count);
 int pf_ctx_create(int device, pf_ctx** out);
 int pf_ctx_destroy(pf_ctx* ctx);
+/* A second context on peer's GPU that enqueues onto peer's HIP stream (own device buffers,
+ * results and completion event). Two such contexts let a reader plan and enqueue row group
+ * i+1 while row group i is still decoding (the same stream keeps them in order), and pf_wait
+ * on one waits only for its own decode. The shared stream lives until both are destroyed. */
+int pf_ctx_create_shared(pf_ctx* peer, pf_ctx** out);
+/* Per-stage timing events (pf_last_timing); on by default. Each event is a marker on the
+ * stream between kernels, so a throughput-critical caller turns them off. */
+int pf_ctx_set_timing(pf_ctx* ctx, int on);
 
 /* Pinned host memory (hipHostMalloc) for chunk bytes and outputs; Java wraps it with
  * MemorySegment.reinterpret. */

@@ -87,15 +87,33 @@ constexpr int64_t FLAT_BLK = 4096;         // pf_pages.hip FBLK   // h2d, snappy
 
 }  // namespace
 
-struct pf_ctx {
+// The HIP stream(s) of a context. Shared by contexts made with pf_ctx_create_shared (the stream
+// lives until the last of them is destroyed).
+struct Streams {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t exec_stream = nullptr;
+    ~Streams() {
+        (void)hipSetDevice(device);
+        if (exec_stream) { (void)hipStreamSynchronize(exec_stream); (void)hipStreamDestroy(exec_stream); }
+        if (stream) { (void)hipStreamSynchronize(stream); (void)hipStreamDestroy(stream); }
+    }
+};
+
+struct pf_ctx {
+    int device = 0;
+    std::shared_ptr<Streams> streams;
+    hipStream_t stream = nullptr;          // = streams->stream
     // PF_EXEC_STREAM=1: the Snappy executor runs on a low-priority stream of its own (event-ordered
     // with `stream`, which then gets the high priority), so the short kernels of another context
     // get CUs ahead of this context's executor waves as those retire.
     hipStream_t exec_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev[N_EVENTS] = {};
+    // recorded after the last operation of this context's decode: pf_wait waits for it, not for the
+    // stream, so a context sharing the stream can have the next batch enqueued behind this one
+    hipEvent_t ev_done = nullptr;
+    bool timing = true;                    // per-stage events (pf_last_timing); pf_ctx_set_timing
     std::string err;
     DevBuf d_in, d_scratch, d_out, d_bits, d_chars, d_meta, d_tokmap;
     DevBuf d_scan_in, d_scan;              // pf_scan_pages: host chunk bytes, tables
@@ -145,6 +163,13 @@ int fail(pf_ctx* ctx, int code, const std::string& msg) {
             return fail(ctx, PF_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// stage-timing event: only when the context has timing on (each record is a marker on the stream,
+// ~7 us between kernels on MI355X, so the product path leaves them off)
+#define EVREC(ctx, ev, st)                                 \
+    do {                                                   \
+        if ((ctx)->timing) HIPCHK(ctx, hipEventRecord(ev, st)); \
+    } while (0)
+
 int type_width(int ptype, int type_length) {
     switch (ptype) {
     case PF_BOOLEAN: return 1;
@@ -185,10 +210,10 @@ int enqueue_kernels(pf_ctx* ctx) {
     uint2* d_subsplits = reinterpret_cast<uint2*>(meta + ctx->off_subsplits);
 
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
-    HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
+    EVREC(ctx, ctx->ev[1], st);
     launch_snappy_parse(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent,
                         ctx->d_lane_out, d_splits, d_subsplits, d_fallback, st);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
+    EVREC(ctx, ctx->ev[2], st);
     if (ctx->exec_stream) {
         HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->exec_stream, ctx->ev_fork, 0));
@@ -200,36 +225,37 @@ int enqueue_kernels(pf_ctx* ctx) {
         launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_subsplits,
                            d_fallback, d_res, st);
     }
-    HIPCHK(ctx, hipEventRecord(ctx->ev[3], st));
+    EVREC(ctx, ctx->ev[3], st);
     BaJob* d_bajobs = reinterpret_cast<BaJob*>(meta + ctx->off_bajobs);
     const int2* d_batiles = reinterpret_cast<const int2*>(meta + ctx->off_batiles);
     const int n_ba = int(ctx->bajobs.size()), n_bt = int(ctx->ba_tiles.size());
     (void)d_dictbin;
     launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[4], st));
+    EVREC(ctx, ctx->ev[4], st);
     launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), d_res, st);
     launch_runs(d_chunks, d_pages, d_runs, int(ctx->l_runs.size()), d_res, st);
     launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st);
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[5], st));
+    EVREC(ctx, ctx->ev[5], st);
     launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st);
     launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
               d_res, st);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[6], st));
+    EVREC(ctx, ctx->ev[6], st);
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[7], st));
+    EVREC(ctx, ctx->ev[7], st);
     launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty());
-    HIPCHK(ctx, hipEventRecord(ctx->ev[8], st));
+    EVREC(ctx, ctx->ev[8], st);
     launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), d_res, st);
     launch_dba_chars(d_chunks, d_pages, d_dba, int(ctx->l_dba.size()), d_res, st);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[9], st));
+    EVREC(ctx, ctx->ev[9], st);
     HIPCHK(ctx, hipGetLastError());
     // results + device-written chunk fields (chars base) back to pinned host memory
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_res.p, meta + ctx->off_res, sizeof(DevChunkResult) * ctx->n_chunks,
                                hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(ctx->h_res.p) + align_up(sizeof(DevChunkResult) * ctx->n_chunks, 256),
                                d_chunks, sizeof(DevChunk) * ctx->n_chunks, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipEventRecord(ctx->ev_done, st));
     return PF_OK;
 }
 
@@ -356,20 +382,45 @@ int pf_device_count(int* count) {
 }
 
 namespace {
-int ctx_init(pf_ctx* ctx) {
+int ctx_init(pf_ctx* ctx, pf_ctx* peer) {
     HIPCHK(nullptr, hipSetDevice(ctx->device));
-    const char* es = std::getenv("PF_EXEC_STREAM");
-    if (es && es[0] && es[0] != '0') {
-        int least = 0, greatest = 0;
-        HIPCHK(nullptr, hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIPCHK(nullptr, hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, greatest));
-        HIPCHK(nullptr, hipStreamCreateWithPriority(&ctx->exec_stream, hipStreamNonBlocking, least));
+    if (peer) {
+        ctx->streams = peer->streams;
+    } else {
+        ctx->streams = std::make_shared<Streams>();
+        ctx->streams->device = ctx->device;
+        const char* es = std::getenv("PF_EXEC_STREAM");
+        if (es && es[0] && es[0] != '0') {
+            int least = 0, greatest = 0;
+            HIPCHK(nullptr, hipDeviceGetStreamPriorityRange(&least, &greatest));
+            HIPCHK(nullptr, hipStreamCreateWithPriority(&ctx->streams->stream, hipStreamNonBlocking, greatest));
+            HIPCHK(nullptr, hipStreamCreateWithPriority(&ctx->streams->exec_stream, hipStreamNonBlocking, least));
+        } else {
+            HIPCHK(nullptr, hipStreamCreateWithFlags(&ctx->streams->stream, hipStreamNonBlocking));
+        }
+    }
+    ctx->stream = ctx->streams->stream;
+    ctx->exec_stream = ctx->streams->exec_stream;
+    if (ctx->exec_stream) {
         HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-    } else {
-        HIPCHK(nullptr, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     }
+    HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
     for (auto& e : ctx->ev) HIPCHK(nullptr, hipEventCreate(&e));
+    return PF_OK;
+}
+
+int ctx_create(int device, pf_ctx* peer, pf_ctx** out) {
+    pf_ctx* ctx = new pf_ctx();
+    ctx->device = device;
+    const int rc = ctx_init(ctx, peer);
+    if (rc != PF_OK) {   // release whatever streams / events were created before the failure
+        const std::string msg = g_err;
+        pf_ctx_destroy(ctx);
+        g_err = msg;
+        return rc;
+    }
+    *out = ctx;
     return PF_OK;
 }
 }  // namespace
@@ -380,23 +431,27 @@ int pf_ctx_create(int device, pf_ctx** out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
         return fail(nullptr, PF_ERR_INVALID_ARG, "no such HIP device");
-    pf_ctx* ctx = new pf_ctx();
-    ctx->device = device;
-    const int rc = ctx_init(ctx);
-    if (rc != PF_OK) {   // release whatever streams / events were created before the failure
-        const std::string msg = g_err;
-        pf_ctx_destroy(ctx);
-        g_err = msg;
-        return rc;
-    }
-    *out = ctx;
+    return ctx_create(device, nullptr, out);
+}
+
+int pf_ctx_create_shared(pf_ctx* peer, pf_ctx** out) {
+    if (!out || !peer) return fail(nullptr, PF_ERR_INVALID_ARG, "null arg");
+    *out = nullptr;
+    return ctx_create(peer->device, peer, out);
+}
+
+int pf_ctx_set_timing(pf_ctx* ctx, int on) {
+    if (!ctx) return fail(nullptr, PF_ERR_INVALID_ARG, "null ctx");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "decode in flight");
+    ctx->timing = on != 0;
+    ctx->timing_valid = false;
     return PF_OK;
 }
 
 int pf_ctx_destroy(pf_ctx* ctx) {
     if (!ctx) return PF_OK;
     (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);   // this context's work and any peer's ahead of it
     if (ctx->exec_stream) (void)hipStreamSynchronize(ctx->exec_stream);
     for (DevBuf* b : {&ctx->d_in, &ctx->d_scratch, &ctx->d_out, &ctx->d_bits, &ctx->d_chars, &ctx->d_meta, &ctx->d_tokmap,
                       &ctx->d_scan_in, &ctx->d_scan})
@@ -406,8 +461,8 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-    if (ctx->exec_stream) (void)hipStreamDestroy(ctx->exec_stream);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
+    ctx->streams.reset();   // destroys the stream(s) when no other context shares them
     delete ctx;
     return PF_OK;
 }
@@ -468,7 +523,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->timing_valid = false;
 
     // ---- input bytes on device ----
-    HIPCHK(ctx, hipEventRecord(ctx->ev[0], st));
+    EVREC(ctx, ctx->ev[0], st);
     const uint8_t* d_bytes = bytes;
     if (!bytes_on_device && n_bytes) {
         HIPCHK(ctx, ctx->d_in.ensure(n_bytes));
@@ -820,7 +875,7 @@ int pf_wait(pf_ctx* ctx) {
     if (!ctx->pending) return fail(ctx, PF_ERR_STATE, "nothing to wait for");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     for (;;) {
-        hipError_t e = hipStreamSynchronize(ctx->stream);
+        hipError_t e = hipEventSynchronize(ctx->ev_done);
         if (e != hipSuccess) { ctx->pending = false; return fail(ctx, PF_ERR_HIP, std::string("decode: ") + hipGetErrorString(e)); }
         const DevChunkResult* r = static_cast<const DevChunkResult*>(ctx->h_res.p);
         const DevChunk* dc = reinterpret_cast<const DevChunk*>(static_cast<uint8_t*>(ctx->h_res.p) +
@@ -1154,6 +1209,7 @@ int pf_debug_snappy_fallback(pf_ctx* ctx, int* out, int n_jobs) {
 
 int pf_last_timing(pf_ctx* ctx, float* stage_ms, int n_stages, int* n_written) {
     if (!ctx || !stage_ms || n_stages < 0) return fail(ctx, PF_ERR_INVALID_ARG, "bad arg");
+    if (!ctx->timing) return fail(ctx, PF_ERR_STATE, "stage timing is off (pf_ctx_set_timing)");
     if (!ctx->timing_valid) return fail(ctx, PF_ERR_STATE, "no finished decode");
     int k = 0;
     for (int i = 0; i + 1 < N_EVENTS && k < n_stages; i++, k++) {

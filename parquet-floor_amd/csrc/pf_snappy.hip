@@ -11,26 +11,24 @@
 //   11 copy     (len (tag>>2)+1, 32-bit LE offset)
 // Copies may overlap their own output (offset < length).
 //
-// Design (one 64-lane wave per page):
-//  * the output window lives in a 64 KiB LDS ring; byte j of a copy reads position
-//    op - off + (j mod off), which always precedes op, so all 64 lanes can copy one token in a
-//    single read-then-write step even when it overlaps itself;
-//  * copies whose offset reaches past the ring read the already-flushed HBM output (a wave's
-//    own stores are ordered before its later loads);
-//  * tokens are parsed in batches into LDS and executed in order; finished output is flushed
-//    ring -> HBM with 16-byte coalesced stores.
+// Design (one 64-lane wave per page, no output staging):
+//  * tokens are parsed in batches of 256 by lane 0 into LDS (4 KiB), then executed in order by
+//    the wave directly in the HBM output: literals lane-parallel from the input, copies by 64
+//    lanes at once (byte j of a copy reads position out - off + (j mod off), which always precedes
+//    out, so a copy never reads its own bytes even when it overlaps itself);
+//  * a workgroup barrier (release/acquire at workgroup scope) between tokens makes every lane's
+//    stores visible to the next token's loads.
 // This serial kernel is the FALLBACK: it only runs for pages the block-parallel path
-// (pf_snappy_par.hip) could not index (corrupt streams — it produces the precise error status).
+// (pf_snappy_par.hip) could not decode (corrupt streams — it produces the precise error status).
+// It is launched on every batch and nearly always finds nothing to do, so it holds almost no LDS:
+// a launch that needs a large LDS allocation waits for CUs the other contexts' kernels occupy.
 #include <hip/hip_runtime.h>
 
 #include "pf_snappy_par.h"
 
 namespace pf {
 
-constexpr uint32_t RING = 65536;
-constexpr uint32_t RMASK = RING - 1;
 constexpr int TOK_BATCH = 256;
-constexpr uint32_t FLUSH_AT = 16384;
 
 struct Token {
     uint32_t src;    // literal: input byte position; copy: offset
@@ -39,25 +37,8 @@ struct Token {
     uint32_t lit;
 };
 
-__device__ __forceinline__ void flush(const uint8_t* ring, uint8_t* dst, uint32_t from, uint32_t to) {
-    // bytes [from, to) of the output are final in the ring; store them to HBM
-    const int lane = threadIdx.x;
-    // align the bulk to 16 B in the destination
-    uint32_t head = min(to, (from + 15u) & ~15u);
-    for (uint32_t q = from + lane; q < head; q += WAVE) dst[q] = ring[q & RMASK];
-    for (uint32_t q = head + uint32_t(lane) * 16u; q + 16u <= to; q += WAVE * 16u) {
-        uint4 v;
-        uint8_t* b = reinterpret_cast<uint8_t*>(&v);
-        #pragma unroll
-        for (int k = 0; k < 16; k++) b[k] = ring[(q + k) & RMASK];
-        *reinterpret_cast<uint4*>(dst + q) = v;
-    }
-    uint32_t tail_start = head + ((to > head ? to - head : 0) & ~15u);
-    for (uint32_t q = tail_start + lane; q < to; q += WAVE) dst[q] = ring[q & RMASK];
-}
-
 // One page, serially, by one wave (LDS passed in by the kernel).
-__device__ void serial_page(const SnappyJob& job, DevChunkResult* res, uint8_t* ring, Token* toks, int& ntok_s,
+__device__ void serial_page(const SnappyJob& job, DevChunkResult* res, Token* toks, int& ntok_s,
                             int& err_s, uint32_t& ip_s) {
     const uint8_t* in = job.src;
     const uint64_t n = job.src_len;
@@ -74,7 +55,7 @@ __device__ void serial_page(const SnappyJob& job, DevChunkResult* res, uint8_t* 
     if (lane == 0) { ip_s = uint32_t(pos); err_s = 0; }
     __syncthreads();
 
-    uint32_t op = 0, flushed = 0;
+    uint32_t op = 0;
     for (;;) {
         // ---- parse a batch of tokens (lane 0, serial) ----
         if (lane == 0) {
@@ -129,43 +110,17 @@ __device__ void serial_page(const SnappyJob& job, DevChunkResult* res, uint8_t* 
         __syncthreads();
         const int nt = ntok_s;
         if (err_s) break;
-        // ---- execute tokens in order ----
+        // ---- execute tokens in order, in the HBM output ----
         for (int i = 0; i < nt; i++) {
-            Token t = toks[i];
+            const Token t = toks[i];
             if (t.lit) {
-                uint32_t done = 0;
-                while (done < t.len) {
-                    uint32_t chunk = min(t.len - done, 8192u);
-                    if (t.out + done + chunk - flushed > RING) {   // keep unflushed bytes in the ring
-                        __syncthreads();
-                        flush(ring, dst, flushed, t.out + done);
-                        flushed = t.out + done;
-                        __syncthreads();
-                    }
-                    for (uint32_t j = lane; j < chunk; j += WAVE)
-                        ring[(t.out + done + j) & RMASK] = in[t.src + done + j];
-                    done += chunk;
-                }
-            } else {
-                uint32_t j = lane;
-                uint8_t v = 0;
-                if (j < t.len) {
-                    uint32_t s = t.out - t.src + (j % t.src);
-                    v = (t.src <= RING - 64) ? ring[s & RMASK] : dst[s];
-                }
-                __syncthreads();   // single wave: orders the reads before the writes
-                if (j < t.len) ring[(t.out + j) & RMASK] = v;
+                for (uint32_t j = lane; j < t.len; j += WAVE) dst[t.out + j] = in[t.src + j];
+            } else if (uint32_t(lane) < t.len) {
+                dst[t.out + lane] = dst[t.out - t.src + (uint32_t(lane) % t.src)];
             }
-            uint32_t end = t.out + t.len;
-            if (end - flushed >= FLUSH_AT) {
-                __syncthreads();
-                flush(ring, dst, flushed, end);
-                flushed = end;
-                __syncthreads();
-            }
-            op = end;
+            __syncthreads();   // this token's bytes are visible to the next token's reads
+            op = t.out + t.len;
         }
-        __syncthreads();
         if (nt < TOK_BATCH) break;   // input exhausted
     }
     __syncthreads();
@@ -173,26 +128,22 @@ __device__ void serial_page(const SnappyJob& job, DevChunkResult* res, uint8_t* 
         if (lane == 0) set_status(res, job.chunk, ST_CORRUPT, job.page);
         return;
     }
-    flush(ring, dst, flushed, op);
 }
 
 
 
-// Grid-stride over the jobs with a small grid: nearly every page was decoded by the parallel path,
-// and a block per job would hold 70 KB of LDS each just to read its flag, waiting for CUs that the
-// other context's executor occupies (a no-op launch measured up to 1.1 ms with two streams).
+// Grid-stride over the jobs with a small grid: nearly every page was decoded by the parallel path.
 constexpr int SERIAL_GRID = 64;
 
 __global__ __launch_bounds__(64) void k_snappy_serial(const SnappyJob* __restrict__ jobs, const int* __restrict__ fallback,
                                                       int n_jobs, DevChunkResult* res) {
-    __shared__ uint8_t ring[RING];
     __shared__ Token toks[TOK_BATCH];
     __shared__ int ntok_s, err_s;
     __shared__ uint32_t ip_s;
     for (int j = blockIdx.x; j < n_jobs; j += gridDim.x) {
         if (fallback[j] != FB_SERIAL) continue;   // the block-parallel path decoded this page
         const SnappyJob job = jobs[j];
-        serial_page(job, res, ring, toks, ntok_s, err_s, ip_s);
+        serial_page(job, res, toks, ntok_s, err_s, ip_s);
         __syncthreads();
     }
 }

@@ -94,6 +94,8 @@ def lib():
         "pf_device_count": ([C.POINTER(C.c_int)], C.c_int),
         "pf_ctx_create": ([i32, C.POINTER(vp)], C.c_int),
         "pf_ctx_destroy": ([vp], C.c_int),
+        "pf_ctx_create_shared": ([vp, C.POINTER(vp)], C.c_int),
+        "pf_ctx_set_timing": ([vp, i32], C.c_int),
         "pf_host_alloc": ([vp, sz, C.POINTER(vp)], C.c_int),
         "pf_host_free": ([vp, vp], C.c_int),
         "pf_device_alloc": ([vp, sz, C.POINTER(vp)], C.c_int),

@@ -137,10 +137,16 @@ class PinnedBuffer:
 class GpuDecoder:
     """One pf_ctx = one GPU + one HIP stream."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, share=None):
+        """share: another GpuDecoder whose HIP stream this context enqueues onto
+        (pf_ctx_create_shared: pipelined decodes of consecutive batches)."""
         L = lib()
         self.h = C.c_void_p()
-        check(L.pf_ctx_create(device, C.byref(self.h)), None, f"pf_ctx_create({device})")
+        if share is not None:
+            check(L.pf_ctx_create_shared(share.h, C.byref(self.h)), None, "pf_ctx_create_shared")
+            device = share.device
+        else:
+            check(L.pf_ctx_create(device, C.byref(self.h)), None, f"pf_ctx_create({device})")
         self.device = device
         self._staging = None
         self.n_chunks = 0
@@ -215,6 +221,9 @@ class GpuDecoder:
             pg = [{f: getattr(pages[i * page_cap + k], f) for f, _ in PageDesc._fields_} for k in range(r.n_pages)]
             out.append((r.status, r.err_page, r.crc_pages, pg))
         return rc, out
+
+    def set_timing(self, on):
+        check(lib().pf_ctx_set_timing(self.h, 1 if on else 0), self.h, "pf_ctx_set_timing")
 
     def timing(self):
         buf = (C.c_float * 16)()

@@ -196,3 +196,62 @@ def test_gpu_multiblock_pages_match_oracle(decoder, oracle, tmp_path, nulls):
                 g = got[(rg, c)]
                 assert g["status"] == 0, (rg, c, got["_error"])
                 assert_chunk_equal(g, of.decode(rg, c), f"big rg{rg} c{c} nulls={nulls}")
+
+
+def test_shared_stream_contexts_pipelined(oracle):
+    """pf_ctx_create_shared: two contexts on one HIP stream, row group i+1 enqueued on one while
+    row group i still decodes on the other (the bench's pipelined steps, a reader's prefetch).
+    Every row group decoded this way is bit-exact vs the oracle; pf_wait on one context returns
+    its own results; timing off gives PF_ERR_STATE from pf_last_timing; destroying the first
+    context leaves the shared stream usable by the second."""
+    from pfloor import _native
+    from pfloor.decoder import GpuDecoder, ParquetFile, PinnedBuffer
+    path = os.path.join(GOLDEN, "c2_lineitem.parquet")
+    a = GpuDecoder(0)
+    b = GpuDecoder(share=a)
+    pair = (a, b)
+    with ParquetFile(path) as pf, oracle.open(path) as of:
+        cols = list(range(pf.num_columns))
+        seq = [rg for _ in range(3) for rg in range(pf.num_row_groups)]
+        bufs = []
+        for rg in range(pf.num_row_groups):
+            items, total = pf.plan([rg], cols)
+            buf = PinnedBuffer(a.h, max(total, 1))
+            descs = []
+            for _rg, col, s, n, off in items:
+                if n:
+                    pf.read_into(s, n, buf.ptr.value + off)
+                descs.append(pf.chunk_desc(_rg, col, off))
+            bufs.append((items, descs, buf, max(total, 1)))
+        for d in pair:
+            d.set_timing(False)
+
+        def check(d, rg):
+            items = bufs[rg][0]
+            for i, (_rg, col, *_r) in enumerate(items):
+                c = pf.columns[col]
+                g = d.fetch(i, c.physical_type, c.max_def, c.max_rep)
+                assert g["status"] == 0
+                assert_chunk_equal(g, of.decode(_rg, col), f"pipelined rg{_rg} c{col}")
+
+        for k, rg in enumerate(seq):
+            items, descs, buf, nb = bufs[rg]
+            pair[k % 2].decode(descs, buf.ptr.value, nb)
+            if k > 0:
+                d = pair[(k - 1) % 2]
+                assert d.wait() == 0, d.error()
+                check(d, seq[k - 1])
+        d = pair[(len(seq) - 1) % 2]
+        assert d.wait() == 0, d.error()
+        check(d, seq[-1])
+        with pytest.raises(_native.PfError):
+            a.timing()
+        a.set_timing(True)
+        a.close()   # b still owns the stream
+        items, descs, buf, nb = bufs[0]
+        b.decode(descs, buf.ptr.value, nb)
+        assert b.wait() == 0, b.error()
+        check(b, 0)
+        for *_x, buf, _n in bufs:
+            buf.free()
+    b.close()
