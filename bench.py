@@ -532,6 +532,7 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--no-write", action="store_true", help="skip the write-path leg")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="timed steps decode -> wait per batch on one context per stream (A/B of the pipelined default)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -700,6 +701,14 @@ def main():
         except Exception as e:
             e2e = {"error": repr(e)}
 
+    # ---- write path: row group 0 re-encoded on the GPU and read back ----
+    write = None
+    if not args.no_write and rank == 0:
+        try:
+            write = measure_write(path, pf, decs[0])
+        except Exception as e:
+            write = {"error": repr(e)}
+
     w = WORKLOADS[args.workload]
     if args.workload == "sf1":
         wl = (f"lineitem SF1 x{world} ({w['rows']} rows x {world}, 16 cols, {pf.num_row_groups * world} row groups of 1Mi rows), "
@@ -753,6 +762,8 @@ def main():
         out["parity"] = parity
     if e2e is not None:
         out["e2e"] = e2e
+    if write is not None:
+        out["write"] = write
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baselines(path, pf)
@@ -770,6 +781,67 @@ def main():
         log("[bench] PARITY FAILURE")
         return 3
     return 0
+
+
+def measure_write(path, pf, dec, passes=3):
+    """Write path (ParquetWriter.java:61-165 settings): row group 0 of the input, decoded on the
+    GPU to host columns, is written WRITE passes times as a one-row-group file by pfloor.writer
+    (per column: H2D, dictionary encode, pages, Snappy on the GPU, headers + file on the host);
+    the best pass is reported as input bytes / wall time. The last file is then decoded on the GPU
+    and compared bit-exactly with the source columns."""
+    import tempfile
+    from pfloor import writer as W
+    from pfloor.decoder import decode_file
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden_util import assert_chunk_equal
+    src = decode_file(path, row_groups=[0], decoder=dec)
+    if src["_status"] != 0:
+        raise RuntimeError(src["_error"])
+    n = pf.row_group_rows(0)
+    fields, cols, in_bytes = [], {}, 0
+    dt = {1: np.int32, 2: np.int64, 4: np.float32, 5: np.float64, 0: np.uint8}
+    for c, col in enumerate(pf.columns):
+        g = src[(0, c)]
+        name = ".".join(col.path)
+        f = W.Field(name, col.physical_type, col.max_def > 0, col.physical_type == 6)
+        fields.append(f)
+        if col.physical_type == 6:
+            d = (g["offsets"], g["chars"])
+            in_bytes += g["offsets"].nbytes + g["chars"].nbytes
+        else:
+            d = g["values"].view(dt[col.physical_type])
+            in_bytes += d.nbytes
+        if col.max_def > 0:
+            d = (*d, g["validity"]) if isinstance(d, tuple) else (d, g["validity"])
+            in_bytes += g["validity"].nbytes
+        cols[name] = d
+    schema = W.MessageType("lineitem", *fields)
+    out_path = os.path.join(tempfile.gettempdir(), f"pfloor_write_{os.getpid()}.parquet")
+    times, encs = [], None
+    for _ in range(passes):
+        t0 = time.perf_counter()
+        wr = W.ParquetWriter(schema, out_path, None, decoder=dec)
+        wr.write_columns(cols, n)
+        wr.close()
+        times.append(time.perf_counter() - t0)
+        encs = list(wr.last_chunks)
+    size = os.path.getsize(out_path)
+    back = decode_file(out_path, decoder=dec)
+    bad = []
+    for c in range(len(fields)):
+        try:
+            assert_chunk_equal(back[(0, c)], src[(0, c)], f"write c{c}")
+        except AssertionError as e:
+            bad.append(str(e)[:160])
+    os.remove(out_path)
+    best = min(times)
+    return {"value": round(in_bytes / best / 1e9, 3), "unit": "GB/s of column bytes in (host) -> Parquet file",
+            "ms_per_row_group": round(best * 1e3, 2), "rows": n, "columns": len(fields), "input_bytes": in_bytes,
+            "file_bytes": size, "dictionary_columns": sum(1 for e in encs if e[1] == 8),
+            "plain_fallbacks": sum(1 for e in encs if e[2] in (1, 2)),
+            "parity": {"chunks": len(fields), "bit_exact": not bad, "mismatches": bad[:3],
+                       "against": "the source columns, read back by the GPU read path"},
+            "passes": passes}
 
 
 def measure_e2e(decs, batches, pf, st_all):

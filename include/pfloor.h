@@ -270,6 +270,64 @@ int pf_file_chunk_desc(pf_file* f, int row_group, int column, uint64_t chunk_off
 /* Read raw bytes of the file (host). */
 int pf_file_read(pf_file* f, uint64_t offset, uint64_t size, void* dst);
 const char* pf_file_created_by(pf_file* f);
+
+/* ---- write path: the reference's ParquetWriter (ParquetWriter.java:61-165: SNAPPY,
+ *      WriterVersion.PARQUET_2_0, parquet-mr 1.12.2 defaults) with the column encoding on the
+ *      GPU: dictionary encode (entries in first-occurrence order, like parquet-mr's
+ *      DictionaryValuesWriter), RLE/bit-packed hybrid ids, PLAIN values, Snappy compression of
+ *      every page. Flat schemas of the types the reference writes (ParquetWriter.java:143-157):
+ *      BOOLEAN, INT32, INT64, FLOAT, DOUBLE, BYTE_ARRAY (UTF8). ---- */
+typedef struct pf_encode_column {
+    int32_t  physical_type;       /* PF_BOOLEAN, PF_INT32, PF_INT64, PF_FLOAT, PF_DOUBLE, PF_BYTE_ARRAY */
+    int32_t  max_def;             /* 0 = REQUIRED, 1 = OPTIONAL */
+    int64_t  num_rows;
+    const void*    values;        /* fixed width, row-indexed (null rows ignored); BOOLEAN: one byte per row */
+    const uint8_t* validity;      /* LSB-first, bit = present; NULL = all present (max_def 1) */
+    const int32_t* offsets;       /* BYTE_ARRAY: num_rows + 1 (null rows: empty) */
+    const uint8_t* chars;         /* BYTE_ARRAY */
+    int64_t  chars_len;
+    int32_t  dictionary;          /* 1: dictionary-encode (PLAIN above dict_page_limit or on a hash collision) */
+    int32_t  page_rows;           /* rows per data page; 0 = 20000 (parquet-mr page.row.count.limit) */
+    int32_t  dict_page_limit;     /* dictionary page bytes; 0 = 1 MiB (parquet.dictionary.page.size) */
+    int32_t  codec;               /* PF_CODEC_SNAPPY (the reference's) or PF_CODEC_UNCOMPRESSED */
+} pf_encode_column;
+
+typedef struct pf_encoded_chunk {
+    const uint8_t* bytes;         /* page headers + bodies as they appear in the file (owned by the ctx,
+                                     valid until its next pf_encode_chunk) */
+    int64_t  size;                /* = ColumnMetaData.total_compressed_size */
+    int64_t  total_uncompressed_size;
+    int64_t  num_values;
+    int64_t  dictionary_page_offset;   /* relative to bytes, -1 if none */
+    int64_t  data_page_offset;         /* relative to bytes */
+    int32_t  n_data_pages;
+    int32_t  dict_entries;        /* 0 when not dictionary-encoded */
+    int32_t  data_encoding;       /* PF_ENC_RLE_DICTIONARY or PF_ENC_PLAIN */
+    int32_t  fallback;            /* 0; 1 dictionary above the limit; 2 hash collision; 3 type (BOOLEAN) */
+    int32_t  codec;               /* ColumnMetaData.codec */
+} pf_encoded_chunk;
+
+/* Encode one column chunk on the context's GPU. Inputs are host memory (copied) unless
+ * on_device != 0. Synchronous. */
+int pf_encode_chunk(pf_ctx* ctx, const pf_encode_column* col, int on_device, pf_encoded_chunk* out);
+/* Snappy-compress one buffer on the GPU (64 KiB blocks, one wave each). Host buffers, synchronous;
+ * *out_len = compressed length (cap >= 32 + n + n / 6 always suffices). */
+int pf_snappy_compress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
+
+/* File writer (host): "PAR1", row groups of encoded chunks, Thrift compact FileMetaData footer. */
+typedef struct pf_writer pf_writer;
+typedef struct pf_write_field {
+    const char* name;
+    int32_t physical_type;
+    int32_t optional;             /* 1 = OPTIONAL, 0 = REQUIRED */
+    int32_t utf8;                 /* BYTE_ARRAY: STRING logical type (the only BINARY the reference writes) */
+} pf_write_field;
+int pf_writer_open(const char* path, const pf_write_field* fields, int n_fields, pf_writer** out);
+/* Append the chunk of field `field` (fields in schema order) to the current row group. */
+int pf_writer_add_chunk(pf_writer* w, int field, const pf_encoded_chunk* chunk);
+int pf_writer_end_row_group(pf_writer* w, int64_t num_rows);
+int pf_writer_close(pf_writer* w);   /* footer; frees w (also on error) */
+const char* pf_writer_last_error(void);
 const char* pf_file_last_error(void);            /* thread-local message of the last pf_file_* error */
 
 #ifdef __cplusplus

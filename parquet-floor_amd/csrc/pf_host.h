@@ -50,4 +50,12 @@ struct FileMeta {
     static void walk_pages(const uint8_t* chunk, size_t size, const ChunkMeta& m, std::vector<pf_page_desc>& out);
 };
 
+// One page header of the write path (pf_write.cpp serialises it as a Thrift compact PageHeader).
+struct PageHeaderOut {
+    int32_t page_type = 0, uncompressed_size = 0, compressed_size = 0;
+    int32_t num_values = 0, num_nulls = 0, num_rows = 0, encoding = 0, def_bytes = 0;
+    bool is_compressed = true;
+};
+void write_page_header(std::vector<uint8_t>& out, const PageHeaderOut& h);
+
 }  // namespace pf

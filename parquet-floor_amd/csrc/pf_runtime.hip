@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "pf_encode.h"
 #include "pf_host.h"
 #include "pf_snappy_par.h"
 #include "pfloor.h"
@@ -117,6 +118,8 @@ struct pf_ctx {
     std::string err;
     DevBuf d_in, d_scratch, d_out, d_bits, d_chars, d_meta, d_tokmap;
     DevBuf d_scan_in, d_scan;              // pf_scan_pages: host chunk bytes, tables
+    DevBuf d_enc, d_enc_sec, d_enc_out;    // pf_encode_chunk / pf_snappy_compress: work arena, values sections, slots
+    std::vector<uint8_t> h_enc;            // the last encoded chunk (headers + bodies)
     HostBuf h_meta, h_res;
     // last batch
     int n_chunks = 0;
@@ -366,6 +369,315 @@ int upload_meta(pf_ctx* ctx) {
 
 }  // namespace
 
+
+// ---------------------------------------------------------------- write path (pf_encode.hip)
+namespace {
+size_t uvarint_len(uint64_t v) { size_t k = 1; while (v >= 0x80) { v >>= 7; k++; } return k; }
+void put_uvarint(std::vector<uint8_t>& o, uint64_t v) {
+    while (v >= 0x80) { o.push_back(uint8_t(v | 0x80)); v >>= 7; }
+    o.push_back(uint8_t(v));
+}
+
+// Snappy-compress `sections` (device, each [off, off + len) of `base`) into 64 KiB-block slots;
+// returns per section the host stream (varint length + block outputs) in `streams`.
+int compress_sections(pf_ctx* ctx, const uint8_t* base, const std::vector<std::pair<uint64_t, uint64_t>>& sections,
+                      std::vector<std::vector<uint8_t>>& streams) {
+    hipStream_t st = ctx->stream;
+    std::vector<SnapCJob> jobs;
+    std::vector<std::pair<size_t, size_t>> range(sections.size());   // jobs of each section
+    for (size_t i = 0; i < sections.size(); i++) {
+        range[i].first = jobs.size();
+        for (uint64_t o = 0; o < sections[i].second; o += SC_BLOCK) {
+            SnapCJob j{};
+            j.src = base + sections[i].first + o;
+            j.len = uint32_t(std::min<uint64_t>(SC_BLOCK, sections[i].second - o));
+            jobs.push_back(j);
+        }
+        range[i].second = jobs.size();
+    }
+    const size_t nj = jobs.size();
+    size_t m = 0;
+    auto take = [](size_t& cur, size_t sz) { size_t o = align_up(cur, 256); cur = o + sz; return o; };
+    const size_t o_jobs = take(m, sizeof(SnapCJob) * std::max<size_t>(nj, 1));
+    const size_t o_len = take(m, 4 * std::max<size_t>(nj, 1));
+    const size_t o_slots = take(m, size_t(SC_SLOT) * std::max<size_t>(nj, 1));
+    HIPCHK(ctx, ctx->d_enc_out.ensure(m));
+    uint8_t* d = static_cast<uint8_t*>(ctx->d_enc_out.p);
+    for (size_t k = 0; k < nj; k++) jobs[k].dst = d + o_slots + k * SC_SLOT;
+    std::vector<uint32_t> lens(nj);
+    std::vector<uint8_t> slots(nj * size_t(SC_SLOT));
+    if (nj) {
+        HIPCHK(ctx, hipMemcpyAsync(d + o_jobs, jobs.data(), sizeof(SnapCJob) * nj, hipMemcpyHostToDevice, st));
+        launch_snappy_compress(reinterpret_cast<const SnapCJob*>(d + o_jobs), int(nj), reinterpret_cast<uint32_t*>(d + o_len), st);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipMemcpyAsync(lens.data(), d + o_len, 4 * nj, hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipMemcpyAsync(slots.data(), d + o_slots, slots.size(), hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    streams.assign(sections.size(), {});
+    for (size_t i = 0; i < sections.size(); i++) {
+        std::vector<uint8_t>& o = streams[i];
+        put_uvarint(o, sections[i].second);
+        for (size_t k = range[i].first; k < range[i].second; k++) {
+            if (lens[k] > SC_SLOT) return fail(ctx, PF_ERR_HIP, "snappy compress: block overflow");
+            const uint8_t* b = slots.data() + k * size_t(SC_SLOT);
+            o.insert(o.end(), b, b + lens[k]);
+        }
+    }
+    return PF_OK;
+}
+}  // namespace
+
+extern "C" int pf_snappy_compress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    if (!ctx || (!src && n) || !out_len) return fail(ctx, PF_ERR_INVALID_ARG, "null arg");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "previous decode not waited for");
+    if (n > 0xffffffffull) return fail(ctx, PF_ERR_INVALID_ARG, "snappy: buffer too large");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (ctx->copies_pending) HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->copies_pending = false;
+    HIPCHK(ctx, ctx->d_enc.ensure(std::max<size_t>(n, 1)));
+    if (n) HIPCHK(ctx, hipMemcpyAsync(ctx->d_enc.p, src, n, hipMemcpyHostToDevice, ctx->stream));
+    std::vector<std::vector<uint8_t>> streams;
+    const int rc = compress_sections(ctx, static_cast<const uint8_t*>(ctx->d_enc.p), {{0, n}}, streams);
+    if (rc) return rc;
+    *out_len = streams[0].size();
+    if (streams[0].size() > cap) return fail(ctx, PF_ERR_CAPACITY, "snappy: destination too small");
+    std::memcpy(dst, streams[0].data(), streams[0].size());
+    return PF_OK;
+}
+
+extern "C" int pf_encode_chunk(pf_ctx* ctx, const pf_encode_column* col, int on_device, pf_encoded_chunk* out) {
+    if (!ctx || !col || !out) return fail(ctx, PF_ERR_INVALID_ARG, "null arg");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "previous decode not waited for");
+    const int pt = col->physical_type;
+    if (pt != PF_BOOLEAN && pt != PF_INT32 && pt != PF_INT64 && pt != PF_FLOAT && pt != PF_DOUBLE && pt != PF_BYTE_ARRAY)
+        return fail(ctx, PF_ERR_UNSUPPORTED_TYPE, "encode: unsupported physical type");
+    const int64_t n = col->num_rows;
+    if (n < 0 || n > 0x7ffffff0 || (col->max_def != 0 && col->max_def != 1)) return fail(ctx, PF_ERR_INVALID_ARG, "encode: bad shape");
+    if (col->codec != PF_CODEC_SNAPPY && col->codec != PF_CODEC_UNCOMPRESSED)
+        return fail(ctx, PF_ERR_UNSUPPORTED_CODEC, "encode: codec must be SNAPPY or UNCOMPRESSED");
+    const bool str = pt == PF_BYTE_ARRAY;
+    if (n > 0 && (str ? (!col->offsets || (!col->chars && col->chars_len > 0) || col->chars_len < 0 || col->chars_len > 0x7fffffff)
+                      : !col->values))
+        return fail(ctx, PF_ERR_INVALID_ARG, "encode: missing input arrays");
+    const int w = pt == PF_BOOLEAN ? 1 : type_width(pt, 0);
+    int64_t page_rows = col->page_rows > 0 ? col->page_rows : 20000;
+    page_rows = (page_rows + 7) / 8 * 8;   // definition levels of a page start on a validity byte
+    const int64_t dict_limit = col->dict_page_limit > 0 ? col->dict_page_limit : (1 << 20);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    if (ctx->copies_pending) HIPCHK(ctx, hipStreamSynchronize(st));
+    ctx->copies_pending = false;
+
+    // host copies of validity / offsets (page plan, definition levels)
+    const size_t vbytes = size_t((n + 7) / 8);
+    std::vector<uint8_t> hval;
+    std::vector<int32_t> hoff;
+    const bool has_val = col->max_def == 1 && col->validity;
+    if (has_val) {
+        hval.resize(vbytes);
+        if (on_device) HIPCHK(ctx, hipMemcpy(hval.data(), col->validity, vbytes, hipMemcpyDeviceToHost));
+        else std::memcpy(hval.data(), col->validity, vbytes);
+    }
+    if (str && n > 0) {
+        hoff.resize(size_t(n) + 1);
+        if (on_device) HIPCHK(ctx, hipMemcpy(hoff.data(), col->offsets, 4 * (size_t(n) + 1), hipMemcpyDeviceToHost));
+        else std::memcpy(hoff.data(), col->offsets, 4 * (size_t(n) + 1));
+        for (int64_t r = 0; r < n; r++)
+            if (hoff[r + 1] < hoff[r] || hoff[r] < 0 || hoff[r + 1] > col->chars_len)
+                return fail(ctx, PF_ERR_INVALID_ARG, "encode: offsets out of order or outside chars");
+    }
+    auto present = [&](int64_t r) { return !has_val || ((hval[size_t(r >> 3)] >> (r & 7)) & 1); };
+    // page plan: rows, present values, PLAIN byte sizes
+    struct PagePlanE { int64_t r0, r1; uint32_t d0, cnt; uint64_t plain; };
+    std::vector<PagePlanE> pp;
+    uint32_t m = 0;
+    for (int64_t r0 = 0; r0 < n || (n == 0 && pp.empty()); r0 += page_rows) {
+        PagePlanE p{r0, std::min(n, r0 + page_rows), m, 0, 0};
+        for (int64_t r = p.r0; r < p.r1; r++)
+            if (present(r)) {
+                p.cnt++;
+                if (str) p.plain += 4 + uint64_t(hoff[r + 1] - hoff[r]);
+            }
+        if (!str) p.plain = pt == PF_BOOLEAN ? (p.cnt + 7) / 8 : uint64_t(p.cnt) * w;
+        m += p.cnt;
+        pp.push_back(p);
+        if (n == 0) break;
+    }
+
+    // ---- device arena ----
+    size_t a_sz = 0;
+    auto take = [](size_t& cur, size_t sz) { size_t o = align_up(cur, 256); cur = o + std::max<size_t>(sz, 1); return o; };
+    const size_t N1 = size_t(n) + 1;
+    const size_t o_in = take(a_sz, str ? 0 : size_t(n) * w), o_vl = take(a_sz, vbytes);
+    const size_t o_of = take(a_sz, str ? 4 * N1 : 0), o_ch = take(a_sz, str ? size_t(col->chars_len) : 0);
+    const size_t o_flag = take(a_sz, 4 * N1), o_pos = take(a_sz, 4 * N1), o_dense = take(a_sz, size_t(n) * w);
+    const size_t o_dsrc = take(a_sz, str ? 4 * N1 : 0), o_dlen = take(a_sz, str ? 4 * N1 : 0);
+    const size_t o_vsz = take(a_sz, str ? 4 * N1 : 0), o_vpre = take(a_sz, str ? 4 * N1 : 0);
+    const size_t o_key = take(a_sz, 8 * N1), o_skey = take(a_sz, 8 * N1), o_didx = take(a_sz, 4 * N1), o_sidx = take(a_sz, 4 * N1);
+    const size_t o_hp = take(a_sz, 4 * N1), o_head = take(a_sz, 4 * N1), o_mark = take(a_sz, 4 * N1), o_did = take(a_sz, 4 * N1);
+    const size_t o_dsz = take(a_sz, 4 * N1), o_doff = take(a_sz, 4 * N1), o_ids = take(a_sz, 4 * N1), o_col = take(a_sz, 256);
+    size_t temp_bytes = 0;
+    HIPCHK(ctx, enc_scan_temp(N1, temp_bytes));
+    const size_t o_temp = take(a_sz, temp_bytes);
+    HIPCHK(ctx, ctx->d_enc.ensure(a_sz));
+    uint8_t* A = static_cast<uint8_t*>(ctx->d_enc.p);
+    EncArgs ea{};
+    ea.ptype = pt; ea.width = w; ea.n = n;
+    if (on_device) {
+        ea.values = static_cast<const uint8_t*>(col->values);
+        ea.validity = has_val ? col->validity : nullptr;
+        ea.offsets = col->offsets;
+        ea.chars = col->chars;
+    } else {
+        if (!str && n) HIPCHK(ctx, hipMemcpyAsync(A + o_in, col->values, size_t(n) * w, hipMemcpyHostToDevice, st));
+        if (has_val && vbytes) HIPCHK(ctx, hipMemcpyAsync(A + o_vl, hval.data(), vbytes, hipMemcpyHostToDevice, st));
+        if (str && n) {
+            HIPCHK(ctx, hipMemcpyAsync(A + o_of, hoff.data(), 4 * N1, hipMemcpyHostToDevice, st));
+            if (col->chars_len) HIPCHK(ctx, hipMemcpyAsync(A + o_ch, col->chars, size_t(col->chars_len), hipMemcpyHostToDevice, st));
+        }
+        ea.values = A + o_in;
+        ea.validity = has_val ? A + o_vl : nullptr;
+        ea.offsets = reinterpret_cast<const int32_t*>(A + o_of);
+        ea.chars = A + o_ch;
+    }
+    ea.flag = reinterpret_cast<uint32_t*>(A + o_flag); ea.pos = reinterpret_cast<uint32_t*>(A + o_pos);
+    ea.dense = A + o_dense;
+    ea.dsrc = reinterpret_cast<uint32_t*>(A + o_dsrc); ea.dlen = reinterpret_cast<uint32_t*>(A + o_dlen);
+    ea.vsz = reinterpret_cast<uint32_t*>(A + o_vsz); ea.vpre = reinterpret_cast<uint32_t*>(A + o_vpre);
+    ea.key = reinterpret_cast<uint64_t*>(A + o_key); ea.skey = reinterpret_cast<uint64_t*>(A + o_skey);
+    ea.didx = reinterpret_cast<uint32_t*>(A + o_didx); ea.sidx = reinterpret_cast<uint32_t*>(A + o_sidx);
+    ea.headpos = reinterpret_cast<uint32_t*>(A + o_hp); ea.head = reinterpret_cast<uint32_t*>(A + o_head);
+    ea.mark = reinterpret_cast<uint32_t*>(A + o_mark); ea.did = reinterpret_cast<uint32_t*>(A + o_did);
+    ea.dsz = reinterpret_cast<uint32_t*>(A + o_dsz); ea.doff = reinterpret_cast<uint32_t*>(A + o_doff);
+    ea.ids = reinterpret_cast<uint32_t*>(A + o_ids); ea.collide = reinterpret_cast<uint32_t*>(A + o_col);
+    void* temp = A + o_temp;
+
+    HIPCHK(ctx, hipMemsetAsync(A + o_col, 0, 256, st));
+    if (str) HIPCHK(ctx, hipMemsetAsync(ea.vsz, 0, 4 * N1, st));
+    if (n) HIPCHK(ctx, enc_dense(ea, temp, temp_bytes, st));
+    if (str) HIPCHK(ctx, enc_plain_sizes(ea, m, temp, temp_bytes, st));
+    const bool want_dict = col->dictionary && pt != PF_BOOLEAN && m > 0;
+    uint32_t hres[3] = {0, 0, 0};   // collide, dictionary entries, dictionary bytes
+    if (want_dict) {
+        HIPCHK(ctx, enc_dictionary(ea, m, w == 4 ? 32 : 64, temp, temp_bytes, st));
+        HIPCHK(ctx, hipMemcpyAsync(&hres[0], ea.collide, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipMemcpyAsync(&hres[1], ea.did + m, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipMemcpyAsync(&hres[2], ea.doff + m, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipStreamSynchronize(st));
+    }
+    int fallback = 0;
+    if (col->dictionary && pt == PF_BOOLEAN) fallback = 3;
+    else if (want_dict && hres[0]) fallback = 2;
+    else if (want_dict && int64_t(hres[2]) > dict_limit) fallback = 1;
+    const bool dict = want_dict && fallback == 0;
+    const uint32_t D = dict ? hres[1] : 0, dict_bytes = dict ? hres[2] : 0;
+    uint32_t bw = 1;
+    while (D > 1 && (uint64_t(1) << bw) < D) bw++;
+
+    // ---- values sections: [dictionary page | page 0 | page 1 | ...] in d_enc_out's front ----
+    std::vector<EncPage> ep(pp.size());
+    std::vector<std::pair<uint64_t, uint64_t>> sections;
+    size_t vo = 0;
+    const size_t o_dict = take(vo, dict_bytes);
+    if (dict) sections.push_back({o_dict, dict_bytes});
+    for (size_t i = 0; i < pp.size(); i++) {
+        const PagePlanE& p = pp[i];
+        uint64_t bytes;
+        if (dict) {
+            const uint64_t groups = (p.cnt + 7) / 8;
+            bytes = p.cnt ? 1 + uvarint_len((groups << 1) | 1) + groups * bw : 1;
+        } else {
+            bytes = p.plain;
+        }
+        ep[i] = EncPage{0, p.d0, p.cnt, dict ? 1u : 0u, bw};
+        ep[i].out_off = take(vo, bytes);
+        sections.push_back({ep[i].out_off, bytes});
+    }
+    const size_t o_pages = take(vo, sizeof(EncPage) * ep.size());
+    HIPCHK(ctx, ctx->d_enc_sec.ensure(vo));
+    uint8_t* SEC = static_cast<uint8_t*>(ctx->d_enc_sec.p);
+    ea.dict_out = SEC + o_dict;
+    ea.vals_out = SEC;
+    if (dict) enc_dictionary_page_and_ids(ea, m, st);
+    HIPCHK(ctx, hipMemcpyAsync(SEC + o_pages, ep.data(), sizeof(EncPage) * ep.size(), hipMemcpyHostToDevice, st));
+    enc_pages(ea, reinterpret_cast<const EncPage*>(SEC + o_pages), int(ep.size()), st);
+    HIPCHK(ctx, hipGetLastError());
+    std::vector<std::vector<uint8_t>> bodies;
+    if (col->codec == PF_CODEC_SNAPPY) {
+        const int rc = compress_sections(ctx, SEC, sections, bodies);
+        if (rc) return rc;
+    } else {
+        std::vector<uint8_t> all(vo);
+        HIPCHK(ctx, hipMemcpyAsync(all.data(), SEC, vo, hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipStreamSynchronize(st));
+        for (const auto& sct : sections) bodies.emplace_back(all.begin() + sct.first, all.begin() + sct.first + sct.second);
+    }
+
+    // ---- page headers + bodies ----
+    std::vector<uint8_t>& o = ctx->h_enc;
+    o.clear();
+    int64_t unc = 0;
+    size_t bi = 0;
+    out->dictionary_page_offset = -1;
+    if (dict) {
+        PageHeaderOut h;
+        h.page_type = PF_PAGE_DICTIONARY;
+        h.uncompressed_size = int32_t(dict_bytes);
+        h.compressed_size = int32_t(bodies[0].size());
+        h.num_values = int32_t(D);
+        h.encoding = PF_ENC_PLAIN;   // parquet-mr PARQUET_2_0: dictionary page PLAIN, data pages RLE_DICTIONARY
+        out->dictionary_page_offset = 0;
+        const size_t h0 = o.size();
+        write_page_header(o, h);
+        unc += int64_t(o.size() - h0) + dict_bytes;
+        o.insert(o.end(), bodies[0].begin(), bodies[0].end());
+        bi = 1;
+    }
+    out->data_page_offset = int64_t(o.size());
+    for (size_t i = 0; i < pp.size(); i++, bi++) {
+        const PagePlanE& p = pp[i];
+        const int64_t rows = p.r1 - p.r0;
+        std::vector<uint8_t> def;
+        if (col->max_def == 1) {   // RLE/bit-packed hybrid, bit width 1: one bit-packed run = the validity bits
+            const uint64_t groups = uint64_t(rows + 7) / 8;
+            put_uvarint(def, (groups << 1) | 1);
+            for (uint64_t g = 0; g < groups; g++) {
+                uint8_t b = has_val ? hval[size_t(p.r0 / 8 + g)] : 0xff;
+                const int64_t left = rows - int64_t(g) * 8;
+                if (left < 8) b &= uint8_t((1u << left) - 1u);
+                def.push_back(b);
+            }
+            if (rows == 0) def.clear();
+        }
+        PageHeaderOut h;
+        h.page_type = PF_PAGE_DATA_V2;
+        h.uncompressed_size = int32_t(def.size() + sections[bi].second);
+        h.compressed_size = int32_t(def.size() + bodies[bi].size());
+        h.num_values = int32_t(rows);
+        h.num_nulls = int32_t(rows - p.cnt);
+        h.num_rows = int32_t(rows);
+        h.encoding = dict ? PF_ENC_RLE_DICTIONARY : PF_ENC_PLAIN;
+        h.def_bytes = int32_t(def.size());
+        h.is_compressed = col->codec == PF_CODEC_SNAPPY;
+        const size_t h0 = o.size();
+        write_page_header(o, h);
+        unc += int64_t(o.size() - h0) + h.uncompressed_size;
+        o.insert(o.end(), def.begin(), def.end());
+        o.insert(o.end(), bodies[bi].begin(), bodies[bi].end());
+    }
+    out->bytes = o.data();
+    out->size = int64_t(o.size());
+    out->total_uncompressed_size = unc;
+    out->num_values = n;
+    out->n_data_pages = int32_t(pp.size());
+    out->dict_entries = int32_t(D);
+    out->data_encoding = dict ? PF_ENC_RLE_DICTIONARY : PF_ENC_PLAIN;
+    out->fallback = fallback;
+    out->codec = col->codec;
+    return PF_OK;
+}
+
 extern "C" {
 
 int pf_abi_version(void) { return PF_ABI_VERSION; }
@@ -454,7 +766,7 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);   // this context's work and any peer's ahead of it
     if (ctx->exec_stream) (void)hipStreamSynchronize(ctx->exec_stream);
     for (DevBuf* b : {&ctx->d_in, &ctx->d_scratch, &ctx->d_out, &ctx->d_bits, &ctx->d_chars, &ctx->d_meta, &ctx->d_tokmap,
-                      &ctx->d_scan_in, &ctx->d_scan})
+                      &ctx->d_scan_in, &ctx->d_scan, &ctx->d_enc, &ctx->d_enc_sec, &ctx->d_enc_out})
         b->release();
     ctx->h_meta.release();
     ctx->h_res.release();

@@ -124,6 +124,13 @@ def lib():
         "pf_file_read": ([vp, C.c_uint64, C.c_uint64, vp], C.c_int),
         "pf_file_created_by": ([vp], C.c_char_p),
         "pf_file_last_error": ([], C.c_char_p),
+        "pf_encode_chunk": ([vp, vp, i32, vp], C.c_int),
+        "pf_snappy_compress": ([vp, vp, sz, vp, sz, C.POINTER(C.c_size_t)], C.c_int),
+        "pf_writer_open": ([C.c_char_p, vp, i32, C.POINTER(vp)], C.c_int),
+        "pf_writer_add_chunk": ([vp, i32, vp], C.c_int),
+        "pf_writer_end_row_group": ([vp, C.c_int64], C.c_int),
+        "pf_writer_close": ([vp], C.c_int),
+        "pf_writer_last_error": ([], C.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
