@@ -8,8 +8,11 @@
 
 namespace pf {
 
-constexpr uint32_t SC_BLOCK = 65536;   // Snappy block (Google's kBlockSize)
-// worst case of one compressed block (literal headers of <= 3 bytes per run): Google's bound
+// Compression job: 16 KiB of input, compressed independently (copies never leave the job), so a
+// 64 KiB Snappy block is four jobs: 4x the waves of one wave per block, and the tokens still never
+// cross the 64 KiB output boundaries the read path's piece executor splits at.
+constexpr uint32_t SC_BLOCK = 16384;
+// worst case of one compressed job (literal headers of <= 3 bytes per run): Google's bound
 constexpr uint32_t SC_SLOT = ((32u + SC_BLOCK + SC_BLOCK / 6u) + 255u) & ~255u;
 
 struct SnapCJob {

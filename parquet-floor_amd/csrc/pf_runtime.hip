@@ -378,7 +378,7 @@ void put_uvarint(std::vector<uint8_t>& o, uint64_t v) {
     o.push_back(uint8_t(v));
 }
 
-// Snappy-compress `sections` (device, each [off, off + len) of `base`) into 64 KiB-block slots;
+// Snappy-compress `sections` (device, each [off, off + len) of `base`) into SC_BLOCK-job slots;
 // returns per section the host stream (varint length + block outputs) in `streams`.
 int compress_sections(pf_ctx* ctx, const uint8_t* base, const std::vector<std::pair<uint64_t, uint64_t>>& sections,
                       std::vector<std::vector<uint8_t>>& streams) {
