@@ -533,6 +533,9 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-write", action="store_true", help="skip the write-path leg")
+    ap.add_argument("--e2e-split", type=int, default=1, help="E2E: batches per row group (column subsets)")
+    ap.add_argument("--e2e-copy", choices=("batch", "chunks"), default="batch",
+                    help="E2E D2H: one copy per output arena (batch) or per chunk array (chunks)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="timed steps decode -> wait per batch on one context per stream (A/B of the pipelined default)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -693,8 +696,12 @@ def main():
             # this plan, 35 with one row group per batch, 26 with the column split.
             e2e_plan, _, _ = units_for_rank(argparse.Namespace(**{**vars(args), "split": "rowgroups"}), pf, world, rank,
                                             args.streams)
+            if args.e2e_split > 1:   # each row group's columns in e2e_split batches (earlier first D2H)
+                k = args.e2e_split
+                e2e_plan = [[[(g, p, cs[i::k]) for g, p, cs in units] for units in bl for i in range(k)]
+                            for bl in e2e_plan]
             e2e_batches = [[BatchInput(pf, units, decs[0].h) for units in bl] for bl in e2e_plan]
-            e2e = measure_e2e(decs[:len(e2e_batches)], e2e_batches, pf, st_all)
+            e2e = measure_e2e(decs[:len(e2e_batches)], e2e_batches, pf, st_all, args.e2e_copy)
             for bl in e2e_batches:
                 for bi in bl:
                     bi.host.free()
@@ -844,10 +851,12 @@ def measure_write(path, pf, dec, passes=3):
             "passes": passes}
 
 
-def measure_e2e(decs, batches, pf, st_all):
+def measure_e2e(decs, batches, pf, st_all, copy_mode="batch"):
     """Whole rank share, E2E_PASSES times: per context, per batch: pinned H2D of the batch's chunk
-    bytes (inside pf_decode_row_group), decode, pf_wait, then pf_copy_columns_async of every chunk
-    into pinned host buffers; the next batch on that context is ordered after those copies."""
+    bytes (inside pf_decode_row_group), decode, pf_wait, then the D2H of the decoded columns into
+    pinned host memory — copy_mode "batch": pf_copy_batch_async, one copy per output arena (3 per
+    batch); "chunks": pf_copy_columns_async, one copy per array of every chunk (up to 8 per chunk).
+    The next batch on that context is ordered after those copies."""
     from pfloor import _native
     from pfloor.decoder import PinnedBuffer
     from pfloor._native import ColumnOut
@@ -864,6 +873,8 @@ def measure_e2e(decs, batches, pf, st_all):
             infos = [d.info(i) for i in range(len(bi.items))]
             row.append(infos)
         layouts.append(row)
+    if copy_mode == "batch":
+        return _e2e_batch(decs, batches, layouts, pf)
     # pinned output buffers: one per context, sized for its largest batch
     outs = []
     for ctx_i, (d, bl) in enumerate(zip(decs, batches)):
@@ -944,7 +955,92 @@ def measure_e2e(decs, batches, pf, st_all):
             "ms_per_pass": round(dt * 1e3, 3), "h2d_bytes": h2d_per_pass, "d2h_bytes": d2h_per_pass,
             "pcie_bound_gbs": PCIE_GBS, "frac": round(t_link / dt, 4),
             "frac_definition": "max(H2D, D2H bytes) / 63 GB/s divided by the measured pass time",
-            "passes": E2E_PASSES}
+            "passes": E2E_PASSES, "d2h_copies": "per chunk array (pf_copy_columns_async)"}
+
+
+def measure_link(nbytes, reps=3):
+    """Raw PCIe rates on this box: one pinned-host <-> HBM copy of nbytes each way (torch), best of reps."""
+    try:
+        import torch
+        n = int(nbytes)
+        dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+        host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        out = {}
+        for name, dst, src in (("d2h_gbs", host, dev), ("h2d_gbs", dev, host)):
+            best = None
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                dst.copy_(src, non_blocking=True)
+                torch.cuda.synchronize()
+                t = time.perf_counter() - t0
+                best = t if best is None else min(best, t)
+            out[name] = round(n / best / 1e9, 2)
+        out["bytes"] = n
+        del dev, host
+        return out
+    except Exception as e:
+        return {"error": repr(e)}
+
+
+def _e2e_batch(decs, batches, layouts, pf):
+    """measure_e2e with pf_copy_batch_async: one pinned buffer per context (its largest batch)."""
+    from pfloor import _native
+    from pfloor.decoder import PinnedBuffer
+    L = _native.lib()
+    d2h_arrays = 0
+    for row, bl in zip(layouts, batches):
+        for infos, bi in zip(row, bl):
+            for ci, (p, c, *_r) in zip(infos, bi.items):
+                d2h_arrays += chunk_decoded_bytes(pf.columns[c], ci)
+    bufs, copied = [], 0
+    for d, bl in zip(decs, batches):
+        need = 0
+        for bi in bl:   # batch sizes from one decode of each batch
+            d.decode(bi.descs, bi.host.ptr.value, bi.nbytes, on_device=False)
+            if d.wait() != 0:
+                raise RuntimeError(d.error())
+            n = C.c_size_t()
+            _native.check(L.pf_batch_bytes(d.h, C.byref(n)), d.h, "pf_batch_bytes")
+            need = max(need, n.value)
+            copied += n.value
+        bufs.append(PinnedBuffer(d.h, max(need, 1)))
+    h2d_per_pass = sum(bi.nbytes for bl in batches for bi in bl)
+    errs = []
+
+    def worker(ci, d, bl):
+        try:
+            buf = bufs[ci]
+            for bi in bl:
+                d.decode(bi.descs, bi.host.ptr.value, bi.nbytes, on_device=False)
+                if d.wait() != 0:
+                    raise RuntimeError(d.error())
+                _native.check(L.pf_copy_batch_async(d.h, buf.ptr, buf.nbytes), d.h, "pf_copy_batch_async")
+            _native.check(L.pf_sync(d.h), d.h, "pf_sync")
+        except Exception as e:
+            errs.append(e)
+
+    def one_pass():
+        ts = [threading.Thread(target=worker, args=(i, d, bl)) for i, (d, bl) in enumerate(zip(decs, batches))]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        if errs:
+            raise errs[0]
+    one_pass()
+    t0 = time.perf_counter()
+    for _ in range(E2E_PASSES):
+        one_pass()
+    dt = (time.perf_counter() - t0) / E2E_PASSES
+    for b in bufs:
+        b.free()
+    t_link = max(h2d_per_pass, copied) / (PCIE_GBS * 1e9)
+    link = measure_link(copied)
+    return {"value": round(d2h_arrays / dt / 1e9, 3), "unit": "decoded GB/s (pinned host in -> host columns out)",
+            "link_measured": link, "frac_of_measured_d2h": round(copied / link["d2h_gbs"] / 1e9 / dt, 4) if "d2h_gbs" in link else None,
+            "ms_per_pass": round(dt * 1e3, 3), "h2d_bytes": h2d_per_pass, "d2h_bytes": copied,
+            "decoded_bytes": d2h_arrays, "pcie_bound_gbs": PCIE_GBS, "frac": round(t_link / dt, 4),
+            "frac_definition": "max(H2D, D2H bytes) / 63 GB/s divided by the measured pass time",
+            "passes": E2E_PASSES, "d2h_copies": "one per output arena per batch (pf_copy_batch_async)"}
 
 
 if __name__ == "__main__":

@@ -202,6 +202,15 @@ int pf_copy_column(pf_ctx* ctx, int chunk, const pf_column_out* out);
  * context is ordered after these copies (same stream), so decode i+1 can be enqueued at once. */
 int pf_copy_columns_async(pf_ctx* ctx, int n, const int* chunks, const pf_column_out* outs);
 
+/* Whole-batch form for the end-to-end pipeline: ONE D2H copy per output arena (values / offsets /
+ * levels, validity bits, chars) into a caller buffer of pf_batch_bytes bytes (pinned), instead of
+ * up to 8 copies per chunk. After pf_sync, pf_column_info_host returns chunk i's pf_column_info
+ * with its d_* pointers rebased into that host buffer (same layout rules as the device arrays).
+ * Valid after pf_wait until the next decode on this context. */
+int pf_batch_bytes(pf_ctx* ctx, size_t* bytes);
+int pf_copy_batch_async(pf_ctx* ctx, void* host, size_t cap);
+int pf_column_info_host(pf_ctx* ctx, int chunk, const void* host, pf_column_info* out);
+
 /* Block until everything enqueued on the context (copies included) has finished. */
 int pf_sync(pf_ctx* ctx);
 

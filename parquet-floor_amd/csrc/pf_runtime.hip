@@ -143,6 +143,7 @@ struct pf_ctx {
     std::vector<int64_t> host_status;      // per chunk host-side planning errors
     std::vector<pf_column_info> info;
     size_t bits_bytes = 0;
+    size_t out_bytes = 0;                  // values / offsets / levels arena extent of the last decode
     size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
     size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0, off_bajobs = 0, off_batiles = 0;
     size_t off_subsplits = 0;
@@ -1006,6 +1007,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     HIPCHK(ctx, ctx->d_bits.ensure(std::max<size_t>(bits, 1)));
     HIPCHK(ctx, ctx->d_chars.ensure(chars_cap));
     ctx->bits_bytes = bits;
+    ctx->out_bytes = out;
     uint8_t* S = static_cast<uint8_t*>(ctx->d_scratch.p);
     uint8_t* O = static_cast<uint8_t*>(ctx->d_out.p);
     uint8_t* B = static_cast<uint8_t*>(ctx->d_bits.p);
@@ -1312,6 +1314,84 @@ int pf_copy_columns_async(pf_ctx* ctx, int n, const int* chunks, const pf_column
         if (rc) return rc;
     }
     ctx->copies_pending = n > 0 || ctx->copies_pending;
+    return PF_OK;
+}
+
+namespace {
+// Host layout of pf_copy_batch_async: [out arena | bits arena | chars arena], each 256-B aligned.
+struct BatchLayout { size_t out, bits_off, bits, chars_off, chars, total; };
+BatchLayout batch_layout(const pf_ctx* ctx) {
+    BatchLayout b{};
+    b.out = ctx->out_bytes;
+    b.bits_off = align_up(b.out, 256);
+    b.bits = ctx->bits_bytes;
+    b.chars_off = align_up(b.bits_off + b.bits, 256);
+    const uint8_t* c0 = static_cast<const uint8_t*>(ctx->d_chars.p);
+    size_t hi = 0, bound = 0;
+    for (int c = 0; c < ctx->n_chunks && c < int(ctx->info.size()); c++) {
+        const pf_column_info& ci = ctx->info[c];
+        if (ci.d_chars && ci.num_chars > 0) {
+            hi = std::max(hi, size_t(static_cast<const uint8_t*>(ci.d_chars) - c0) + size_t(ci.num_chars));
+            bound += align_up(size_t(ci.num_chars), 256);
+        }
+    }
+    b.chars = hi;   // bytes copied: the arena's used extent (depends on the order k_scan placed the chunks)
+    // buffer size: an order-independent bound, so equal batches always need equal buffers
+    b.total = b.chars_off + std::max(hi, bound);
+    return b;
+}
+}  // namespace
+
+int pf_batch_bytes(pf_ctx* ctx, size_t* bytes) {
+    if (!ctx || !bytes) return fail(ctx, PF_ERR_INVALID_ARG, "null arg");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
+    if (!ctx->tables_from_decode) return fail(ctx, PF_ERR_STATE, "no finished decode");
+    *bytes = batch_layout(ctx).total;
+    return PF_OK;
+}
+
+int pf_copy_batch_async(pf_ctx* ctx, void* host, size_t cap) {
+    if (!ctx || (!host && cap)) return fail(ctx, PF_ERR_INVALID_ARG, "null arg");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
+    if (!ctx->tables_from_decode) return fail(ctx, PF_ERR_STATE, "no finished decode");
+    const BatchLayout b = batch_layout(ctx);
+    if (b.total > cap) return fail(ctx, PF_ERR_CAPACITY, "batch buffer too small (pf_batch_bytes)");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    uint8_t* h = static_cast<uint8_t*>(host);
+    if (b.out) HIPCHK(ctx, hipMemcpyAsync(h, ctx->d_out.p, b.out, hipMemcpyDeviceToHost, ctx->stream));
+    if (b.bits) HIPCHK(ctx, hipMemcpyAsync(h + b.bits_off, ctx->d_bits.p, b.bits, hipMemcpyDeviceToHost, ctx->stream));
+    if (b.chars) HIPCHK(ctx, hipMemcpyAsync(h + b.chars_off, ctx->d_chars.p, b.chars, hipMemcpyDeviceToHost, ctx->stream));
+    ctx->copies_pending = true;
+    return PF_OK;
+}
+
+int pf_column_info_host(pf_ctx* ctx, int chunk, const void* host, pf_column_info* out) {
+    if (!ctx || !out || !host) return fail(ctx, PF_ERR_INVALID_ARG, "null arg");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
+    if (chunk < 0 || chunk >= ctx->n_chunks) return fail(ctx, PF_ERR_INVALID_ARG, "chunk index out of range");
+    const BatchLayout b = batch_layout(ctx);
+    const uint8_t* h = static_cast<const uint8_t*>(host);
+    auto rebase = [&](const void* p) -> const void* {
+        if (!p) return nullptr;
+        const uint8_t* q = static_cast<const uint8_t*>(p);
+        const uint8_t* o = static_cast<const uint8_t*>(ctx->d_out.p);
+        const uint8_t* v = static_cast<const uint8_t*>(ctx->d_bits.p);
+        const uint8_t* c = static_cast<const uint8_t*>(ctx->d_chars.p);
+        if (q >= o && q <= o + b.out) return h + (q - o);
+        if (q >= v && q <= v + b.bits) return h + b.bits_off + (q - v);
+        if (q >= c && q <= c + b.chars) return h + b.chars_off + (q - c);
+        return nullptr;
+    };
+    pf_column_info ci = ctx->info[chunk];
+    ci.d_values = rebase(ci.d_values);
+    ci.d_validity = static_cast<const uint8_t*>(rebase(ci.d_validity));
+    ci.d_offsets = static_cast<const int32_t*>(rebase(ci.d_offsets));
+    ci.d_chars = static_cast<const uint8_t*>(rebase(ci.d_chars));
+    ci.d_list_offsets = static_cast<const int32_t*>(rebase(ci.d_list_offsets));
+    ci.d_list_validity = static_cast<const uint8_t*>(rebase(ci.d_list_validity));
+    ci.d_def_levels = static_cast<const uint8_t*>(rebase(ci.d_def_levels));
+    ci.d_rep_levels = static_cast<const uint8_t*>(rebase(ci.d_rep_levels));
+    *out = ci;
     return PF_OK;
 }
 

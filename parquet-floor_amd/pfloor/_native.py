@@ -107,6 +107,9 @@ def lib():
         "pf_copy_column": ([vp, i32, C.POINTER(ColumnOut)], C.c_int),
         "pf_copy_columns_async": ([vp, i32, C.POINTER(C.c_int), C.POINTER(ColumnOut)], C.c_int),
         "pf_sync": ([vp], C.c_int),
+        "pf_batch_bytes": ([vp, C.POINTER(C.c_size_t)], C.c_int),
+        "pf_copy_batch_async": ([vp, vp, sz], C.c_int),
+        "pf_column_info_host": ([vp, i32, vp, C.POINTER(ColumnInfo)], C.c_int),
         "pf_last_timing": ([vp, C.POINTER(C.c_float), i32, C.POINTER(C.c_int)], C.c_int),
         "pf_snappy_decompress": ([vp, vp, sz, vp, sz, C.POINTER(C.c_size_t)], C.c_int),
         "pf_snappy_last_fallback": ([vp], C.c_int),

@@ -232,6 +232,51 @@ class GpuDecoder:
         names = ["h2d", "snappy_parse", "snappy_exec", "dict", "delta", "count", "scan", "flat", "decode"]
         return dict(zip(names, list(buf)[:n.value]))
 
+    def fetch_batch(self, chunk_types):
+        """All chunks of the last decode with ONE D2H per output arena (pf_copy_batch_async), then
+        per chunk the canonical arrays cut from the host copy (pf_column_info_host).
+        chunk_types: [(physical_type, max_def, max_rep)] per chunk."""
+        L = lib()
+        n = C.c_size_t()
+        check(L.pf_batch_bytes(self.h, C.byref(n)), self.h, "pf_batch_bytes")
+        buf = PinnedBuffer(self.h, max(1, n.value))
+        try:
+            check(L.pf_copy_batch_async(self.h, buf.ptr, buf.nbytes), self.h, "pf_copy_batch_async")
+            check(L.pf_sync(self.h), self.h, "pf_sync")
+            host = buf.array()
+            base = buf.ptr.value
+            out = []
+            for i, (ptype, max_def, max_rep) in enumerate(chunk_types):
+                ci = ColumnInfo()
+                check(L.pf_column_info_host(self.h, i, buf.ptr, C.byref(ci)), self.h, "pf_column_info_host")
+                g = {"status": ci.status, "num_entries": ci.num_entries, "num_slots": ci.num_slots,
+                     "num_values": ci.num_values, "num_rows": ci.num_rows, "num_chars": ci.num_chars, "width": ci.width}
+                if ci.status == 0:
+                    ns, nr, ne = ci.num_slots, ci.num_rows, ci.num_entries
+
+                    def cut(ptr, nbytes, dtype=np.uint8):
+                        if not ptr:
+                            raise AssertionError("array missing from the batch copy")
+                        o = ptr - base
+                        return host[o:o + nbytes].copy().view(dtype)
+                    if ptype == 6:
+                        g["offsets"] = cut(ci.d_offsets, 4 * (ns + 1), np.int32)
+                        g["chars"] = cut(ci.d_chars, ci.num_chars) if ci.num_chars else np.zeros(0, np.uint8)
+                    else:
+                        g["values"] = cut(ci.d_values, ns * ci.width) if ns * ci.width else np.zeros(0, np.uint8)
+                    if max_def > 0:
+                        g["validity"] = cut(ci.d_validity, (ns + 7) // 8)
+                    if max_rep == 1:
+                        g["list_offsets"] = cut(ci.d_list_offsets, 4 * (nr + 1), np.int32)
+                        g["list_validity"] = cut(ci.d_list_validity, (nr + 7) // 8)
+                    if max_rep > 0:
+                        g["def_levels"] = cut(ci.d_def_levels, ne)
+                        g["rep_levels"] = cut(ci.d_rep_levels, ne)
+                out.append(g)
+            return out
+        finally:
+            buf.free()
+
     def fetch(self, i, physical_type, max_def, max_rep):
         """Copy chunk i's decoded arrays to host numpy (canonical layout)."""
         ci = self.info(i)

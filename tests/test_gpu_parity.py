@@ -255,3 +255,32 @@ def test_shared_stream_contexts_pipelined(oracle):
         for *_x, buf, _n in bufs:
             buf.free()
     b.close()
+
+
+@pytest.mark.parametrize("name", golden_files())
+def test_batch_copy_matches_per_chunk_copy(decoder, oracle, name):
+    """pf_copy_batch_async (one D2H per output arena) + pf_column_info_host give the same arrays
+    as pf_copy_column per chunk, and both match the oracle (E2E path of bench.py)."""
+    from pfloor.decoder import ParquetFile
+    path = os.path.join(GOLDEN, name + ".parquet")
+    with ParquetFile(path) as pf, oracle.open(path) as of:
+        items, total = pf.plan(list(range(pf.num_row_groups)), list(range(pf.num_columns)))
+        buf = decoder.staging(total)
+        descs = []
+        for rg, col, s, n, off in items:
+            if n:
+                pf.read_into(s, n, buf.ptr.value + off)
+            descs.append(pf.chunk_desc(rg, col, off))
+        decoder.decode(descs, buf.ptr.value, max(total, 1))
+        rc = decoder.wait()
+        types = [(pf.columns[col].physical_type, pf.columns[col].max_def, pf.columns[col].max_rep)
+                 for _rg, col, *_r in items]
+        got = decoder.fetch_batch(types)
+        for i, (rg, col, *_r) in enumerate(items):
+            one = decoder.fetch(i, *types[i])
+            assert got[i]["status"] == one["status"]
+            if one["status"] != 0:
+                assert rc != 0
+                continue
+            assert_chunk_equal(got[i], one, f"{name} rg{rg} c{col} [batch vs chunk]")
+            assert_chunk_equal(got[i], of.decode(rg, col), f"{name} rg{rg} c{col} [batch vs oracle]")
