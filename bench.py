@@ -712,7 +712,9 @@ def main():
     write = None
     if not args.no_write and rank == 0:
         try:
-            write = measure_write(path, pf, decs[0])
+            for d in decs:
+                d.set_timing(True)
+            write = measure_write(path, pf, decs[0], decs=decs)
         except Exception as e:
             write = {"error": repr(e)}
 
@@ -790,7 +792,7 @@ def main():
     return 0
 
 
-def measure_write(path, pf, dec, passes=3):
+def measure_write(path, pf, dec, passes=3, decs=None):
     """Write path (ParquetWriter.java:61-165 settings): row group 0 of the input, decoded on the
     GPU to host columns, is written WRITE passes times as a one-row-group file by pfloor.writer
     (per column: H2D, dictionary encode, pages, Snappy on the GPU, headers + file on the host);
@@ -824,14 +826,15 @@ def measure_write(path, pf, dec, passes=3):
         cols[name] = d
     schema = W.MessageType("lineitem", *fields)
     out_path = os.path.join(tempfile.gettempdir(), f"pfloor_write_{os.getpid()}.parquet")
-    times, encs = [], None
+    times, encs, kms = [], None, None
     for _ in range(passes):
         t0 = time.perf_counter()
-        wr = W.ParquetWriter(schema, out_path, None, decoder=dec)
+        wr = W.ParquetWriter(schema, out_path, None, decoder=None if decs else dec, decoders=decs)
         wr.write_columns(cols, n)
         wr.close()
         times.append(time.perf_counter() - t0)
         encs = list(wr.last_chunks)
+        kms = dict(wr.kernel_ms)
     size = os.path.getsize(out_path)
     back = decode_file(out_path, decoder=dec)
     bad = []
@@ -848,6 +851,16 @@ def measure_write(path, pf, dec, passes=3):
             "plain_fallbacks": sum(1 for e in encs if e[2] in (1, 2)),
             "parity": {"chunks": len(fields), "bit_exact": not bad, "mismatches": bad[:3],
                        "against": "the source columns, read back by the GPU read path"},
+            "contexts": len(decs) if decs else 1,
+            "roofline": {"bound": "hbm", "kernel": "k_snappy_compress (all 16 columns' launches, summed)",
+                         "algorithmic_bytes": kms["snappy_in"] + kms["snappy_out"], "kernel_ms": round(kms["snappy"], 3),
+                         "achieved": round((kms["snappy_in"] + kms["snappy_out"]) / (kms["snappy"] * 1e-3) / 1e9, 2)
+                         if kms["snappy"] > 0 else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round((kms["snappy_in"] + kms["snappy_out"]) / (kms["snappy"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                         if kms["snappy"] > 0 else None,
+                         "source": "HIP events around each k_snappy_compress launch (pf_encoded_chunk.snappy_ms), "
+                                   "launches on up to 4 streams may overlap"},
+            "encode_kernels_ms": round(kms["encode"], 3),
             "passes": passes}
 
 

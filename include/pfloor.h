@@ -314,6 +314,9 @@ typedef struct pf_encoded_chunk {
     int32_t  data_encoding;       /* PF_ENC_RLE_DICTIONARY or PF_ENC_PLAIN */
     int32_t  fallback;            /* 0; 1 dictionary above the limit; 2 hash collision; 3 type (BOOLEAN) */
     int32_t  codec;               /* ColumnMetaData.codec */
+    float    snappy_ms;           /* k_snappy_compress time (HIP events; 0 when stage timing is off) */
+    float    encode_ms;           /* dictionary + page kernels time (HIP events; 0 when timing is off) */
+    int64_t  snappy_in, snappy_out;    /* bytes into / out of the compressor */
 } pf_encoded_chunk;
 
 /* Encode one column chunk on the context's GPU. Inputs are host memory (copied) unless

@@ -382,7 +382,7 @@ void put_uvarint(std::vector<uint8_t>& o, uint64_t v) {
 // Snappy-compress `sections` (device, each [off, off + len) of `base`) into SC_BLOCK-job slots;
 // returns per section the host stream (varint length + block outputs) in `streams`.
 int compress_sections(pf_ctx* ctx, const uint8_t* base, const std::vector<std::pair<uint64_t, uint64_t>>& sections,
-                      std::vector<std::vector<uint8_t>>& streams) {
+                      std::vector<std::vector<uint8_t>>& streams, float* kernel_ms = nullptr) {
     hipStream_t st = ctx->stream;
     std::vector<SnapCJob> jobs;
     std::vector<std::pair<size_t, size_t>> range(sections.size());   // jobs of each section
@@ -409,12 +409,18 @@ int compress_sections(pf_ctx* ctx, const uint8_t* base, const std::vector<std::p
     std::vector<uint8_t> slots(nj * size_t(SC_SLOT));
     if (nj) {
         HIPCHK(ctx, hipMemcpyAsync(d + o_jobs, jobs.data(), sizeof(SnapCJob) * nj, hipMemcpyHostToDevice, st));
+        EVREC(ctx, ctx->ev[0], st);
         launch_snappy_compress(reinterpret_cast<const SnapCJob*>(d + o_jobs), int(nj), reinterpret_cast<uint32_t*>(d + o_len), st);
         HIPCHK(ctx, hipGetLastError());
+        EVREC(ctx, ctx->ev[1], st);
         HIPCHK(ctx, hipMemcpyAsync(lens.data(), d + o_len, 4 * nj, hipMemcpyDeviceToHost, st));
         HIPCHK(ctx, hipMemcpyAsync(slots.data(), d + o_slots, slots.size(), hipMemcpyDeviceToHost, st));
     }
     HIPCHK(ctx, hipStreamSynchronize(st));
+    if (kernel_ms) {
+        *kernel_ms = 0.f;
+        if (ctx->timing && nj) HIPCHK(ctx, hipEventElapsedTime(kernel_ms, ctx->ev[0], ctx->ev[1]));
+    }
     streams.assign(sections.size(), {});
     for (size_t i = 0; i < sections.size(); i++) {
         std::vector<uint8_t>& o = streams[i];
@@ -556,16 +562,20 @@ extern "C" int pf_encode_chunk(pf_ctx* ctx, const pf_encode_column* col, int on_
 
     HIPCHK(ctx, hipMemsetAsync(A + o_col, 0, 256, st));
     if (str) HIPCHK(ctx, hipMemsetAsync(ea.vsz, 0, 4 * N1, st));
+    EVREC(ctx, ctx->ev[2], st);
     if (n) HIPCHK(ctx, enc_dense(ea, temp, temp_bytes, st));
     if (str) HIPCHK(ctx, enc_plain_sizes(ea, m, temp, temp_bytes, st));
     const bool want_dict = col->dictionary && pt != PF_BOOLEAN && m > 0;
     uint32_t hres[3] = {0, 0, 0};   // collide, dictionary entries, dictionary bytes
+    float enc_ms = 0.f;
     if (want_dict) {
         HIPCHK(ctx, enc_dictionary(ea, m, w == 4 ? 32 : 64, temp, temp_bytes, st));
+        EVREC(ctx, ctx->ev[3], st);
         HIPCHK(ctx, hipMemcpyAsync(&hres[0], ea.collide, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(ctx, hipMemcpyAsync(&hres[1], ea.did + m, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(ctx, hipMemcpyAsync(&hres[2], ea.doff + m, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(ctx, hipStreamSynchronize(st));
+        if (ctx->timing) HIPCHK(ctx, hipEventElapsedTime(&enc_ms, ctx->ev[2], ctx->ev[3]));
     }
     int fallback = 0;
     if (col->dictionary && pt == PF_BOOLEAN) fallback = 3;
@@ -600,13 +610,16 @@ extern "C" int pf_encode_chunk(pf_ctx* ctx, const pf_encode_column* col, int on_
     uint8_t* SEC = static_cast<uint8_t*>(ctx->d_enc_sec.p);
     ea.dict_out = SEC + o_dict;
     ea.vals_out = SEC;
+    EVREC(ctx, ctx->ev[4], st);
     if (dict) enc_dictionary_page_and_ids(ea, m, st);
     HIPCHK(ctx, hipMemcpyAsync(SEC + o_pages, ep.data(), sizeof(EncPage) * ep.size(), hipMemcpyHostToDevice, st));
     enc_pages(ea, reinterpret_cast<const EncPage*>(SEC + o_pages), int(ep.size()), st);
     HIPCHK(ctx, hipGetLastError());
+    EVREC(ctx, ctx->ev[5], st);
     std::vector<std::vector<uint8_t>> bodies;
+    float snap_ms = 0.f;
     if (col->codec == PF_CODEC_SNAPPY) {
-        const int rc = compress_sections(ctx, SEC, sections, bodies);
+        const int rc = compress_sections(ctx, SEC, sections, bodies, &snap_ms);
         if (rc) return rc;
     } else {
         std::vector<uint8_t> all(vo);
@@ -676,6 +689,20 @@ extern "C" int pf_encode_chunk(pf_ctx* ctx, const pf_encode_column* col, int on_
     out->data_encoding = dict ? PF_ENC_RLE_DICTIONARY : PF_ENC_PLAIN;
     out->fallback = fallback;
     out->codec = col->codec;
+    if (ctx->timing) {   // the page kernels' events have completed (the stream was synchronised since)
+        float pg_ms = 0.f;
+        HIPCHK(ctx, hipEventElapsedTime(&pg_ms, ctx->ev[4], ctx->ev[5]));
+        enc_ms += pg_ms;
+    }
+    out->snappy_ms = snap_ms;
+    out->encode_ms = enc_ms;
+    out->snappy_in = 0;
+    out->snappy_out = 0;
+    if (col->codec == PF_CODEC_SNAPPY)
+        for (size_t i = 0; i < sections.size(); i++) {
+            out->snappy_in += int64_t(sections[i].second);
+            out->snappy_out += int64_t(bodies[i].size());
+        }
     return PF_OK;
 }
 

@@ -38,7 +38,8 @@ class EncodedChunk(C.Structure):
     _fields_ = [("bytes", C.c_void_p), ("size", C.c_int64), ("total_uncompressed_size", C.c_int64),
                 ("num_values", C.c_int64), ("dictionary_page_offset", C.c_int64), ("data_page_offset", C.c_int64),
                 ("n_data_pages", C.c_int32), ("dict_entries", C.c_int32), ("data_encoding", C.c_int32),
-                ("fallback", C.c_int32), ("codec", C.c_int32)]
+                ("fallback", C.c_int32), ("codec", C.c_int32), ("snappy_ms", C.c_float), ("encode_ms", C.c_float),
+                ("snappy_in", C.c_int64), ("snappy_out", C.c_int64)]
 
 
 class WriteField(C.Structure):
@@ -208,13 +209,18 @@ class ParquetWriter:
     row_group_rows bounds the rows buffered per row group (parquet-mr flushes by its 128 MiB
     block size; the bound here is in rows, the byte size of a row group is the caller's)."""
 
-    def __init__(self, schema, path, dehydrator, row_group_rows=1 << 20, device=0, decoder=None, codec=1):
+    def __init__(self, schema, path, dehydrator, row_group_rows=1 << 20, device=0, decoder=None, codec=1,
+                 decoders=None):
+        """decoders: several contexts (GpuDecoder) to encode the columns of a row group in parallel
+        (one host thread each); chunks are still appended in schema order."""
         from .decoder import GpuDecoder
         self.schema, self.dehydrator = schema, dehydrator
         self.row_group_rows = row_group_rows
-        self._own = decoder is None
-        self.dec = decoder or GpuDecoder(device)
+        self._own = decoder is None and not decoders
+        self.dec = decoder or (decoders[0] if decoders else GpuDecoder(device))
         self.enc = GpuColumnEncoder(self.dec)
+        self.encoders = [GpuColumnEncoder(d) for d in decoders] if decoders else [self.enc]
+        self.kernel_ms = {"snappy": 0.0, "encode": 0.0, "snappy_in": 0, "snappy_out": 0}
         self.codec = codec
         self.buf = _RowBuffer(schema)
         self.last_chunks = []     # (dict_entries, data_encoding, fallback) of the last row group
@@ -244,7 +250,7 @@ class ParquetWriter:
         one row group (buffered records are flushed first)."""
         self._flush()
         self.last_chunks = []
-        encoded = []
+        work = []
         for f in self.schema.fields:
             d = columns[f.name]
             validity = None
@@ -254,15 +260,61 @@ class ParquetWriter:
                 d, validity = (d[0], d[1]), d[2]
             if f.optional and validity is None:
                 validity = np.packbits(np.ones(n, bool), bitorder="little")
-            encoded.append(self._encode_add(f, d, validity, n, len(encoded)))
+            work.append((f, d, validity))
+        if len(self.encoders) == 1:
+            for i, (f, d, validity) in enumerate(work):
+                self._encode_add(f, d, validity, n, i)
+        else:
+            self._encode_parallel(work, n)
         self._end_group(n)
 
-    def _encode_add(self, f, data, validity, n, i):
-        out = self.enc.encode(f, data, validity, n, codec=self.codec)
+    def _encode_parallel(self, work, n):
+        """Columns encoded concurrently, one host thread per context (ctypes releases the GIL), biggest
+        first; each chunk's bytes are copied out of its context before the context encodes again."""
+        import threading
+        size = [sum(np.asarray(x).nbytes for x in (d if isinstance(d, tuple) else (d,))) for _f, d, _v in work]
+        order = sorted(range(len(work)), key=lambda i: -size[i])
+        results = [None] * len(work)
+        lock = threading.Lock()
+        errs = []
+
+        def worker(enc):
+            try:
+                while True:
+                    with lock:
+                        if not order:
+                            return
+                        i = order.pop(0)
+                    f, d, validity = work[i]
+                    out = enc.encode(f, d, validity, n, codec=self.codec)
+                    keep = C.create_string_buffer(C.string_at(out.bytes, out.size), max(1, out.size))
+                    cp = EncodedChunk.from_buffer_copy(out)
+                    cp.bytes = C.cast(keep, C.c_void_p)
+                    results[i] = (cp, keep)
+            except Exception as e:   # reported after the join
+                errs.append(e)
+
+        ts = [threading.Thread(target=worker, args=(e,)) for e in self.encoders]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        if errs:
+            raise errs[0]
+        for i, (cp, _keep) in enumerate(results):
+            self._add(cp, i)
+
+    def _add(self, out, i):
         self.last_chunks.append((out.dict_entries, out.data_encoding, out.fallback))
+        self.kernel_ms["snappy"] += out.snappy_ms
+        self.kernel_ms["encode"] += out.encode_ms
+        self.kernel_ms["snappy_in"] += out.snappy_in
+        self.kernel_ms["snappy_out"] += out.snappy_out
         rc = lib().pf_writer_add_chunk(self.w, i, C.byref(out))
         if rc != 0:
             raise PfError(rc, "pf_writer_add_chunk: " + (lib().pf_writer_last_error() or b"").decode(errors="replace"))
+
+    def _encode_add(self, f, data, validity, n, i):
+        out = self.enc.encode(f, data, validity, n, codec=self.codec)
+        self._add(out, i)
         return out
 
     def _end_group(self, n):
