@@ -10,7 +10,7 @@
 //   data pages   -> values section per page: bit width byte + one bit-packed run of the ids
 //                   (RLE_DICTIONARY), or PLAIN; definition levels (v2 pages, bit width 1) are the
 //                   validity bits themselves, written by the host
-//   Snappy       -> k_snappy_compress: one wave per 16 KiB job (hash table of 4-byte
+//   Snappy       -> k_snappy_compress: one wave per 8 KiB job (hash table of 4-byte
 //                   prefixes in LDS, 64 candidate positions per step, wave-parallel match
 //                   extension); jobs are independent, so a page's stream is the varint length
 //                   followed by its jobs' outputs; no token crosses a 64 KiB output boundary,
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(ENT) void k_enc_pages(EncArgs a, const EncPage* __r
 }
 
 // ---------------------------------------------------------------- Snappy compression
-// One wave per job of <= 16 KiB (SC_BLOCK): the job is staged in LDS with a 4096-entry table of the last
+// One wave per job of <= 8 KiB (SC_BLOCK): the job is staged in LDS with a 4096-entry table of the last
 // position (+1) of each 4-byte prefix hash. Each step the 64 lanes look up positions ip..ip+63
 // against the table as it stood before the step (so candidates always precede them); the first
 // lane whose candidate matches starts a copy: literal [lit, q), match extended 64 bytes per
