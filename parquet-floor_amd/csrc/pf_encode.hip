@@ -188,7 +188,8 @@ __global__ __launch_bounds__(ENT) void k_enc_pages(EncArgs a, const EncPage* __r
 // against the table as it stood before the step (so candidates always precede them); the first
 // lane whose candidate matches starts a copy: literal [lit, q), match extended 64 bytes per
 // ballot, emitted as copies of <= 64 bytes (copy-1 for 4..11 bytes at offsets < 2048, else
-// copy-2). No match in the step: its 64 positions are hashed in and the wave moves on.
+// copy-2); further matching lanes after that copy's end become tokens in the same step. No match
+// in the step: its 64 positions are hashed in and the wave moves on.
 namespace {
 constexpr uint32_t SC_HBITS = 12;
 __device__ __forceinline__ uint32_t sc_hash(uint32_t v) { return (v * 0x1e35a7bdu) >> (32 - SC_HBITS); }
@@ -239,27 +240,36 @@ __global__ __launch_bounds__(64) void k_snappy_compress(const SnapCJob* __restri
             ip += 64;
             continue;
         }
-        const uint32_t f = uint32_t(__ffsll(mask) - 1);
-        const uint32_t qf = ip + f;
-        const uint32_t cand = uint32_t(__builtin_amdgcn_readlane(int(c), int(f))) - 1u;
-        if (valid && uint32_t(lane) <= f) tab[h] = uint16_t(q + 1);
-        uint32_t L = 4;
-        for (;;) {   // extend the match 64 bytes per step
-            const uint32_t x = qf + L + uint32_t(lane), y = cand + L + uint32_t(lane);
-            const bool eq = x < len && buf[x] == buf[y];
-            const unsigned long long ne = __ballot(!eq);
-            if (!ne) { L += 64; continue; }
-            L += uint32_t(__ffsll(ne) - 1);
-            break;
+        // every match of this window, greedily: after a copy ending at e, the next token is the
+        // first lane at or after e whose candidate matched (candidates all precede ip, so each is
+        // valid); the lanes in between join the literal
+        unsigned long long mk = mask;
+        uint32_t e = ip;
+        while (mk) {
+            const uint32_t f = uint32_t(__ffsll(mk) - 1);
+            const uint32_t qf = ip + f;
+            const uint32_t cand = uint32_t(__builtin_amdgcn_readlane(int(c), int(f))) - 1u;
+            uint32_t L = 4;
+            for (;;) {   // extend the match 64 bytes per step
+                const uint32_t x = qf + L + uint32_t(lane), y = cand + L + uint32_t(lane);
+                const bool eq = x < len && buf[x] == buf[y];
+                const unsigned long long ne = __ballot(!eq);
+                if (!ne) { L += 64; continue; }
+                L += uint32_t(__ffsll(ne) - 1);
+                break;
+            }
+            if (qf > lit) op = sc_literal(dst, op, buf, lit, qf - lit);
+            const uint32_t off = qf - cand;
+            uint32_t rem = L;
+            while (rem >= 68) { op = sc_copy(dst, op, off, 64); rem -= 64; }
+            if (rem > 64) { op = sc_copy(dst, op, off, 60); rem -= 60; }
+            op = sc_copy(dst, op, off, rem);
+            e = qf + L;
+            lit = e;
+            mk = e - ip >= 64 ? 0ull : (mk & ~((1ull << (e - ip)) - 1ull));
         }
-        if (qf > lit) op = sc_literal(dst, op, buf, lit, qf - lit);
-        const uint32_t off = qf - cand;
-        uint32_t rem = L;
-        while (rem >= 68) { op = sc_copy(dst, op, off, 64); rem -= 64; }
-        if (rem > 64) { op = sc_copy(dst, op, off, 60); rem -= 60; }
-        op = sc_copy(dst, op, off, rem);
-        ip = qf + L;
-        lit = ip;
+        if (valid && q < e) tab[h] = uint16_t(q + 1);   // positions passed by this window's tokens
+        ip = e;   // lanes after the last copy had no match: rescanned with the table updated
     }
     if (len > lit) op = sc_literal(dst, op, buf, lit, len - lit);
     if (lane == 0) out_len[blockIdx.x] = op;
