@@ -24,7 +24,7 @@ cat "$OUT/bench.json"
 [ $rc -eq 0 ] || { echo "bench failed rc=$rc"; tail -40 "$OUT/bench.err"; exit 1; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-pmc --no-e2e --no-parity > "$OUT/prof.log" 2>&1
+    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-pmc --no-e2e --no-parity --no-write > "$OUT/prof.log" 2>&1
 rc=$?
 [ $rc -eq 0 ] || { echo "rocprof failed rc=$rc"; tail -40 "$OUT/prof.log"; exit 1; }
 find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \;
