@@ -520,7 +520,7 @@ class ContextPool:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=300)   # ~1.2 s timed: long enough for an SMI sampler to see the GPU busy
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="sf1")
     ap.add_argument("--data-dir", default=os.environ.get("PF_BENCH_DIR", "/tmp/pfloor_bench"))

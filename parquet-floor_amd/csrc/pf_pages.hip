@@ -557,14 +557,19 @@ __global__ __launch_bounds__(NT) void k_ba_verify(BaJob* __restrict__ jobs, cons
     if (__syncthreads_or(bad) && threadIdx.x == 0) { atomicExch(&J.state, int32_t(BA_FALLBACK)); PSTAMP(6, 1); }
 }
 
-__global__ __launch_bounds__(NT) void k_ba_fallback(BaJob* __restrict__ jobs, DevChunkResult* res) {
+// Grid-stride over the jobs with a small grid: nearly every walk was accepted by the checks above,
+// and a block per job (21 KB of LDS each) would wait for CUs held by other streams' kernels.
+__global__ __launch_bounds__(NT) void k_ba_fallback(BaJob* __restrict__ jobs, int n_jobs, DevChunkResult* res) {
     __shared__ BinWalkLds W;
-    BaJob& J = jobs[blockIdx.x];
-    if (J.state != BA_FALLBACK) return;
-    const int64_t t = binary_walk_wg(J.p, J.n, J.count, J.pos, J.len, W);
-    if (threadIdx.x == 0) {
-        if (t < 0) set_status(res, J.chunk, ST_CORRUPT, J.page);
-        else if (J.chars_out) *J.chars_out = t;
+    for (int j = blockIdx.x; j < n_jobs; j += gridDim.x) {
+        BaJob& J = jobs[j];
+        if (J.state != BA_FALLBACK) continue;
+        const int64_t t = binary_walk_wg(J.p, J.n, J.count, J.pos, J.len, W);
+        if (threadIdx.x == 0) {
+            if (t < 0) set_status(res, J.chunk, ST_CORRUPT, J.page);
+            else if (J.chars_out) *J.chars_out = t;
+        }
+        __syncthreads();
     }
 }
 
@@ -766,11 +771,9 @@ __device__ inline void flush_bits(const uint32_t* bits, uint64_t b0, uint32_t nb
     }
 }
 
-__global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                               const int* page_list, DevChunkResult* res) {
-    __shared__ DecodeLds S;
+__device__ void decode_page(const DevChunk* __restrict__ chunks, DevPage* pages, const int pi, DevChunkResult* res,
+                            DecodeLds& S) {
     LevelLds& L = S.L;
-    const int pi = page_list[blockIdx.x];
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
@@ -989,6 +992,19 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
     if (L.err || S.verr) { if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
     if (!counted && tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values),
                                         (unsigned long long)vidx);
+}
+
+// Pages the flat kernels did not take (nested, DELTA_LENGTH / DELTA_BYTE_ARRAY, RLE booleans, BSS,
+// anything they rejected). Grid-stride over the batch's page list with a grid sized by the host to
+// the pages that will need it (listed first): most blocks find their pages done, and a launch of
+// one large-LDS block per page would wait for CUs that other streams' kernels hold.
+__global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                               const int* page_list, int n, DevChunkResult* res) {
+    __shared__ DecodeLds S;
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        decode_page(chunks, pages, page_list[i], res, S);
+        __syncthreads();
+    }
 }
 
 // ---- k_flat: data pages of flat columns (max_rep == 0) ------------------------------------------
@@ -2410,7 +2426,7 @@ void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevC
     hipLaunchKernelGGL(k_ba_scan, dim3(n_jobs), dim3(NT), 0, st, d_jobs);
     hipLaunchKernelGGL(k_ba_emit, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
     hipLaunchKernelGGL(k_ba_verify, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
-    hipLaunchKernelGGL(k_ba_fallback, dim3(n_jobs), dim3(NT), 0, st, d_jobs, d_res);
+    hipLaunchKernelGGL(k_ba_fallback, dim3(std::min(n_jobs, 64)), dim3(NT), 0, st, d_jobs, n_jobs, d_res);
 }
 void launch_scan(DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                  uint8_t* arena, uint64_t cap, unsigned long long* used, hipStream_t st) {
@@ -2432,9 +2448,12 @@ void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
     if (nullable) hipLaunchKernelGGL(k_flat_null, dim3(n), dim3(NTN), 0, st, d_chunks, d_pages, blocks, d_res);
     hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
 }
-void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
-                   hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_decode, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res);
+void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int n_first,
+                   DevChunkResult* d_res, hipStream_t st) {
+    // n_first: pages at the head of the list that will need k_decode (host-known); the rest are
+    // checked by the stride loop
+    const int g = std::min(n, std::max(256, n_first));
+    if (n > 0) hipLaunchKernelGGL(k_decode, dim3(g), dim3(NT), 0, st, d_chunks, d_pages, d_list, n, d_res);
 }
 
 }  // namespace pf

@@ -39,7 +39,7 @@ void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*
 void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool);
 void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
-void launch_decode(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_decode(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
 void launch_page_scan(const ScanChunk*, int, pf_page_desc*, ScanCrc*, ScanResult*, hipStream_t);
 void launch_page_crc(const ScanCrc*, const int*, int, ScanResult*, int32_t*, hipStream_t);
 }  // namespace pf
@@ -143,6 +143,7 @@ struct pf_ctx {
     std::vector<int64_t> host_status;      // per chunk host-side planning errors
     std::vector<pf_column_info> info;
     size_t bits_bytes = 0;
+    int n_decode_first = 0;                // l_decode: pages that will need k_decode come first
     size_t out_bytes = 0;                  // values / offsets / levels arena extent of the last decode
     size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
     size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0, off_bajobs = 0, off_batiles = 0;
@@ -250,7 +251,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     EVREC(ctx, ctx->ev[7], st);
     launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty());
     EVREC(ctx, ctx->ev[8], st);
-    launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), d_res, st);
+    launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), ctx->n_decode_first, d_res, st);
     launch_dba_chars(d_chunks, d_pages, d_dba, int(ctx->l_dba.size()), d_res, st);
     EVREC(ctx, ctx->ev[9], st);
     HIPCHK(ctx, hipGetLastError());
@@ -1123,6 +1124,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     std::vector<int> xq[8];
     std::vector<int> spread;
     std::vector<std::vector<int>> sticky(static_cast<size_t>(n_chunks));
+    std::vector<int> decode_first;
     for (size_t i = 0; i < ctx->pages.size(); i++) {
         const DevPage& pg = ctx->pages[i];
         if (pg.flags & PG_DICT) continue;
@@ -1136,8 +1138,17 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             std::vector<int>& q = big_dict ? sticky[size_t(pg.chunk)] : spread;
             for (int b = 0; b < nb; b++) { q.push_back(int(i)); q.push_back(b); }
         }
-        ctx->l_decode.push_back(int(i));
+        // k_decode does the pages the flat kernels do not take: nested pages and encodings other than
+        // PLAIN / dictionary / DELTA_BINARY_PACKED go first (one block each), the rest are only checked
+        const int e = pg.encoding;
+        if (ck.max_rep > 0 || !(e == PF_ENC_PLAIN || e == PF_ENC_PLAIN_DICTIONARY || e == PF_ENC_RLE_DICTIONARY ||
+                                e == PF_ENC_DELTA_BINARY_PACKED) || ck.ptype == PF_BOOLEAN)
+            decode_first.push_back(int(i));
+        else
+            ctx->l_decode.push_back(int(i));
     }
+    ctx->n_decode_first = int(decode_first.size());
+    ctx->l_decode.insert(ctx->l_decode.begin(), decode_first.begin(), decode_first.end());
     {
         size_t load[8] = {};
         std::vector<int> order(static_cast<size_t>(n_chunks));

@@ -815,13 +815,9 @@ __global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict
 // One wave per window: make the bitmap and lane output counts of windows whose true entry is not
 // their own chain's start exact — tokens in [W0, merge point) for WM_MERGE, the whole window for
 // WM_FULL — by parsing from the true entry on the staged window.
-__global__ __launch_bounds__(64) void k_snappy_repair(const SnappyJob* __restrict__ jobs, const int2* __restrict__ wins,
-                                                      const SnapWin* __restrict__ win, uint32_t* __restrict__ lane_out,
-                                                      int* __restrict__ fb) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[SNAP_WSTAGE];
-    __shared__ __attribute__((aligned(16))) uint32_t sbits[SNAP_WWORDS];
-    __shared__ uint32_t slo[64];
-    const int2 jw = wins[blockIdx.x];
+__device__ void repair_window(const SnappyJob* __restrict__ jobs, const int2 jw, const SnapWin* __restrict__ win,
+                              uint32_t* __restrict__ lane_out, int* __restrict__ fb, uint8_t* stage, uint32_t* sbits,
+                              uint32_t* slo) {
     const SnappyJob job = jobs[jw.x];
     const int lane = threadIdx.x;
     if (fb[jw.x] == FB_SERIAL) return;
@@ -873,6 +869,21 @@ __global__ __launch_bounds__(64) void k_snappy_repair(const SnappyJob* __restric
         }
     }
     lo[lane] = acc;
+}
+
+// Grid-stride over the windows with a bounded grid: only windows the chain pass could not resolve
+// (WM_MERGE / WM_FULL) do work, and a launch of one staged block per 8 KiB window would wait for
+// CUs held by other streams' kernels.
+__global__ __launch_bounds__(64) void k_snappy_repair(const SnappyJob* __restrict__ jobs, const int2* __restrict__ wins,
+                                                      int n_wins, const SnapWin* __restrict__ win,
+                                                      uint32_t* __restrict__ lane_out, int* __restrict__ fb) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[SNAP_WSTAGE];
+    __shared__ __attribute__((aligned(16))) uint32_t sbits[SNAP_WWORDS];
+    __shared__ uint32_t slo[64];
+    for (int b = blockIdx.x; b < n_wins; b += gridDim.x) {
+        repair_window(jobs, wins[b], win, lane_out, fb, stage, sbits, slo);
+        __syncthreads();
+    }
 }
 
 // One wave per page: check the output total, then find the input position of the token that
@@ -2054,7 +2065,8 @@ void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins
     if (n_jobs <= 0) return;
     hipLaunchKernelGGL(k_snappy_index, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, d_win, d_ent, d_lane_out, d_fb);
     hipLaunchKernelGGL(k_snappy_chain, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_win, (const SnapEnt*)d_ent, d_lane_out, d_fb);
-    hipLaunchKernelGGL(k_snappy_repair, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, (const SnapWin*)d_win, d_lane_out, d_fb);
+    hipLaunchKernelGGL(k_snappy_repair, dim3(std::min(n_wins, 1024)), dim3(64), 0, s, d_jobs, d_wins, n_wins,
+                       (const SnapWin*)d_win, d_lane_out, d_fb);
     // sub-piece boundaries only for the sub-piece executor (PF_EXEC=3)
     hipLaunchKernelGGL(k_snappy_splits, dim3(n_jobs), dim3(64), 0, s, d_jobs, (const SnapWin*)d_win,
                        (const uint32_t*)d_lane_out, d_splits, snappy_exec_mode() == 3 ? d_subsplits : nullptr, d_fb);
