@@ -121,6 +121,7 @@ struct pf_ctx {
     DevBuf d_enc, d_enc_sec, d_enc_out;    // pf_encode_chunk / pf_snappy_compress: work arena, values sections, slots
     std::vector<uint8_t> h_enc;            // the last encoded chunk (headers + bodies)
     HostBuf h_meta, h_res;
+    HostBuf h_enc_slots;                   // pf_encode_chunk / pf_snappy_compress: compressed slots D2H
     // last batch
     int n_chunks = 0;
     bool pending = false;
@@ -406,16 +407,18 @@ int compress_sections(pf_ctx* ctx, const uint8_t* base, const std::vector<std::p
     HIPCHK(ctx, ctx->d_enc_out.ensure(m));
     uint8_t* d = static_cast<uint8_t*>(ctx->d_enc_out.p);
     for (size_t k = 0; k < nj; k++) jobs[k].dst = d + o_slots + k * SC_SLOT;
-    std::vector<uint32_t> lens(nj);
-    std::vector<uint8_t> slots(nj * size_t(SC_SLOT));
+    // compressed lengths + slots come back into the context's pinned staging (no zero-fill, DMA speed)
+    HIPCHK(ctx, ctx->h_enc_slots.ensure(align_up(4 * std::max<size_t>(nj, 1), 256) + nj * size_t(SC_SLOT)));
+    uint32_t* lens = static_cast<uint32_t*>(ctx->h_enc_slots.p);
+    uint8_t* slots = static_cast<uint8_t*>(ctx->h_enc_slots.p) + align_up(4 * std::max<size_t>(nj, 1), 256);
     if (nj) {
         HIPCHK(ctx, hipMemcpyAsync(d + o_jobs, jobs.data(), sizeof(SnapCJob) * nj, hipMemcpyHostToDevice, st));
         EVREC(ctx, ctx->ev[0], st);
         launch_snappy_compress(reinterpret_cast<const SnapCJob*>(d + o_jobs), int(nj), reinterpret_cast<uint32_t*>(d + o_len), st);
         HIPCHK(ctx, hipGetLastError());
         EVREC(ctx, ctx->ev[1], st);
-        HIPCHK(ctx, hipMemcpyAsync(lens.data(), d + o_len, 4 * nj, hipMemcpyDeviceToHost, st));
-        HIPCHK(ctx, hipMemcpyAsync(slots.data(), d + o_slots, slots.size(), hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipMemcpyAsync(lens, d + o_len, 4 * nj, hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipMemcpyAsync(slots, d + o_slots, nj * size_t(SC_SLOT), hipMemcpyDeviceToHost, st));
     }
     HIPCHK(ctx, hipStreamSynchronize(st));
     if (kernel_ms) {
@@ -428,7 +431,7 @@ int compress_sections(pf_ctx* ctx, const uint8_t* base, const std::vector<std::p
         put_uvarint(o, sections[i].second);
         for (size_t k = range[i].first; k < range[i].second; k++) {
             if (lens[k] > SC_SLOT) return fail(ctx, PF_ERR_HIP, "snappy compress: block overflow");
-            const uint8_t* b = slots.data() + k * size_t(SC_SLOT);
+            const uint8_t* b = slots + k * size_t(SC_SLOT);
             o.insert(o.end(), b, b + lens[k]);
         }
     }
@@ -799,6 +802,7 @@ int pf_ctx_destroy(pf_ctx* ctx) {
         b->release();
     ctx->h_meta.release();
     ctx->h_res.release();
+    ctx->h_enc_slots.release();
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
