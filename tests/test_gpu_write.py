@@ -303,3 +303,46 @@ def test_parallel_column_encoding(dec, oracle, tmp_path):
         for rg in range(2):
             a = of.decode(rg, 0)
             assert np.array_equal(np.frombuffer(a["values"].tobytes(), np.int64), cols["id"])
+
+
+def test_write_config4_shape(dec, oracle, tmp_path):
+    """Config-4-shaped columns through the writer: nullable INT32 / FLOAT, 30 % nulls, values from
+    100K-value pools (dictionary ~400 KB, ids of 17 bits), plus NaN payloads kept bit-exact
+    (raw-bit dictionary keys); read back by the oracle, pyarrow and the GPU reader."""
+    pq = pytest.importorskip("pyarrow.parquet")
+    from pfloor import writer as W
+    from pfloor.decoder import decode_file
+    rng = np.random.default_rng(4)
+    n, ncol = 200003, 6
+    fields, cols, exp = [], {}, {}
+    for k in range(ncol):
+        t = W.INT32 if k % 2 == 0 else W.FLOAT
+        pool = rng.integers(-2**31, 2**31 - 1, 100000, dtype=np.int64).astype(np.int32)
+        if t == W.FLOAT:
+            pool = pool.view(np.float32).copy()
+            pool[:3] = np.array([0x7fc00001, 0x7fc00002, 0xffc00000], np.uint32).view(np.float32)   # NaN payloads
+        vals = pool[rng.integers(0, 100000, n)]
+        present = rng.random(n) >= 0.3
+        vals = np.where(present, vals, np.zeros(1, vals.dtype))
+        name = f"c{k}"
+        fields.append(W.optional(t).named(name))
+        cols[name] = (vals, np.packbits(present, bitorder="little"))
+        exp[k] = (vals, present)
+    path = str(tmp_path / "c4.parquet")
+    w = W.ParquetWriter(W.MessageType("wide", *fields), path, None, decoder=dec)
+    w.write_columns(cols, n)
+    encs = list(w.last_chunks)
+    w.close()
+    assert all(e[1] == 8 for e in encs), encs
+    got = decode_file(path, decoder=dec)
+    assert got["_status"] == 0, got["_error"]
+    with oracle.open(path) as of:
+        for k in range(ncol):
+            g = got[(0, k)]
+            assert_chunk_equal(g, of.decode(0, k), f"c4 col {k}")
+            vals, present = exp[k]
+            gv = np.frombuffer(g["values"].tobytes(), np.uint32)
+            assert np.array_equal(gv[present], vals.view(np.uint32)[present])
+            assert np.array_equal(np.unpackbits(g["validity"], bitorder="little")[:n].astype(bool), present)
+    t = pq.read_table(path)
+    assert t.column("c0").null_count == int((~exp[0][1]).sum())
