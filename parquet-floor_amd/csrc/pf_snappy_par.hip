@@ -1007,7 +1007,10 @@ __global__ __launch_bounds__(64) void k_snappy_splits(const SnappyJob* __restric
 // ======================================================================== executor
 
 
-constexpr uint32_t XRING = 4096;     // output ring (LDS)
+#ifndef PF_XRING
+#define PF_XRING 4096
+#endif
+constexpr uint32_t XRING = PF_XRING; // output ring (LDS); copies reaching further back read HBM (far copies)
 constexpr uint32_t XRMASK = XRING - 1;
 constexpr uint32_t XSLOT = 1024;     // flush granule
 constexpr uint32_t XCHUNK = 1024;    // input bytes whose tokens are enumerated at once
