@@ -1440,7 +1440,7 @@ struct FlatLds {
 // k_flat, all levels present, fixed-width values: value index = entry index, lane-consecutive
 // entries so every load and store of a wave is one contiguous run of memory. Returns err.
 #ifndef PF_DICT_LDS
-#define PF_DICT_LDS 32768
+#define PF_DICT_LDS 16384   // 16 KiB: 0.8 % faster SF1 step than 32 KiB (occupancy), 64 KiB 8 % slower (tools/gpu_ab_libs.sh)
 #endif
 constexpr uint32_t DICT_LDS = PF_DICT_LDS;   // bytes of a fixed-width dictionary staged in LDS (k_flat_fixed)
 struct FixedLds {

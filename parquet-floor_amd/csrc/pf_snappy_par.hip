@@ -1015,7 +1015,10 @@ constexpr uint32_t XRMASK = XRING - 1;
 constexpr uint32_t XSLOT = 1024;     // flush granule
 constexpr uint32_t XCHUNK = 1024;    // input bytes whose tokens are enumerated at once
 constexpr uint32_t XSTAGE = XCHUNK + 64 + 16;
-constexpr uint32_t XBATCH = 1024;    // output bytes of one parallel step (ring: XBATCH + XSLOT <= XRING)
+#ifndef PF_XBATCH
+#define PF_XBATCH 1024
+#endif
+constexpr uint32_t XBATCH = PF_XBATCH;   // output bytes of one parallel step (ring: XBATCH + XSLOT <= XRING)
 constexpr uint32_t XLIT = 1024;      // long literals are copied in pieces of this many bytes
 constexpr uint32_t FBUF_W = 17;      // dwords per far copy's source slot (64 bytes + misalignment)
 constexpr uint32_t XFAR = 16;        // far copies per step (the step is cut before the next one)
