@@ -1016,7 +1016,11 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
 // per thread step (coalesced stores), instead of a byte loop per value.
 // Pages it does not take (run tables full, BIT_PACKED levels, RLE booleans, BYTE_STREAM_SPLIT,
 // corrupt section layout) keep done == 0 and are decoded by k_decode.
-constexpr int FT = 2048;             // entries per tile
+#ifndef PF_FT
+#define PF_FT 1024   // 1024: SF1 step 3.82-3.84 vs 3.94-3.97 ms with 2048, 4.04-4.06 with 512 (tools/gpu_ab_libs.sh)
+#endif
+constexpr int FT = PF_FT;            // entries per tile (fewer registers per thread, more blocks resident)
+static_assert(FT <= 2048 && FBLK % FT == 0, "FT = 4096 fails the multi-block parity test; tiles must divide blocks");
 constexpr int FEPT = FT / NT;        // consecutive entries per thread
 constexpr int RUN_CAP = 256;
 

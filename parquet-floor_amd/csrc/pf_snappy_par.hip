@@ -1021,7 +1021,10 @@ constexpr uint32_t XSTAGE = XCHUNK + 64 + 16;
 constexpr uint32_t XBATCH = PF_XBATCH;   // output bytes of one parallel step (ring: XBATCH + XSLOT <= XRING)
 constexpr uint32_t XLIT = 1024;      // long literals are copied in pieces of this many bytes
 constexpr uint32_t FBUF_W = 17;      // dwords per far copy's source slot (64 bytes + misalignment)
-constexpr uint32_t XFAR = 16;        // far copies per step (the step is cut before the next one)
+#ifndef PF_XFAR
+#define PF_XFAR 16
+#endif
+constexpr uint32_t XFAR = PF_XFAR;   // far copies per step (the step is cut before the next one)
 
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
