@@ -1025,7 +1025,10 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
 constexpr int FT = PF_FT;            // entries per tile (fewer registers per thread, more blocks resident)
 static_assert(FT <= 2048 && FBLK % FT == 0, "FT = 4096 fails the multi-block parity test; tiles must divide blocks");
 constexpr int FEPT = FT / NT;        // consecutive entries per thread
-constexpr int RUN_CAP = 256;
+#ifndef PF_RUN_CAP
+#define PF_RUN_CAP 256
+#endif
+constexpr int RUN_CAP = PF_RUN_CAP;
 
 struct Run {
     uint32_t first;    // index of the first value the run covers (entries for levels)
