@@ -1503,7 +1503,10 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
         const bool wide = w == 4 || w == 8;
         if (!bad && wide && ((dict && dalign) || enc == 0 || enc == 5)) {
             // batched: the loads of FB entries per thread are in flight together
-            constexpr uint32_t FB = FEPT / 2;
+#ifndef PF_FB_DIV
+#define PF_FB_DIV 2
+#endif
+            constexpr uint32_t FB = FEPT / PF_FB_DIV;   // entries per thread per load batch
             for (uint32_t kb = 0; kb < FEPT; kb += FB) {
             uint64_t v[FB];
             uint32_t id[FB];
