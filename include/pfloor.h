@@ -190,7 +190,8 @@ int pf_wait(pf_ctx* ctx);
 /* Sizes + device pointers of chunk i of the last decode (after pf_wait). */
 int pf_column_info_get(pf_ctx* ctx, int chunk, pf_column_info* out);
 
-/* Copy chunk i's decoded arrays into caller buffers (host, synchronous).
+/* Copy chunk i's decoded arrays into caller buffers (host, synchronous: returns when these
+ * copies are done, without waiting for a peer context's work queued behind them).
  * Fails with PF_ERR_CAPACITY (nothing copied) if any non-NULL buffer is too small. */
 int pf_copy_column(pf_ctx* ctx, int chunk, const pf_column_out* out);
 
@@ -211,7 +212,8 @@ int pf_batch_bytes(pf_ctx* ctx, size_t* bytes);
 int pf_copy_batch_async(pf_ctx* ctx, void* host, size_t cap);
 int pf_column_info_host(pf_ctx* ctx, int chunk, const void* host, pf_column_info* out);
 
-/* Block until everything enqueued on the context (copies included) has finished. */
+/* Block until the copies this context enqueued (pf_copy_columns_async / pf_copy_batch_async) have
+ * finished. A peer context's decode queued behind them on a shared stream is not waited for. */
 int pf_sync(pf_ctx* ctx);
 
 /* Kernel timing of the last decode (sum of per-stage HIP-event times, ms). */

@@ -32,7 +32,6 @@ struct SnappyJob {
     uint32_t* tokmap;     // bit i = a token starts at input byte i (n_win * 256 words, index pass)
     uint32_t win_base;    // first entry of this job's 8 KiB index windows (SnapWin / lane outs)
     uint32_t n_win;       // ceil(src_len / 8192), >= 1
-    uint16_t* cells;      // sub-piece executor: 2 bytes per output byte (value, or 256 + distance back), or null
 };
 
 enum : int32_t { DONE_FIXED = 1, DONE_FLAT = 2, DONE_NULL = 4 };

@@ -24,12 +24,11 @@
 #include "pfloor.h"
 
 namespace pf {
-void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, const int2*, int, uint32_t*,
-                   uint2*, int*, DevChunkResult*, hipStream_t);
-void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, uint2*, int*,
-                         hipStream_t);
-void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, const uint2*, int*, DevChunkResult*, hipStream_t);
-int snappy_exec_mode();
+void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, const int2*, int, int, uint32_t*,
+                   int*, int*, DevChunkResult*, hipStream_t);
+void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, int*, hipStream_t);
+void launch_snappy_exec(const SnappyJob*, int, const int2*, int, int, uint32_t*, int*, int*, DevChunkResult*, hipStream_t);
+bool snappy_wg_enabled();
 void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
@@ -114,6 +113,9 @@ struct pf_ctx {
     // recorded after the last operation of this context's decode: pf_wait waits for it, not for the
     // stream, so a context sharing the stream can have the next batch enqueued behind this one
     hipEvent_t ev_done = nullptr;
+    // recorded after the last enqueued D2H copy of this context's outputs: pf_copy_column / pf_sync
+    // wait for it, not for the stream, so a peer's decode queued behind the copies keeps running
+    hipEvent_t ev_copy = nullptr;
     bool timing = true;                    // per-stage events (pf_last_timing); pf_ctx_set_timing
     std::string err;
     DevBuf d_in, d_scratch, d_out, d_bits, d_chars, d_meta, d_tokmap;
@@ -133,6 +135,7 @@ struct pf_ctx {
     std::vector<SnappyJob> jobs;
     std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode, l_runs, l_dlen, l_dba, l_lvl;
     std::vector<int2> wins, pieces;       // Snappy index windows / 64 KiB pieces (job, index)
+    int n_wg_pieces = 0;                   // pieces[0, n) are dense: the workgroup executor takes them
     std::vector<BaJob> bajobs;             // PLAIN BYTE_ARRAY walks: dictionary pages, then data pages
     std::vector<int2> ba_tiles;            // (job relative to its batch, tile)
     int n_ba_dict = 0, n_ba_dict_tiles = 0;
@@ -148,7 +151,7 @@ struct pf_ctx {
     size_t out_bytes = 0;                  // values / offsets / levels arena extent of the last decode
     size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
     size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0, off_bajobs = 0, off_batiles = 0;
-    size_t off_subsplits = 0;
+    size_t off_pdone = 0;                  // per Snappy piece: 1 = decoded by k_snappy_exec_wg
     uint64_t chars_need = 0;
     const uint8_t* d_bytes = nullptr;
     int reruns = 0;
@@ -213,23 +216,23 @@ int enqueue_kernels(pf_ctx* ctx) {
     uint32_t* d_splits = reinterpret_cast<uint32_t*>(meta + ctx->off_splits);
     int* d_fallback = reinterpret_cast<int*>(meta + ctx->off_fallback);
     const int2* d_wins = reinterpret_cast<const int2*>(meta + ctx->off_wins);
-    uint2* d_subsplits = reinterpret_cast<uint2*>(meta + ctx->off_subsplits);
+    int* d_pdone = reinterpret_cast<int*>(meta + ctx->off_pdone);
 
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
     EVREC(ctx, ctx->ev[1], st);
     launch_snappy_parse(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent,
-                        ctx->d_lane_out, d_splits, d_subsplits, d_fallback, st);
+                        ctx->d_lane_out, d_splits, d_fallback, st);
     EVREC(ctx, ctx->ev[2], st);
     if (ctx->exec_stream) {
         HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->exec_stream, ctx->ev_fork, 0));
-        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_subsplits,
-                           d_fallback, d_res, ctx->exec_stream);
+        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), ctx->n_wg_pieces, d_splits,
+                           d_fallback, d_pdone, d_res, ctx->exec_stream);
         HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->exec_stream));
         HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_join, 0));
     } else {
-        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_subsplits,
-                           d_fallback, d_res, st);
+        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), ctx->n_wg_pieces, d_splits,
+                           d_fallback, d_pdone, d_res, st);
     }
     EVREC(ctx, ctx->ev[3], st);
     BaJob* d_bajobs = reinterpret_cast<BaJob*>(meta + ctx->off_bajobs);
@@ -263,6 +266,16 @@ int enqueue_kernels(pf_ctx* ctx) {
                                d_chunks, sizeof(DevChunk) * ctx->n_chunks, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipEventRecord(ctx->ev_done, st));
     return PF_OK;
+}
+
+// Workgroup-executor routing window (compressed bytes per 64 KiB piece); PF_XW_LO / PF_XW_HI (KiB).
+uint64_t wg_lo() {
+    static const uint64_t v = [] { const char* e = std::getenv("PF_XW_LO"); return (e ? std::strtoull(e, nullptr, 10) : 12ull) << 10; }();
+    return v;
+}
+uint64_t wg_hi() {
+    static const uint64_t v = [] { const char* e = std::getenv("PF_XW_HI"); return (e ? std::strtoull(e, nullptr, 10) : 56ull) << 10; }();
+    return v;
 }
 
 // Snappy tables of the batch's jobs: 8 KiB index windows and 64 KiB pieces. d_tokmap holds, per
@@ -301,13 +314,24 @@ int plan_snappy(pf_ctx* ctx) {
             ctx->pieces[pi++] = int2{int(j), int(k)};
         }
     }
-    if (lpt) {   // descending cost, ties in page order
-        std::sort(keyed.begin(), keyed.end(), [](uint64_t a, uint64_t b) {
+    // Dense pieces (many tokens per 64 KiB: compressed bytes per piece in [lo, hi)) go first and to the
+    // workgroup executor (k_snappy_exec_wg, ~10x lower latency per dense piece, one piece per CU);
+    // light and incompressible pieces to the single-wave executor, which runs many pieces per CU.
+    ctx->n_wg_pieces = 0;
+    if (lpt) {   // (dense first), descending cost, ties in page order
+        const uint64_t lo = wg_lo(), hi = wg_hi();
+        auto dense = [&](uint64_t key) { const uint64_t c = key >> 32; return snappy_wg_enabled() && c >= lo && c < hi; };
+        std::sort(keyed.begin(), keyed.end(), [&](uint64_t a, uint64_t b) {
+            const bool da = dense(a), db = dense(b);
+            if (da != db) return da;
             const uint64_t ca = a >> 32, cb = b >> 32;
             return ca != cb ? ca > cb : uint32_t(a) < uint32_t(b);
         });
         std::vector<int2> sorted(tp);
-        for (size_t i = 0; i < tp; i++) sorted[i] = ctx->pieces[size_t(uint32_t(keyed[i]))];
+        for (size_t i = 0; i < tp; i++) {
+            sorted[i] = ctx->pieces[size_t(uint32_t(keyed[i]))];
+            if (dense(keyed[i])) ctx->n_wg_pieces++;
+        }
         ctx->pieces.swap(sorted);
     }
     const size_t tok_bytes = size_t(n_win) * SNAP_WWORDS * 4, lo_bytes = size_t(n_win) * 64 * 4;
@@ -330,7 +354,6 @@ int upload_meta(pf_ctx* ctx) {
     std::memcpy(h + ctx->off_jobs, ctx->jobs.data(), sizeof(SnappyJob) * ctx->jobs.size());
     std::memcpy(h + ctx->off_pieces, ctx->pieces.data(), sizeof(int2) * ctx->pieces.size());
     std::memset(h + ctx->off_splits, 0xff, sizeof(uint32_t) * ctx->n_splits);
-    std::memset(h + ctx->off_subsplits, 0xff, sizeof(uint2) * size_t(ctx->n_splits) * (SNAP_SUBS - 1));
     std::memcpy(h + ctx->off_wins, ctx->wins.data(), sizeof(int2) * ctx->wins.size());
     {   // data-page walks report their chars into the page record
         BaJob* bj = reinterpret_cast<BaJob*>(h + ctx->off_bajobs);
@@ -750,6 +773,7 @@ int ctx_init(pf_ctx* ctx, pf_ctx* peer) {
         HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
     }
     HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
+    HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
     for (auto& e : ctx->ev) HIPCHK(nullptr, hipEventCreate(&e));
     return PF_OK;
 }
@@ -807,6 +831,7 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
+    if (ctx->ev_copy) (void)hipEventDestroy(ctx->ev_copy);
     ctx->streams.reset();   // destroys the stream(s) when no other context shares them
     delete ctx;
     return PF_OK;
@@ -878,9 +903,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->d_bytes = d_bytes;
 
     // ---- plan: sizes of scratch / outputs ----
-    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; uint64_t cell_off;
-                      uint64_t lt_off; };
-    const bool sub_exec = snappy_exec_mode() == 3;   // the sub-piece executor keeps 16-bit cells per output byte
+    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; uint64_t lt_off; };
     std::vector<PagePlan> pplan;
     size_t scratch = 0, out = 0, bits = 0;
     uint64_t chars_hint = 0;
@@ -928,12 +951,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     hs = PF_ERR_CORRUPT_PAGE; break;
                 }
                 bool compressed = cd.codec == PF_CODEC_SNAPPY && (!v2 || pd.is_compressed);
-                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull, ~0ull, ~0ull};
+                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull, ~0ull};
                 if (v2) { pg.lvl = src; pg.rep_len = uint32_t(pd.rep_bytes); pg.def_len = uint32_t(pd.def_bytes); }
                 if (compressed) {
                     pp.scratch_off = take(scratch, pd.uncompressed_size - lvl, 16);
-                    if (sub_exec && pd.uncompressed_size - lvl > SNAP_SUB)
-                        pp.cell_off = take(scratch, 2ull * (pd.uncompressed_size - lvl) + 16, 16);
                     pg.flags |= PG_COMPRESSED;
                     pg.body_len = pd.uncompressed_size - lvl;
                     SnappyJob j{};
@@ -1051,10 +1072,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             if (pg.flags & PG_COMPRESSED) {
                 pg.body = S + pp.scratch_off;
                 while (ji < ctx->jobs.size() && ctx->jobs[ji].page != int(i)) ji++;
-                if (ji < ctx->jobs.size()) {
-                    ctx->jobs[ji].dst = S + pp.scratch_off;
-                    ctx->jobs[ji].cells = pp.cell_off == ~0ull ? nullptr : reinterpret_cast<uint16_t*>(S + pp.cell_off);
-                }
+                if (ji < ctx->jobs.size()) ctx->jobs[ji].dst = S + pp.scratch_off;
             }
             if (pp.aux_off != ~0ull) {
                 pg.aux = reinterpret_cast<uint32_t*>(S + pp.aux_off);
@@ -1199,7 +1217,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_res = take(m, sizeof(DevChunkResult) * n_chunks);
     ctx->off_pieces = take(m, sizeof(int2) * ctx->pieces.size());
     ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);
-    ctx->off_subsplits = take(m, sizeof(uint2) * size_t(ctx->n_splits) * (SNAP_SUBS - 1));
+    ctx->off_pdone = take(m, sizeof(int) * ctx->pieces.size());
     ctx->off_fallback = take(m, sizeof(int) * ctx->jobs.size());
     ctx->off_wins = take(m, sizeof(int2) * ctx->wins.size());
     ctx->off_bajobs = take(m, sizeof(BaJob) * ctx->bajobs.size());
@@ -1325,7 +1343,8 @@ int enqueue_copy(pf_ctx* ctx, int chunk, const pf_column_out* o) {
 int pf_copy_column(pf_ctx* ctx, int chunk, const pf_column_out* o) {
     const int rc = enqueue_copy(ctx, chunk, o);
     if (rc) return rc;
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipEventRecord(ctx->ev_copy, ctx->stream));
+    HIPCHK(ctx, hipEventSynchronize(ctx->ev_copy));
     return PF_OK;
 }
 
@@ -1355,7 +1374,10 @@ int pf_copy_columns_async(pf_ctx* ctx, int n, const int* chunks, const pf_column
         const int rc = enqueue_copy(ctx, chunks[i], &outs[i]);
         if (rc) return rc;
     }
-    ctx->copies_pending = n > 0 || ctx->copies_pending;
+    if (n > 0) {
+        HIPCHK(ctx, hipEventRecord(ctx->ev_copy, ctx->stream));
+        ctx->copies_pending = true;
+    }
     return PF_OK;
 }
 
@@ -1403,6 +1425,7 @@ int pf_copy_batch_async(pf_ctx* ctx, void* host, size_t cap) {
     if (b.out) HIPCHK(ctx, hipMemcpyAsync(h, ctx->d_out.p, b.out, hipMemcpyDeviceToHost, ctx->stream));
     if (b.bits) HIPCHK(ctx, hipMemcpyAsync(h + b.bits_off, ctx->d_bits.p, b.bits, hipMemcpyDeviceToHost, ctx->stream));
     if (b.chars) HIPCHK(ctx, hipMemcpyAsync(h + b.chars_off, ctx->d_chars.p, b.chars, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipEventRecord(ctx->ev_copy, ctx->stream));
     ctx->copies_pending = true;
     return PF_OK;
 }
@@ -1441,7 +1464,7 @@ int pf_sync(pf_ctx* ctx) {
     if (!ctx) return fail(nullptr, PF_ERR_INVALID_ARG, "null ctx");
     if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->copies_pending) HIPCHK(ctx, hipEventSynchronize(ctx->ev_copy));   // this context's copies only
     ctx->copies_pending = false;
     return PF_OK;
 }
@@ -1468,13 +1491,11 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     ctx->info.clear();
     ctx->tables_from_decode = false;   // d_meta now holds this call's layout
     HIPCHK(ctx, ctx->d_in.ensure(std::max<size_t>(n, 1)));
-    const size_t cells_at = align_up(std::max<size_t>(ulen, 1) + 16, 256);
-    HIPCHK(ctx, ctx->d_scratch.ensure(cells_at + 2 * std::max<size_t>(ulen, 1) + 16));
+    HIPCHK(ctx, ctx->d_scratch.ensure(std::max<size_t>(ulen, 1) + 16));
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
     SnappyJob job{};
     job.src = static_cast<const uint8_t*>(ctx->d_in.p);
     job.dst = static_cast<uint8_t*>(ctx->d_scratch.p);
-    job.cells = reinterpret_cast<uint16_t*>(static_cast<uint8_t*>(ctx->d_scratch.p) + cells_at);
     job.src_len = uint32_t(n);
     job.dst_len = uint32_t(ulen);
     ctx->jobs.assign(1, job);
@@ -1487,7 +1508,7 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     size_t o_job = take(m, sizeof(SnappyJob)), o_pc = take(m, sizeof(int2) * ctx->pieces.size());
     size_t o_sp = take(m, 4 * ctx->pieces.size()), o_fb = take(m, 4), o_wn = take(m, sizeof(int2) * ctx->wins.size());
     size_t o_res = take(m, sizeof(DevChunkResult));
-    size_t o_ss = take(m, sizeof(uint2) * ctx->pieces.size() * (SNAP_SUBS - 1));
+    size_t o_pd = take(m, sizeof(int) * std::max<size_t>(ctx->pieces.size(), 1));
     m = align_up(m, 256);
     HIPCHK(ctx, ctx->d_meta.ensure(m));
     HIPCHK(ctx, ctx->h_meta.ensure(m));
@@ -1496,15 +1517,14 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     std::memcpy(h + o_job, ctx->jobs.data(), sizeof(SnappyJob));
     std::memcpy(h + o_pc, ctx->pieces.data(), sizeof(int2) * ctx->pieces.size());
     std::memset(h + o_sp, 0xff, 4 * ctx->pieces.size());
-    std::memset(h + o_ss, 0xff, sizeof(uint2) * ctx->pieces.size() * (SNAP_SUBS - 1));
     std::memcpy(h + o_wn, ctx->wins.data(), sizeof(int2) * ctx->wins.size());
     uint8_t* d = static_cast<uint8_t*>(ctx->d_meta.p);
     HIPCHK(ctx, hipMemcpyAsync(d, h, m, hipMemcpyHostToDevice, st));
     ctx->d_last_splits = reinterpret_cast<const uint32_t*>(d + o_sp);
     launch_snappy(reinterpret_cast<const SnappyJob*>(d + o_job), 1, reinterpret_cast<const int2*>(d + o_wn),
                   int(ctx->wins.size()), ctx->d_win, ctx->d_ent, ctx->d_lane_out, reinterpret_cast<const int2*>(d + o_pc),
-                  int(ctx->pieces.size()), reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<uint2*>(d + o_ss),
-                  reinterpret_cast<int*>(d + o_fb),
+                  int(ctx->pieces.size()), ctx->n_wg_pieces, reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb),
+                  reinterpret_cast<int*>(d + o_pd),
                   reinterpret_cast<DevChunkResult*>(d + o_res), st);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, ctx->h_res.ensure(512));

@@ -17,8 +17,6 @@ constexpr uint32_t SNAP_WSTAGE = SNAP_WIN + 96;   // staged window: + alignment 
 constexpr uint32_t SNAP_WWORDS = SNAP_WIN / 32;   // token-start bitmap words per window
 constexpr uint32_t SNAP_INVALID = 0xffffffffu;
 constexpr uint32_t SNAP_BLOCK = 65536;            // Google Snappy block = executor piece
-constexpr uint32_t SNAP_SUBS = 4;                 // sub-piece boundaries per piece (k_snappy_splits)
-constexpr uint32_t SNAP_SUB = SNAP_BLOCK / SNAP_SUBS;
 
 // per-job decode path (SnappyJob fallback flags, ordered: atomicMax escalates)
 enum : int { FB_OK = 0, FB_WHOLE = 1, FB_REDO = 2, FB_SERIAL = 3 };

@@ -814,7 +814,8 @@ __global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict
 
 // One wave per window: make the bitmap and lane output counts of windows whose true entry is not
 // their own chain's start exact — tokens in [W0, merge point) for WM_MERGE, the whole window for
-// WM_FULL — by parsing from the true entry on the staged window.
+// WM_FULL — by parsing from the true entry on the staged window; clear the bitmap of windows the
+// chain jumps over (WM_SKIP).
 __device__ void repair_window(const SnappyJob* __restrict__ jobs, const int2 jw, const SnapWin* __restrict__ win,
                               uint32_t* __restrict__ lane_out, int* __restrict__ fb, uint8_t* stage, uint32_t* sbits,
                               uint32_t* slo) {
@@ -824,6 +825,11 @@ __device__ void repair_window(const SnappyJob* __restrict__ jobs, const int2 jw,
     const uint32_t w = uint32_t(jw.y);
     const SnapWin sw = win[job.win_base + w];
     const uint32_t W0 = w * SNAP_WIN;
+    if (sw.flags == WM_SKIP) {   // inside a literal: no token starts here (the index pass's guesses are cleared,
+                                 // so the bitmap is exact over the whole stream: k_snappy_exec_wg reads it so)
+        reinterpret_cast<uint4*>(job.tokmap + size_t(w) * SNAP_WWORDS)[lane] = make_uint4(0, 0, 0, 0);
+        return;
+    }
     if (!((sw.flags == WM_MERGE && sw.entry != W0) || sw.flags == WM_FULL)) return;
     const uint64_t n = job.src_len;
     const uint64_t wend = min(uint64_t(W0) + SNAP_WIN, n);
@@ -890,7 +896,7 @@ __global__ __launch_bounds__(64) void k_snappy_repair(const SnappyJob* __restric
 // starts at each 64 KiB output boundary (window prefix sums -> lane region -> bitmap walk).
 __global__ __launch_bounds__(64) void k_snappy_splits(const SnappyJob* __restrict__ jobs, const SnapWin* __restrict__ win,
                                                       const uint32_t* __restrict__ lane_out, uint32_t* __restrict__ splits,
-                                                      uint2* __restrict__ subsplits, int* __restrict__ fb) {
+                                                      int* __restrict__ fb) {
     __shared__ uint32_t s_pre[FIX_MAXW + 1];
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
@@ -953,54 +959,6 @@ __global__ __launch_bounds__(64) void k_snappy_splits(const SnappyJob* __restric
             }
         }
         sp[k] = found;
-    }
-    if (!subsplits) return;
-    // sub-piece boundaries (SNAP_SUBS per piece, for the sub-piece executor): the first token whose
-    // output starts at or after k * 64 KiB + q * 16 KiB, searched in the region holding that byte
-    // (none there, or past the piece's end: SNAP_INVALID, the previous sub-piece runs on)
-    __threadfence_block();
-    __syncthreads();
-    uint2* ssp = subsplits + size_t(job.split_base) * (SNAP_SUBS - 1);
-    for (uint32_t e = lane; e < job.n_pieces * (SNAP_SUBS - 1); e += 64) {
-        const uint32_t k = e / (SNAP_SUBS - 1), q = 1 + e % (SNAP_SUBS - 1);
-        uint2 res = make_uint2(SNAP_INVALID, SNAP_INVALID);
-        const uint32_t B = k * SNAP_BLOCK + q * SNAP_SUB;
-        uint32_t pe = job.dst_len;   // the piece's end: the next valid main split
-        for (uint32_t k2 = k + 1; k2 < job.n_pieces; k2++)
-            if (sp[k2] != SNAP_INVALID) { pe = k2 * SNAP_BLOCK; break; }
-        if ((k == 0 || sp[k] != SNAP_INVALID) && B < pe) {
-            uint32_t a = 0, b = nw;
-            while (b - a > 1) {
-                const uint32_t m = (a + b) / 2;
-                if (s_pre[m] <= B) a = m; else b = m;
-            }
-            const uint32_t w = a;
-            uint32_t cum = s_pre[w];
-            const uint32_t* lo = LO + size_t(w) * 64;
-            int l = 0;
-            for (; l < 63; l++) {
-                const uint32_t v = lo[l];
-                if (B < cum + v) break;
-                cum += v;
-            }
-            const uint32_t rs = w * SNAP_WIN + uint32_t(l) * SNAP_RB;
-            const uint32_t* tm = job.tokmap + size_t(w) * SNAP_WWORDS + l * 4;
-            bool done = false;
-            for (int wd = 0; wd < 4 && !done; wd++) {
-                uint32_t mm = tm[wd];
-                while (mm) {
-                    const uint32_t p = rs + uint32_t(wd) * 32 + uint32_t(__ffs(mm) - 1);
-                    mm &= mm - 1;
-                    if (cum >= B) {
-                        if (cum < pe) res = make_uint2(p, cum);
-                        done = true;
-                        break;
-                    }
-                    cum += snap_tok(glb_read8(job.src, n, p)).ol;
-                }
-            }
-        }
-        ssp[e] = res;
     }
 }
 
@@ -1089,297 +1047,6 @@ __device__ __forceinline__ void wait_vmem_last_slot() {   // all but the last fl
     else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
 }
 
-// Executor step descriptor of one token (LDS, indexed by the token's lane).
-enum : uint32_t { XD_LIT = 0, XD_NEAR = 1, XD_FAR = 2, XD_DEP = 3 };
-struct XDesc {
-    uint32_t rel;    // output position relative to the step start
-    uint32_t src;    // LIT: stage offset; NEAR: absolute output position; FAR: fbuf byte offset
-    uint32_t off;    // copy offset (NEAR copies with off < len repeat their source)
-    uint32_t kind;
-};
-
-// One wave per 64 KiB piece (or per page). Token starts come from the bitmap, XCHUNK input bytes
-// at a time; 64 tokens are decoded at once (one per lane) and their output positions scanned
-// (DPP). A step then writes up to XBATCH output bytes into the LDS ring:
-//   far copies (source older than the ring) first issue their HBM loads (flushed output), so the
-//     latency overlaps the next phase;
-//   A. byte-parallel: output byte x of the step is lane x mod 64; its token comes from a
-//      token-start bitmap of the step's output (word prefix counts + popcount), then the byte is
-//      taken from the staged literal or the ring — every literal and every copy whose source
-//      lies wholly before the step;
-//   F. the far copies' bytes, from their prefetched source;
-//   B. copies whose source overlaps this step's output, in token order, one 64-lane
-//      read-then-write each (byte j reads src + j mod offset, always earlier output).
-// Literals longer than 64 bytes (or not staged) are copied alone, XLIT bytes at a time. Full
-// 2 KiB ring slots are flushed with 16-byte stores. A token chain that disagrees with the bitmap,
-// a copy reaching before the piece, or a piece not ending on a token marks the page for the
-// whole-page redo.
-__global__ __launch_bounds__(64) void k_snappy_exec(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
-                                                    const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring[XRING];
-    __shared__ __attribute__((aligned(16))) uint8_t stage[XSTAGE];
-    __shared__ uint16_t tokpos[XCHUNK / 2];
-    __shared__ __attribute__((aligned(16))) uint32_t fbuf[XFAR * FBUF_W];  // far-copy sources, one slot per far token
-    __shared__ __attribute__((aligned(16))) XDesc desc[64];
-    __shared__ uint32_t sbits[XBATCH / 32];                               // token starts of the step's output
-    __shared__ uint32_t wpre[XBATCH / 32];                                // tokens starting in earlier words
-    const int lane = threadIdx.x;
-    int j, k;
-    if (mode == 0) { const int2 pc = pieces[blockIdx.x]; j = pc.x; k = pc.y; }
-    else { j = blockIdx.x; k = 0; }
-    const int f = fb[j];
-    bool whole;
-    if (mode == 0) {
-        if (f >= FB_REDO || (f == FB_WHOLE && k > 0)) return;
-        whole = f == FB_WHOLE;
-    } else {
-        if (f != FB_REDO) return;
-        whole = true;
-    }
-    const SnappyJob job = jobs[j];
-    const uint8_t* in = job.src;
-    uint8_t* dst = job.dst;
-    const uint64_t n = job.src_len;
-    const uint32_t* sp = splits + job.split_base;
-    uint64_t pos0 = 0, ulen = 0;
-    if (!uvarint(in, n, pos0, ulen) || ulen != job.dst_len) {
-        if (lane == 0) atomicMax(&fb[j], FB_SERIAL);
-        return;
-    }
-    uint32_t ip, out_start, out_end = job.dst_len;
-    if (whole) {
-        ip = uint32_t(pos0);
-        out_start = 0;
-    } else {
-        if (k > 0 && sp[k] == SNAP_INVALID) return;   // no token at this boundary: an earlier piece covers it
-        ip = k == 0 ? uint32_t(pos0) : sp[k];
-        out_start = uint32_t(k) * SNAP_BLOCK;
-        for (uint32_t k2 = k + 1; k2 < job.n_pieces; k2++)
-            if (sp[k2] != SNAP_INVALID) { out_end = k2 * SNAP_BLOCK; break; }
-    }
-    const uint16_t* tm16 = reinterpret_cast<const uint16_t*>(job.tokmap);
-    uint32_t op = out_start, F = out_start;
-    uint32_t nst = 0;   // store instructions issued by the last flush (still possibly in flight)
-    bool bad = false;
-    XT_DECL;
-#ifdef PF_STAMPS
-    const unsigned long long xt0 = xt_;
-    if (lane == 0) STAMP_ADD(13, 1);
-#endif
-    while (op < out_end && !bad) {
-        if (ip >= n) { bad = true; break; }
-        const uint32_t I = ip & ~15u;
-        __syncthreads();
-        const uint32_t woff = snap_stage(stage, in, n, I, XSTAGE, lane);
-        // token starts in [ip, I + XCHUNK): 16 input bytes per lane
-        const uint32_t p16 = I + 16u * uint32_t(lane);
-        uint32_t bits = uint64_t(p16) < n ? uint32_t(tm16[p16 >> 4]) : 0u;
-        if (p16 + 16u <= ip) bits = 0;
-        else if (p16 < ip) bits &= ~((1u << (ip - p16)) - 1u);
-        const uint32_t cnt = __popc(bits);
-        const uint32_t ex = dpp_incl_scan(cnt);
-        const uint32_t T = __builtin_amdgcn_readlane(ex, 63);
-        uint32_t q = ex - cnt;
-        while (bits) {
-            const uint32_t b = uint32_t(__ffs(bits) - 1);
-            bits &= bits - 1;
-            tokpos[q++] = uint16_t(16u * uint32_t(lane) + b);
-        }
-        nst = 0;   // the bitmap loads above waited for every earlier store
-        __syncthreads();
-        XT(7);
-        if (T == 0) { bad = true; break; }
-        uint32_t sb = 0;
-        while (sb < T && op < out_end) {
-            const uint32_t t = sb + uint32_t(lane);
-            const bool v = t < T;
-            const uint32_t pos = v ? uint32_t(tokpos[t]) : 0u;
-            const SnapTok tk = snap_tok(lds_read8(stage, woff + pos));
-            const uint32_t ol = v ? tk.ol : 0u;
-            const uint32_t start = I + pos;
-            const uint32_t endp = tk.tl > uint64_t(0xffffffffu - start) ? 0xffffffffu : start + uint32_t(tk.tl);
-            const uint32_t prev = dpp_prev(endp);
-            const uint32_t inc = dpp_incl_scan(ol);
-            const uint32_t otok = op + inc - ol;
-            const bool take = v && otok < out_end;
-            const int nt = __popcll(__ballot(take));
-            const bool wrong = take && ((lane == 0 ? start != ip : start != prev) || endp > n || op + inc > out_end ||
-                                        inc < ol);
-            if (__any(wrong)) { bad = true; break; }
-            if (nt == 0) break;   // the previous step ended exactly at out_end
-            const uint32_t kd = tk.kind;
-            const uint32_t off = tk.arg;
-            const uint32_t srcv = start + tk.arg;   // literal data position
-            const bool lstaged = srcv + ol <= I + XCHUNK + 64;
-            XT(1);
-            if (lane == 0) STAMP_ADD(0, 1);
-            // step = tokens before the first long / unstaged literal and within XBATCH output bytes
-            // far copies: source wholly before the step and older than the ring can hold for any
-            // step (offset-independent of where the step is cut); at most XFAR per step
-            const uint32_t a = otok - off;                       // copy source start
-            const bool farc = take && kd != 0 && a + min(ol, off) <= op && int32_t(a - (op + XBATCH - XRING)) < 0;
-            const unsigned long long farm = __ballot(farc);
-            const uint32_t frank = uint32_t(__popcll(farm & lane_mask_lt(uint32_t(lane))));
-            const unsigned long long cutm = __ballot(take && (ol > 64u || inc > XBATCH || (kd == 0 && !lstaged) ||
-                                                              (farc && frank >= XFAR)));
-            const uint32_t cut = cutm ? uint32_t(__ffsll(cutm) - 1) : uint32_t(nt);
-            uint32_t used, btot;
-            if (cut == 0) {
-                // one literal, from HBM (copies are <= 64 bytes, so only a literal gets here)
-                const uint32_t L0 = __builtin_amdgcn_readfirstlane(ol);
-                const uint32_t s0 = __builtin_amdgcn_readfirstlane(srcv);
-                if (__builtin_amdgcn_readfirstlane(kd) != 0) { bad = true; break; }
-                uint32_t fl_slots = 0;
-                for (uint32_t d0 = 0; d0 < L0; d0 += XLIT) {
-                    const uint32_t c = min(L0 - d0, XLIT);
-                    const uint32_t b0 = uint32_t(lane) * 16u;
-                    if (b0 < c) {
-                        uint8_t by[16];
-                        #pragma unroll
-                        for (int u = 0; u < 16; u++) by[u] = b0 + u < c ? in[s0 + d0 + b0 + u] : uint8_t(0);
-                        #pragma unroll
-                        for (int u = 0; u < 16; u++)
-                            if (b0 + u < c) ring[(op + d0 + b0 + u) & XRMASK] = by[u];
-                    }
-                    fl_slots += flush_slots(ring, dst, F, op + d0 + c, lane);
-                }
-                nst = fl_slots;
-                used = 1;
-                btot = L0;
-                XT(11);
-            } else {
-                used = cut;
-                btot = __builtin_amdgcn_readlane(inc, cut - 1);
-                const bool inb = take && uint32_t(lane) < cut;
-                const bool lit = inb && kd == 0;
-                const bool cp = inb && kd != 0;
-                if (__any(cp && (off == 0 || off > otok - out_start))) { bad = true; break; }
-                const bool dep = cp && a + min(ol, off) > op;        // reads this step's output
-                const bool far = cp && farc;
-                const bool anyfar = __any(far);
-                // far copies: issue the HBM loads of their source now (flushed output)
-                uint32_t fw[FBUF_W];
-                if (anyfar) {
-                    if (nst == XST) wait_vmem_last_slot();   // all but the last slot's stores have landed
-                    else wait_vmem();
-                    const uint32_t* fsrc = reinterpret_cast<const uint32_t*>(dst + (a & ~3u));
-                    const uint32_t nwd = far ? ((a & 3u) + ol + 3u) >> 2 : 0u;
-                    #pragma unroll
-                    for (int u = 0; u < int(FBUF_W); u++) fw[u] = uint32_t(u) < nwd ? fsrc[u] : 0u;
-                }
-                // step descriptors + token-start bitmap over the step's output
-                const uint32_t rel = otok - op;
-                if (inb) {
-                    XDesc dd;
-                    dd.rel = rel;
-                    dd.off = off;
-                    if (lit) { dd.kind = XD_LIT; dd.src = woff + (srcv - I); }
-                    else if (dep) { dd.kind = XD_DEP; dd.src = a; }
-                    else if (far) { dd.kind = XD_FAR; dd.src = frank * (FBUF_W * 4) + (a & 3u); }
-                    else { dd.kind = XD_NEAR; dd.src = a; }
-                    desc[lane] = dd;
-                }
-                if (lane < int(XBATCH / 32)) sbits[lane] = 0;
-                __syncthreads();
-                if (inb) atomicOr(&sbits[rel >> 5], 1u << (rel & 31u));
-                __syncthreads();
-                {
-                    const uint32_t c = lane < int(XBATCH / 32) ? __popc(sbits[lane]) : 0u;
-                    const uint32_t ex = dpp_incl_scan(c) - c;
-                    if (lane < int(XBATCH / 32)) wpre[lane] = ex;
-                }
-                __syncthreads();
-                XT(3);
-                // A: byte-parallel literals + near copies
-                for (uint32_t x0 = 0; x0 < btot; x0 += 128) {
-                    uint8_t by[2];
-                    uint32_t xs[2];
-                    bool wr[2];
-                    #pragma unroll
-                    for (int u = 0; u < 2; u++) {
-                        const uint32_t x = x0 + uint32_t(u) * 64 + uint32_t(lane);
-                        xs[u] = x;
-                        wr[u] = false;
-                        by[u] = 0;
-                        if (x < btot) {
-                            const uint32_t wd = x >> 5;
-                            const uint32_t ti = wpre[wd] + __popc(sbits[wd] & ((2u << (x & 31u)) - 1u)) - 1u;
-                            const XDesc dd = desc[ti];
-                            const uint32_t jj = x - dd.rel;
-                            if (dd.kind == XD_LIT) { by[u] = stage[dd.src + jj]; wr[u] = true; }
-                            else if (dd.kind == XD_NEAR) {
-                                const uint32_t r = jj < dd.off ? jj : mod_small(jj, dd.off);
-                                by[u] = ring[(dd.src + r) & XRMASK];
-                                wr[u] = true;
-                            }
-                        }
-                    }
-                    #pragma unroll
-                    for (int u = 0; u < 2; u++)
-                        if (wr[u]) ring[(op + xs[u]) & XRMASK] = by[u];
-                }
-                XT(2);
-                if (anyfar) {   // F: far copies (never self-overlapping: offset > ring > 64)
-                    if (lane == 0) STAMP_ADD(9, 1);
-                    uint32_t* fl = fbuf + (far ? frank : 0u) * FBUF_W;
-                    const uint32_t nwd = far ? ((a & 3u) + ol + 3u) >> 2 : 0u;
-                    #pragma unroll
-                    for (int u = 0; u < int(FBUF_W); u++)
-                        if (uint32_t(u) < nwd) fl[u] = fw[u];
-                    __syncthreads();
-                    const uint8_t* fb8 = reinterpret_cast<const uint8_t*>(fbuf);
-                    for (uint32_t x0 = 0; x0 < btot; x0 += 64) {
-                        const uint32_t x = x0 + uint32_t(lane);
-                        if (x < btot) {
-                            const uint32_t wd = x >> 5;
-                            const uint32_t ti = wpre[wd] + __popc(sbits[wd] & ((2u << (x & 31u)) - 1u)) - 1u;
-                            const XDesc dd = desc[ti];
-                            if (dd.kind == XD_FAR) ring[(op + x) & XRMASK] = fb8[dd.src + (x - dd.rel)];
-                        }
-                    }
-                }
-                XT(4);
-                // B: dependent copies in token order
-                unsigned long long dm = __ballot(dep);
-                if (lane == 0) STAMP_ADD(8, __popcll(dm));
-                while (dm) {
-                    const int i = __ffsll(dm) - 1;
-                    dm &= dm - 1;
-                    const uint32_t oi = __builtin_amdgcn_readlane(otok, i);
-                    const uint32_t fi = __builtin_amdgcn_readlane(off, i);
-                    const uint32_t li = __builtin_amdgcn_readlane(ol, i);
-                    if (uint32_t(lane) < li) {
-                        const uint32_t r = fi < li ? mod_small(uint32_t(lane), fi) : uint32_t(lane);
-                        const uint8_t byte = ring[(oi - fi + r) & XRMASK];
-                        ring[(oi + uint32_t(lane)) & XRMASK] = byte;
-                    }
-                }
-#ifdef PF_SNAP_SAFE
-                __syncthreads();
-#endif
-                XT(5);
-                const uint32_t sl = flush_slots(ring, dst, F, op + btot, lane);
-                if (sl) nst = sl;
-                XT(6);
-            }
-            op += btot;
-            ip = __builtin_amdgcn_readlane(endp, int(used) - 1);
-            sb += used;
-        }
-    }
-    if (bad) {
-        if (lane == 0) atomicMax(&fb[j], whole ? FB_SERIAL : FB_REDO);
-        return;
-    }
-#ifdef PF_STAMPS
-    if (lane == 0) STAMP_ADD(12, __builtin_amdgcn_s_memtime() - xt0);
-#endif
-    // tail: bytes [F, op)
-    for (uint32_t a = F + uint32_t(lane) * 16u; a + 16u <= op; a += 1024u)
-        *reinterpret_cast<uint4*>(dst + a) = *reinterpret_cast<const uint4*>(ring + (a & XRMASK));
-    for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) dst[a] = ring[a & XRMASK];
-}
-
 // ======================================================================== executor v2
 //
 // Same token supply, chain checks, step cuts and far-copy prefetch as k_snappy_exec, but every
@@ -1402,7 +1069,8 @@ constexpr uint32_t X2_LDS = X2_FBUF_OFF + XFAR * FBUF_W * 4;
 enum : uint32_t { X2_LDSADDR = 0, X2_COPY = 1 };
 
 __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
-                                                     const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
+                                                     const uint32_t* __restrict__ splits, int* __restrict__ fb,
+                                                     const int* __restrict__ pdone, int mode) {
     __shared__ __attribute__((aligned(16))) uint8_t L[X2_LDS];
     __shared__ uint16_t tokpos[XCHUNK / 2];
     __shared__ uint32_t sbits[XBATCH / 32];                               // token starts of the step's output
@@ -1412,8 +1080,15 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
     uint32_t* const fbuf = reinterpret_cast<uint32_t*>(L + X2_FBUF_OFF);
     const int lane = threadIdx.x;
     int j, k;
-    if (mode == 0) { const int2 pc = pieces[blockIdx.x]; j = pc.x; k = pc.y; }
-    else { j = blockIdx.x; k = 0; }
+    if (mode == 0) {
+        if (pdone && pdone[blockIdx.x]) return;   // decoded by k_snappy_exec_wg
+        const int2 pc = pieces[blockIdx.x];
+        j = pc.x;
+        k = pc.y;
+    } else {
+        j = blockIdx.x;
+        k = 0;
+    }
     const int f = fb[j];
     bool whole;
     if (mode == 0) {
@@ -1668,389 +1343,6 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
     for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) gdst[a] = ring[a & XRMASK];
 }
 
-// ======================================================================== executor v3: sub-pieces
-//
-// A 64 KiB piece is split at the first token at/after each 16 KiB (or 32 KiB) output mark
-// (k_snappy_splits) and its sub-pieces run concurrently, one wave each, with the v2 byte-lane
-// machinery. Sub-piece 0 writes final bytes. A later sub-piece cannot see the bytes of the ones
-// before it, so it works on 16-bit cells: a cell is a byte value (< 256) or "the byte `d` positions
-// before this sub-piece's start" (256 + d). Copies propagate cells unchanged, so dependent copies,
-// self-overlapping runs and far copies work as in v2; the cells go to a scratch array (2 bytes per
-// output byte). A resolution pass then runs over the sub-pieces in order (all waves of the
-// workgroup): value cells are written as bytes, reference cells read the already final byte.
-// The serial token chain of a piece is thus cut into NSUB chains; the extra traffic is the cell
-// scratch (write + read, 2 bytes per byte of sub-pieces 1..NSUB-1).
-constexpr uint32_t S_RING = 4096;                                  // ring cells per wave
-constexpr uint32_t S_RMASK = S_RING - 1;
-constexpr uint32_t S_FBW = 34;                                     // dwords per far slot (64 cells + misalignment)
-constexpr uint32_t S_STAGE_OFF = 2 * S_RING;                       // byte offsets in a wave's LDS slice
-constexpr uint32_t S_FBUF_OFF = S_STAGE_OFF + ((XSTAGE + 15u) & ~15u);
-constexpr uint32_t S_TOK_OFF = S_FBUF_OFF + XFAR * S_FBW * 4;
-constexpr uint32_t S_SBITS_OFF = S_TOK_OFF + XCHUNK;               // tokpos: XCHUNK / 2 u16
-constexpr uint32_t S_WPRE_OFF = S_SBITS_OFF + XBATCH / 8;
-constexpr uint32_t S_SLICE = S_WPRE_OFF + XBATCH / 8;
-constexpr uint32_t SYM_PEND = 0xF000u;                             // pending word: SYM_PEND | window position
-constexpr uint32_t SYM_MAXD = SYM_PEND - 1u - 256u;                // largest distance a reference cell carries
-static_assert(S_SLICE % 16 == 0, "LDS slice alignment");
-
-// One sub-piece [op, out_end) from the token at input position ip. Copies may reach back to lo_bound
-// (the piece start). SYM: sources before sym_base become reference cells. Returns true if the token
-// chain disagrees with the bitmap or a copy reaches outside the piece (the page is redone whole).
-template <bool SYM>
-__device__ bool sub_exec(const SnappyJob& job, uint32_t ip, uint32_t op, const uint32_t out_end, const uint32_t lo_bound,
-                         const uint32_t sym_base, uint8_t* sl, const int lane) {
-    uint8_t* const stage = sl + S_STAGE_OFF;
-    uint32_t* const fbuf = reinterpret_cast<uint32_t*>(sl + S_FBUF_OFF);
-    uint16_t* const tokpos = reinterpret_cast<uint16_t*>(sl + S_TOK_OFF);
-    uint32_t* const sbits = reinterpret_cast<uint32_t*>(sl + S_SBITS_OFF);
-    uint32_t* const wpre = reinterpret_cast<uint32_t*>(sl + S_WPRE_OFF);
-    uint8_t* const ring8 = sl;
-    uint16_t* const ring16 = reinterpret_cast<uint16_t*>(sl);
-    const uint8_t* in = job.src;
-    const uint64_t n = job.src_len;
-    const PF_GLOBAL uint16_t* tm16 = (const PF_GLOBAL uint16_t*)(job.tokmap);
-    const PF_GLOBAL uint8_t* gin = gptr(in);
-    PF_GLOBAL uint8_t* gdst = gptr(job.dst);
-    PF_GLOBAL uint16_t* gcell = gptr(job.cells);
-    uint32_t F = op;   // cells / bytes below F are stored
-    bool bad = false;
-    auto put = [&](uint32_t pos, uint32_t v) {
-        if constexpr (SYM) ring16[pos & S_RMASK] = uint16_t(v);
-        else ring8[pos & S_RMASK] = uint8_t(v);
-    };
-    // store [F, upto) in whole XSLOT slots (SYM: the unaligned head of the sub-piece cell by cell first)
-    auto flush = [&](uint32_t upto) {
-        if constexpr (SYM) {
-            if ((F & 7u) && upto - F >= XSLOT) {
-                const uint32_t h = min(8u - (F & 7u), upto - F);
-                if (uint32_t(lane) < h) gcell[F + lane] = ring16[(F + lane) & S_RMASK];
-                F += h;
-            }
-        }
-        while (upto - F >= XSLOT) {
-            if constexpr (SYM) {
-                const uint32_t a0 = F + uint32_t(lane) * 16u;
-                const u32x4 v0 = *reinterpret_cast<const u32x4*>(ring16 + (a0 & S_RMASK));
-                const u32x4 v1 = *reinterpret_cast<const u32x4*>(ring16 + ((a0 + 8u) & S_RMASK));
-                *(PF_GLOBAL u32x4*)(gcell + a0) = v0;
-                *(PF_GLOBAL u32x4*)(gcell + a0 + 8u) = v1;
-            } else {
-                const uint32_t a0 = F + uint32_t(lane) * 16u;
-                *(PF_GLOBAL u32x4*)(gdst + a0) = *reinterpret_cast<const u32x4*>(ring8 + (a0 & S_RMASK));
-            }
-            F += XSLOT;
-        }
-    };
-    while (op < out_end && !bad) {
-        if (ip >= n) { bad = true; break; }
-        const uint32_t I = ip & ~15u;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (single wave: LDS is in order; compiler fence)
-        const uint32_t woff = snap_stage(stage, in, n, I, XSTAGE, lane);
-        const uint32_t p16 = I + 16u * uint32_t(lane);
-        uint32_t bits = uint64_t(p16) < n ? uint32_t(tm16[p16 >> 4]) : 0u;
-        if (p16 + 16u <= ip) bits = 0;
-        else if (p16 < ip) bits &= ~((1u << (ip - p16)) - 1u);
-        const uint32_t cnt = __popc(bits);
-        const uint32_t ex = dpp_incl_scan(cnt);
-        const uint32_t T = __builtin_amdgcn_readlane(ex, 63);
-        uint32_t q = ex - cnt;
-        while (bits) {
-            const uint32_t b = uint32_t(__ffs(bits) - 1);
-            bits &= bits - 1;
-            tokpos[q++] = uint16_t(16u * uint32_t(lane) + b);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (T == 0) { bad = true; break; }
-        uint32_t sb = 0;
-        while (sb < T && op < out_end) {
-            const uint32_t t = sb + uint32_t(lane);
-            const bool v = t < T;
-            const uint32_t pos = v ? uint32_t(tokpos[t]) : 0u;
-            const SnapTok tk = snap_tok(lds_read8(stage, woff + pos));
-            const uint32_t ol = v ? tk.ol : 0u;
-            const uint32_t start = I + pos;
-            const uint32_t endp = tk.tl > uint64_t(0xffffffffu - start) ? 0xffffffffu : start + uint32_t(tk.tl);
-            const uint32_t prev = dpp_prev(endp);
-            const uint32_t inc = dpp_incl_scan(ol);
-            const uint32_t otok = op + inc - ol;
-            const bool take = v && otok < out_end;
-            const int nt = __popcll(__ballot(take));
-            const bool wrong = take && ((lane == 0 ? start != ip : start != prev) || endp > n || inc < ol);
-            if (__any(wrong)) { bad = true; break; }
-            if (nt == 0) break;
-            const uint32_t kd = tk.kind;
-            const uint32_t off = tk.arg;
-            const uint32_t srcv = start + tk.arg;   // literal data position
-            const bool lstaged = srcv + ol <= I + XCHUNK + 64;
-            const uint32_t a = otok - off;         // copy source start
-            // far: source wholly before the step, older than the ring, and (SYM) not wholly a reference
-            const bool farc = take && kd != 0 && a + min(ol, off) <= op && int32_t(a - (op + XBATCH - S_RING)) < 0 &&
-                              (!SYM || a + ol > sym_base);
-            const unsigned long long farm = __ballot(farc);
-            const uint32_t frank = uint32_t(__popcll(farm & lane_mask_lt(uint32_t(lane))));
-            const unsigned long long cutm = __ballot(take && (ol > 64u || inc > XBATCH || (kd == 0 && !lstaged) ||
-                                                              (farc && frank >= XFAR)));
-            const uint32_t cut = cutm ? uint32_t(__ffsll(cutm) - 1) : uint32_t(nt);
-            uint32_t used, btot;
-            if (cut == 0) {
-                // one long literal, from HBM
-                const uint32_t L0 = __builtin_amdgcn_readfirstlane(ol);
-                const uint32_t s0 = __builtin_amdgcn_readfirstlane(srcv);
-                if (__builtin_amdgcn_readfirstlane(kd) != 0 || op + L0 > out_end) { bad = true; break; }
-                for (uint32_t d0 = 0; d0 < L0; d0 += XLIT) {
-                    const uint32_t c = min(L0 - d0, XLIT);
-                    const uint32_t b0 = uint32_t(lane) * 16u;
-                    if (b0 < c) {
-                        uint8_t by[16];
-                        #pragma unroll
-                        for (int u = 0; u < 16; u++) by[u] = b0 + u < c ? gin[s0 + d0 + b0 + u] : uint8_t(0);
-                        #pragma unroll
-                        for (int u = 0; u < 16; u++)
-                            if (b0 + u < c) put(op + d0 + b0 + u, by[u]);
-                    }
-                    flush(op + d0 + c);
-                }
-                used = 1;
-                btot = L0;
-            } else {
-                used = cut;
-                btot = __builtin_amdgcn_readlane(inc, cut - 1);
-                if (op + btot > out_end) { bad = true; break; }
-                const bool inb = take && uint32_t(lane) < cut;
-                const bool lit = inb && kd == 0;
-                const bool cp = inb && kd != 0;
-                if (__any(cp && (off == 0 || off > otok - lo_bound))) { bad = true; break; }
-                const bool far = cp && farc;
-                if (__any(far)) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // flushed cells / bytes have landed
-                    if (far) {
-                        uint32_t fw[S_FBW];
-                        uint32_t nwd;
-                        if constexpr (SYM) {
-                            const PF_GLOBAL uint32_t* fsrc = (const PF_GLOBAL uint32_t*)(gcell + (a & ~1u));
-                            nwd = ((a & 1u) * 2u + 2u * ol + 3u) >> 2;
-                            #pragma unroll
-                            for (int u = 0; u < int(S_FBW); u++) fw[u] = uint32_t(u) < nwd ? fsrc[u] : 0u;
-                        } else {
-                            const PF_GLOBAL uint32_t* fsrc = (const PF_GLOBAL uint32_t*)(gdst + (a & ~3u));
-                            nwd = ((a & 3u) + ol + 3u) >> 2;
-                            #pragma unroll
-                            for (int u = 0; u < int(FBUF_W); u++) fw[u] = uint32_t(u) < nwd ? fsrc[u] : 0u;
-                        }
-                        uint32_t* fl = fbuf + frank * S_FBW;
-                        #pragma unroll
-                        for (int u = 0; u < int(S_FBW); u++)
-                            if (uint32_t(u) < nwd) fl[u] = fw[u];
-                    }
-                }
-                // descriptor: d0 = rel (10 bits) | kind << 10 (0 literal, 1 near copy, 2 far copy)
-                //                  | (near: self-overlap flag, far: slot) << 12 | offset << 16
-                //             d1 = literal: LDS byte address of its data; copy: output position of its source
-                const uint32_t rel = otok - op;
-                uint32_t d0 = 0, d1 = 0;
-                if (inb) {
-                    const uint32_t kk = lit ? 0u : (far ? 2u : 1u);
-                    const uint32_t aux = far ? frank : ((cp && off < ol) ? 1u : 0u);
-                    d0 = rel | (kk << 10) | (aux << 12) | (min(off, 0xffffu) << 16);
-                    d1 = lit ? S_STAGE_OFF + woff + (srcv - I) : a;
-                }
-                if (lane < int(XBATCH / 32)) sbits[lane] = 0;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (inb) atomicOr(&sbits[rel >> 5], 1u << (rel & 31u));
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                {
-                    const uint32_t c = lane < int(XBATCH / 32) ? __popc(sbits[lane]) : 0u;
-                    const uint32_t e2 = dpp_incl_scan(c) - c;
-                    if (lane < int(XBATCH / 32)) wpre[lane] = e2;
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                bool sbad = false;
-                for (uint32_t w0 = 0; w0 < btot; w0 += 256) {
-                    const uint32_t s0 = op + w0;
-                    uint32_t W[4], xw[4], ti[4], i0[4], i1[4], a8[4], ac[4];
-                    bool act[4], pend[4], isref[4], islit[4];
-                    #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t x = w0 + 64u * uint32_t(u) + uint32_t(lane);
-                        act[u] = x < btot;
-                        xw[u] = act[u] ? x : btot - 1u;
-                    }
-                    #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t wd = xw[u] >> 5;
-                        ti[u] = wpre[wd] + __popc(sbits[wd] & ((2u << (xw[u] & 31u)) - 1u)) - 1u;
-                    }
-                    #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        i0[u] = uint32_t(__builtin_amdgcn_ds_bpermute(int(ti[u] << 2), int(d0)));
-                        i1[u] = uint32_t(__builtin_amdgcn_ds_bpermute(int(ti[u] << 2), int(d1)));
-                    }
-                    #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t jj = xw[u] - (i0[u] & 0x3ffu);
-                        const uint32_t kk = (i0[u] >> 10) & 3u;
-                        const uint32_t aux = (i0[u] >> 12) & 15u;
-                        const uint32_t offv = max(i0[u] >> 16, 1u);
-                        islit[u] = kk == 0u;
-                        const uint32_t r = (kk == 1u && (aux & 1u)) ? mod_small(jj & 63u, offv) : jj;
-                        const uint32_t y = i1[u] + r;                       // copy: output position of the source
-                        isref[u] = SYM && !islit[u] && y < sym_base;        // before this sub-piece
-                        pend[u] = act[u] && !islit[u] && !isref[u] && y >= s0;
-                        a8[u] = islit[u] ? i1[u] + jj : S_STAGE_OFF;        // literal byte (stage)
-                        if constexpr (SYM)
-                            ac[u] = islit[u] ? 0u : (kk == 2u ? S_FBUF_OFF + aux * (S_FBW * 4u) + (i1[u] & 1u) * 2u + 2u * jj
-                                                              : 2u * (y & S_RMASK));
-                        else
-                            ac[u] = islit[u] ? 0u : (kk == 2u ? S_FBUF_OFF + aux * (S_FBW * 4u) + (i1[u] & 3u) + jj
-                                                              : (y & S_RMASK));
-                        const uint32_t d = sym_base - y;
-                        sbad |= act[u] && isref[u] && d > SYM_MAXD;
-                        W[u] = pend[u] ? (SYM_PEND | ((y - s0) & 0xffu)) : (isref[u] ? 256u + d : 0u);
-                    }
-                    #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t lv = uint32_t(sl[min(a8[u], S_SLICE - 1u)]);
-                        uint32_t cv;
-                        if constexpr (SYM) cv = uint32_t(*reinterpret_cast<const uint16_t*>(sl + (min(ac[u], S_SLICE - 2u) & ~1u)));
-                        else cv = uint32_t(sl[min(ac[u], S_SLICE - 1u)]);
-                        const uint32_t val = islit[u] ? lv : cv;
-                        W[u] = (pend[u] || isref[u]) ? W[u] : (act[u] ? val : 0u);
-                    }
-                    // pointer jumping over the window's 256 positions (a source always precedes its reader)
-                    while (__any(W[0] >= SYM_PEND || W[1] >= SYM_PEND || W[2] >= SYM_PEND || W[3] >= SYM_PEND)) {
-                        const uint32_t R01 = W[0] | (W[1] << 16), R23 = W[2] | (W[3] << 16);
-                        uint32_t G[4];
-                        #pragma unroll
-                        for (int u = 0; u < 4; u++) {
-                            const uint32_t pl = W[u] & 0xffu;
-                            const uint32_t g01 = uint32_t(__builtin_amdgcn_ds_bpermute(int((pl & 63u) << 2), int(R01)));
-                            const uint32_t g23 = uint32_t(__builtin_amdgcn_ds_bpermute(int((pl & 63u) << 2), int(R23)));
-                            const uint32_t g = (pl >> 6) < 2u ? g01 : g23;
-                            G[u] = ((pl >> 6) & 1u) ? (g >> 16) : (g & 0xffffu);
-                        }
-                        #pragma unroll
-                        for (int u = 0; u < 4; u++) W[u] = W[u] >= SYM_PEND ? G[u] : W[u];
-                    }
-                    #pragma unroll
-                    for (int u = 0; u < 4; u++)
-                        if (act[u]) put(s0 + 64u * uint32_t(u) + uint32_t(lane), W[u]);
-                }
-                if (__any(sbad)) { bad = true; break; }
-                flush(op + btot);
-            }
-            op += btot;
-            ip = __builtin_amdgcn_readlane(endp, int(used) - 1);
-            sb += used;
-        }
-    }
-    if (bad) return true;
-    // tail [F, op)
-    if constexpr (SYM) {
-        const uint32_t hd = min((8u - (F & 7u)) & 7u, op - F);
-        if (uint32_t(lane) < hd) gcell[F + lane] = ring16[(F + lane) & S_RMASK];
-        F += hd;
-        const uint32_t mid = F + ((op - F) & ~7u);
-        for (uint32_t a = F + uint32_t(lane) * 8u; a < mid; a += 512u)
-            *(PF_GLOBAL u32x4*)(gcell + a) = *reinterpret_cast<const u32x4*>(ring16 + (a & S_RMASK));
-        for (uint32_t a = mid + uint32_t(lane); a < op; a += 64) gcell[a] = ring16[a & S_RMASK];
-    } else {
-        for (uint32_t a = F + uint32_t(lane) * 16u; a + 16u <= op; a += 1024u)
-            *(PF_GLOBAL u32x4*)(gdst + a) = *reinterpret_cast<const u32x4*>(ring8 + (a & S_RMASK));
-        for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) gdst[a] = ring8[a & S_RMASK];
-    }
-    return false;
-}
-
-template <int NSUB>
-__global__ __launch_bounds__(64 * NSUB) void k_snappy_exec_sub(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
-                                                               const uint32_t* __restrict__ splits,
-                                                               const uint2* __restrict__ subsplits, int* __restrict__ fb) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[NSUB * S_SLICE];
-    __shared__ uint32_t s_lo[NSUB + 1], s_ip[NSUB];
-    __shared__ int s_bad;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int2 pc = pieces[blockIdx.x];
-    const int j = pc.x, k = pc.y;
-    if (fb[j] >= FB_REDO) return;
-    const SnappyJob job = jobs[j];
-    const uint32_t* sp = splits + job.split_base;
-    if (k > 0 && sp[k] == SNAP_INVALID) return;   // no token at this mark: an earlier piece covers it
-    if (tid == 0) {
-        uint64_t pos0 = 0, ulen = 0;
-        s_bad = (!uvarint(job.src, job.src_len, pos0, ulen) || ulen != job.dst_len) ? 2 : 0;
-        const uint32_t P = uint32_t(k) * SNAP_BLOCK;
-        uint32_t pe = job.dst_len;
-        for (uint32_t k2 = k + 1; k2 < job.n_pieces; k2++)
-            if (sp[k2] != SNAP_INVALID) { pe = k2 * SNAP_BLOCK; break; }
-        s_lo[0] = P;
-        s_ip[0] = k == 0 ? uint32_t(pos0) : sp[k];
-        const uint2* ss = subsplits + size_t(job.split_base + uint32_t(k)) * (SNAP_SUBS - 1);
-        for (int w = 1; w < NSUB; w++) {
-            const uint2 e = ss[w * (int(SNAP_SUBS) / NSUB) - 1];
-            s_lo[w] = e.x == SNAP_INVALID ? SNAP_INVALID : e.y;
-            s_ip[w] = e.x;
-        }
-        s_lo[NSUB] = pe;
-    }
-    __syncthreads();
-    if (s_bad == 2) {
-        if (tid == 0) atomicMax(&fb[j], FB_SERIAL);
-        return;
-    }
-    auto end_of = [&](int w) {
-        for (int w2 = w + 1; w2 < NSUB; w2++)
-            if (s_lo[w2] != SNAP_INVALID) return s_lo[w2];
-        return s_lo[NSUB];
-    };
-    const uint32_t P = s_lo[0];
-    bool bad = false;
-    const uint32_t my_lo = s_lo[wave];
-    if (my_lo != SNAP_INVALID) {
-        const uint32_t e = end_of(wave);
-        if (e > my_lo) {
-            if (wave == 0) bad = sub_exec<false>(job, s_ip[0], P, e, P, P, lds, lane);
-            else bad = sub_exec<true>(job, s_ip[wave], my_lo, e, P, my_lo, lds + wave * S_SLICE, lane);
-        }
-    }
-    if (bad && lane == 0) atomicOr(&s_bad, 1);
-    __threadfence_block();
-    __syncthreads();
-    if (s_bad) {
-        if (tid == 0) atomicMax(&fb[j], FB_REDO);
-        return;
-    }
-    // resolution, sub-piece by sub-piece: value cells -> bytes, reference cells -> the final byte
-    const PF_GLOBAL uint16_t* gcell = gptr(job.cells);
-    PF_GLOBAL uint8_t* gdst = gptr(job.dst);
-    for (int w = 1; w < NSUB; w++) {
-        const uint32_t lo = s_lo[w];
-        if (lo == SNAP_INVALID) continue;
-        const uint32_t hi = end_of(w);
-        const uint32_t lo8 = min((lo + 7u) & ~7u, hi), hi8 = max(lo8, hi & ~7u);
-        for (uint32_t i = lo + uint32_t(tid); i < lo8; i += 64u * NSUB) {
-            const uint32_t c = gcell[i];
-            gdst[i] = uint8_t(c < 256u ? c : gdst[lo - (c - 256u)]);
-        }
-        for (uint32_t i = hi8 + uint32_t(tid); i < hi; i += 64u * NSUB) {
-            const uint32_t c = gcell[i];
-            gdst[i] = uint8_t(c < 256u ? c : gdst[lo - (c - 256u)]);
-        }
-        for (uint32_t b = lo8 + 8u * uint32_t(tid); b < hi8; b += 8u * 64u * NSUB) {
-            const u32x4 c4 = *(const PF_GLOBAL u32x4*)(gcell + b);
-            uint32_t cc[8] = {c4.x & 0xffffu, c4.x >> 16, c4.y & 0xffffu, c4.y >> 16,
-                              c4.z & 0xffffu, c4.z >> 16, c4.w & 0xffffu, c4.w >> 16};
-            uint32_t by[8];
-            #pragma unroll
-            for (int u = 0; u < 8; u++) by[u] = cc[u] < 256u ? cc[u] : uint32_t(gdst[lo - (cc[u] - 256u)]);
-            const uint64_t v = uint64_t(by[0] | (by[1] << 8) | (by[2] << 16) | (by[3] << 24)) |
-                               (uint64_t(by[4] | (by[5] << 8) | (by[6] << 16) | (by[7] << 24)) << 32);
-            *(PF_GLOBAL uint64_t*)(gdst + b) = v;
-        }
-        __threadfence_block();
-        __syncthreads();
-    }
-}
-
 #ifdef PF_STAMPS
 extern "C" int pf_debug_stamps(unsigned long long* out, int n, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_stamps), sizeof(unsigned long long) * (n < 16 ? n : 16)) != hipSuccess) return -1;
@@ -2066,56 +1358,44 @@ void launch_snappy_serial(const SnappyJob*, int, const int*, DevChunkResult*, hi
 
 // Parse stage (token-start bitmaps, chain, 64 KiB split points) and execute stage, separately so
 // the runtime can time them apart.
-int snappy_exec_mode();
-
 void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
-                         SnapEnt* d_ent, uint32_t* d_lane_out, uint32_t* d_splits, uint2* d_subsplits, int* d_fb,
-                         hipStream_t s) {
+                         SnapEnt* d_ent, uint32_t* d_lane_out, uint32_t* d_splits, int* d_fb, hipStream_t s) {
     if (n_jobs <= 0) return;
     hipLaunchKernelGGL(k_snappy_index, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, d_win, d_ent, d_lane_out, d_fb);
     hipLaunchKernelGGL(k_snappy_chain, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_win, (const SnapEnt*)d_ent, d_lane_out, d_fb);
     hipLaunchKernelGGL(k_snappy_repair, dim3(std::min(n_wins, 1024)), dim3(64), 0, s, d_jobs, d_wins, n_wins,
                        (const SnapWin*)d_win, d_lane_out, d_fb);
-    // sub-piece boundaries only for the sub-piece executor (PF_EXEC=3)
     hipLaunchKernelGGL(k_snappy_splits, dim3(n_jobs), dim3(64), 0, s, d_jobs, (const SnapWin*)d_win,
-                       (const uint32_t*)d_lane_out, d_splits, snappy_exec_mode() == 3 ? d_subsplits : nullptr, d_fb);
+                       (const uint32_t*)d_lane_out, d_splits, d_fb);
 }
 
-int snappy_exec_mode() {
-    // PF_EXEC=1: token-serial executor v1; 2: byte-lane executor v2; default (3): sub-piece executor
-    // (PF_NSUB=2 or 4 sub-pieces per 64 KiB piece, default 4)
-    static const int m = [] { const char* e = std::getenv("PF_EXEC"); return e && e[0] >= '1' && e[0] <= '3' ? e[0] - '0' : 2; }();
-    return m;
+void launch_snappy_exec_wg(const SnappyJob*, const int2*, int, const uint32_t*, int*, int*, hipStream_t);
+
+// PF_XW=0: every piece goes to the single-wave executor (A/B); default: workgroup executor first.
+bool snappy_wg_enabled() {
+    static const bool on = [] { const char* e = std::getenv("PF_XW"); return !(e && e[0] == '0'); }();
+    return on;
 }
 
-void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
-                        const uint2* d_subsplits, int* d_fb, DevChunkResult* d_res, hipStream_t s) {
+void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_pieces, int n_pieces, int n_wg,
+                        uint32_t* d_splits, int* d_fb, int* d_pdone, DevChunkResult* d_res, hipStream_t s) {
     if (n_jobs <= 0) return;
-    static const int nsub = [] { const char* e = std::getenv("PF_NSUB"); return e && e[0] == '2' ? 2 : 4; }();
-    const int mode = snappy_exec_mode();
-    if (mode == 3 && d_subsplits) {
-        if (nsub == 2)
-            hipLaunchKernelGGL(k_snappy_exec_sub<2>, dim3(n_pieces), dim3(128), 0, s, d_jobs, d_pieces,
-                               (const uint32_t*)d_splits, d_subsplits, d_fb);
-        else
-            hipLaunchKernelGGL(k_snappy_exec_sub<4>, dim3(n_pieces), dim3(256), 0, s, d_jobs, d_pieces,
-                               (const uint32_t*)d_splits, d_subsplits, d_fb);
-    } else {
-        const auto kx = mode == 1 ? k_snappy_exec : k_snappy_exec2;
-        hipLaunchKernelGGL(kx, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
-    }
+    const bool wg = snappy_wg_enabled() && d_pdone && n_wg > 0;
+    if (wg) launch_snappy_exec_wg(d_jobs, d_pieces, n_wg, d_splits, d_fb, d_pdone, s);
+    hipLaunchKernelGGL(k_snappy_exec2, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb,
+                       (const int*)(wg ? d_pdone : nullptr), 0);
     // whole-page redo of pages whose pieces were not independent
-    hipLaunchKernelGGL(mode == 1 ? k_snappy_exec : k_snappy_exec2, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces,
-                       (const uint32_t*)d_splits, d_fb, 1);
+    hipLaunchKernelGGL(k_snappy_exec2, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb,
+                       (const int*)nullptr, 1);
     launch_snappy_serial(d_jobs, n_jobs, d_fb, d_res, s);
 }
 
-// All Snappy work of one batch, in stream order. fb must be zero on entry.
+// All Snappy work of one batch, in stream order. fb and pdone must be zero on entry.
 void launch_snappy(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
-                   SnapEnt* d_ent, uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
-                   uint2* d_subsplits, int* d_fb, DevChunkResult* d_res, hipStream_t s) {
-    launch_snappy_parse(d_jobs, n_jobs, d_wins, n_wins, d_win, d_ent, d_lane_out, d_splits, d_subsplits, d_fb, s);
-    launch_snappy_exec(d_jobs, n_jobs, d_pieces, n_pieces, d_splits, d_subsplits, d_fb, d_res, s);
+                   SnapEnt* d_ent, uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, int n_wg, uint32_t* d_splits,
+                   int* d_fb, int* d_pdone, DevChunkResult* d_res, hipStream_t s) {
+    launch_snappy_parse(d_jobs, n_jobs, d_wins, n_wins, d_win, d_ent, d_lane_out, d_splits, d_fb, s);
+    launch_snappy_exec(d_jobs, n_jobs, d_pieces, n_pieces, n_wg, d_splits, d_fb, d_pdone, d_res, s);
 }
 
 }  // namespace pf

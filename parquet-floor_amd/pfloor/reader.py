@@ -12,8 +12,13 @@ call order, error behaviour), Hydrator.java and HydratorSupplier.java:
   * any failure while iterating -> RuntimeError("Failed to read parquet") from the cause (:209-211)
   * trySplit() -> None, estimateSize() = total rows, characteristics ORDERED|NONNULL|DISTINCT
 Decoding happens per row group on the GPU (one batch of the selected column chunks);
-only the row assembly loop (a1) runs on the host, as the Java adapter would.
+only the row assembly loop (a1) runs on the host, as the Java adapter would. With several
+devices (`devices=[...]`) row groups are dealt round-robin to per-device contexts and decoded
+ahead of the row loop (north_star: row groups sharded across the GPUs of a node, no collective);
+rows still come out in file order, as the reference's single ORDERED stream delivers them
+(ParquetReader.java:176-212, :225-227).
 """
+import collections
 import struct
 import uuid as _uuid
 
@@ -209,18 +214,96 @@ class _ColumnCursor:
         self.e += 1
 
 
+class RowGroupPipeline:
+    """Row groups decoded ahead of the consumer on one or more devices, delivered in file order.
+
+    Row group g goes to device slot g % G (G = len(devices)); each device has `depth` contexts
+    on one HIP stream (pf_ctx_create_shared), so up to G * depth row groups are in flight: the
+    chunk bytes of g are read into its context's pinned staging buffer and the decode enqueued
+    (pf_decode_row_group is asynchronous); `take(g)` waits for g (pf_wait) and copies its columns
+    to the host. A context is reused only after its previous row group was taken, so its staging
+    buffer and output arenas are never overwritten while in use."""
+
+    def __init__(self, reader, columns, row_groups, devices=(0,), depth=2):
+        if not devices:
+            raise ValueError("devices must not be empty")
+        self.reader = reader
+        self.columns = columns
+        self.row_groups = list(row_groups)
+        self.depth = max(1, int(depth))
+        self.decs = []   # [device slot][k]
+        try:
+            for d in devices:
+                first = GpuDecoder(d)
+                slot = [first]
+                for _ in range(self.depth - 1):
+                    slot.append(GpuDecoder(share=first))
+                self.decs.append(slot)
+        except Exception:
+            self.close()
+            raise
+        self.inflight = collections.OrderedDict()   # position in row_groups -> decoder, or the enqueue error
+        self.next_enqueue = 0
+
+    def _decoder(self, i):
+        g = len(self.decs)
+        return self.decs[i % g][(i // g) % self.depth]
+
+    def _enqueue(self, i):
+        rg = self.row_groups[i]
+        dec = self._decoder(i)
+        try:
+            idx = [c.index for c in self.columns]
+            items, total = self.reader.plan([rg], idx)
+            buf = dec.staging(total)
+            descs = []
+            for _rg, col, s, n, off in items:
+                if n:
+                    self.reader.read_into(s, n, buf.ptr.value + off)
+                descs.append(self.reader.chunk_desc(rg, col, off))
+            dec.decode(descs, buf.ptr.value, max(total, 1))
+            self.inflight[i] = dec
+        except Exception as e:   # surfaces when row group i is reached, as readNextRowGroup would raise it
+            self.inflight[i] = e
+
+    def take(self, i):
+        """Decoded columns of row_groups[i] (list of per-column array dicts); i must be taken in order."""
+        window = len(self.decs) * self.depth
+        while self.next_enqueue < len(self.row_groups) and self.next_enqueue < i + window:
+            self._enqueue(self.next_enqueue)
+            self.next_enqueue += 1
+        dec = self.inflight.pop(i)
+        if isinstance(dec, Exception):
+            raise dec
+        rc = dec.wait()
+        if rc != 0:
+            raise RuntimeError(dec.error())
+        return [dec.fetch(k, c.physical_type, c.max_def, c.max_rep) for k, c in enumerate(self.columns)]
+
+    def close(self):
+        for dec in self.inflight.values():
+            if not isinstance(dec, Exception):
+                dec.wait()
+        self.inflight.clear()
+        for slot in self.decs:
+            for dec in reversed(slot):   # shared contexts before the stream's owner
+                dec.close()
+        self.decs = []
+
+
 class ParquetReader:
     """Spliterator-like reader (ParquetReader.java:34-260)."""
 
     # --- static factories (ParquetReader.java:47-84) ---
     @staticmethod
-    def streamContent(file, hydratorSupplier, columns=None, device=0):
-        return ParquetReader.stream(ParquetReader.spliterator(file, hydratorSupplier, columns, device))
+    def streamContent(file, hydratorSupplier, columns=None, device=0, devices=None):
+        return ParquetReader.stream(ParquetReader.spliterator(file, hydratorSupplier, columns, device, devices))
 
     @staticmethod
-    def spliterator(file, hydratorSupplier, columns=None, device=0):
+    def spliterator(file, hydratorSupplier, columns=None, device=0, devices=None):
+        """devices: GPUs to deal the row groups over (default [device]); rows stay in file order."""
         column_set = frozenset() if columns is None else frozenset(columns)
-        return ParquetReader(str(file), column_set, hydratorSupplier, device)
+        return ParquetReader(str(file), column_set, hydratorSupplier, device, devices)
 
     @staticmethod
     def stream(reader):
@@ -259,7 +342,7 @@ class ParquetReader:
         return f
 
     # --- instance (ParquetReader.java:119-131) ---
-    def __init__(self, path, column_names, hydrator_supplier, device=0):
+    def __init__(self, path, column_names, hydrator_supplier, device=0, devices=None):
         try:
             self.reader = ParquetFile(path)
         except Exception as e:
@@ -271,8 +354,8 @@ class ParquetReader:
         self.current_row_group_size = -1
         self.current_row_index = -1
         self.cursors = None
-        self._device = device
-        self._dec = None
+        self._devices = list(devices) if devices else [device]
+        self._pipe = None
 
     def _read_next_row_group(self):
         self.current_rg += 1
@@ -282,24 +365,10 @@ class ParquetReader:
         if self.reader.row_group_rows(rg) == 0:
             # parquet-mr 1.12.2 ParquetFileReader.readNextRowGroup [upstream, restated]
             raise RuntimeError("Illegal row group of 0 rows")
-        if self._dec is None:
-            self._dec = GpuDecoder(self._device)
-        idx = [c.index for c in self.columns]
-        items, total = self.reader.plan([rg], idx)
-        buf = self._dec.staging(total)
-        descs = []
-        for _rg, col, s, n, off in items:
-            if n:
-                self.reader.read_into(s, n, buf.ptr.value + off)
-            descs.append(self.reader.chunk_desc(rg, col, off))
-        self._dec.decode(descs, buf.ptr.value, max(total, 1))
-        rc = self._dec.wait()
-        if rc != 0:
-            raise RuntimeError(self._dec.error())
-        self.cursors = []
-        for i, c in enumerate(self.columns):
-            arrays = self._dec.fetch(i, c.physical_type, c.max_def, c.max_rep)
-            self.cursors.append(_ColumnCursor(c, arrays))
+        if self._pipe is None:
+            self._pipe = RowGroupPipeline(self.reader, self.columns, range(self.reader.num_row_groups), self._devices)
+        arrays = self._pipe.take(rg)
+        self.cursors = [_ColumnCursor(c, a) for c, a in zip(self.columns, arrays)]
         self.current_row_group_size = self.reader.row_group_rows(rg)
         self.current_row_index = 0
         return True
@@ -338,9 +407,9 @@ class ParquetReader:
         return self.reader
 
     def close(self):
-        if self._dec is not None:
-            self._dec.close()
-            self._dec = None
+        if self._pipe is not None:
+            self._pipe.close()
+            self._pipe = None
         self.reader.close()
 
 
