@@ -55,9 +55,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PCIE_GBS = 63.0         # MI355X_MICROARCH.md: PCIe Gen5 x16 per direction
 # kernels of each stage (rocprof names), for the PMC traffic and the label of the roofline object
 STAGE_KERNELS = {"snappy_exec": r"k_snappy_exec", "snappy_parse": r"k_snappy_(index|chain)$",
-                 "flat": r"k_flat(_fixed|_null)?$", "decode": r"k_decode$"}
+                 "flat": r"k_flat(_fixed|_null)?$", "decode": r"k_decode$", "delta": r"k_delta$",
+                 "count": r"k_count(_flat)?$"}
 STAGE_LABEL = {"snappy_exec": "k_snappy_exec2 (Snappy executor stage)", "snappy_parse": "k_snappy_index + k_snappy_chain",
-               "flat": "flat stage: k_flat_fixed + k_flat_null + k_flat", "decode": "k_decode"}
+               "flat": "flat stage: k_flat_fixed + k_flat_null + k_flat", "decode": "k_decode",
+               "delta": "k_delta (DELTA_BINARY_PACKED)", "count": "count stage: k_count_flat + k_count"}
 ROOF_PASSES = 3         # isolated decodes of context 0's first batch for the roofline kernel time
 E2E_PASSES = 2
 METRIC = "decoded GB/s + rows/s (node), lineitem-shape Snappy+dict, 1/2/4/8 GPUs"
@@ -67,6 +69,10 @@ WORKLOADS = {
     "sf1": dict(rows=SF1_ROWS, rg_rows=RG_ROWS, seed=SEED, kind="lineitem", batch=0),
     "sf100": dict(rows=8_000_000, rg_rows=4_000_000, seed=43, kind="lineitem", batch=1, logical=150),
     "wide": dict(rows=1_000_000, rg_rows=1_000_000, seed=4, kind="wide", batch=1),
+    # (configs[4]) l optional LIST<STRUCT<a INT64 (DELTA_BINARY_PACKED), b UTF8 (dictionary)>>, v2 pages
+    "nested": dict(rows=1_000_000, rg_rows=250_000, seed=5, kind="nested", batch=1),
+    # (configs[0]) INT64 / DOUBLE / nullable INT32 / dictionary UTF8, uncompressed
+    "flat": dict(rows=1_000_000, rg_rows=250_000, seed=1, kind="flat", batch=1),
 }
 
 
@@ -88,13 +94,21 @@ def make_input(args):
     w = WORKLOADS[args.workload]
     t0 = time.time()
     os.makedirs(args.data_dir, exist_ok=True)
+    kw = dict(compression="snappy")
     if w["kind"] == "lineitem":
         # sf100's row groups are SF100-shaped (key ranges of the full 600M-row file)
         t = datagen.lineitem_table(w["rows"], seed=w["seed"], scale=100.0 if args.workload == "sf100" else None)
+    elif w["kind"] == "nested":
+        t = datagen.nested_table(w["rows"], seed=w["seed"])
+        kw = dict(compression="snappy", data_page_version="2.0",
+                  column_encoding={"l.list.element.a": "DELTA_BINARY_PACKED"}, use_dictionary=["l.list.element.b"])
+    elif w["kind"] == "flat":
+        t = datagen.flat_table(w["rows"], seed=w["seed"])
+        kw = dict(compression="NONE")
     else:
         t = datagen.wide_table(w["rows"], seed=w["seed"])
     tmp = path + f".tmp{os.getpid()}"
-    pq.write_table(t, tmp, compression="snappy", row_group_size=w["rg_rows"])
+    pq.write_table(t, tmp, row_group_size=w["rg_rows"], **kw)
     os.replace(tmp, path)
     log(f"[bench] wrote {path} ({os.path.getsize(path) / 1e6:.1f} MB) in {time.time() - t0:.1f}s")
     return path
@@ -199,7 +213,7 @@ class BatchInput:
 
 def page_stats(descs):
     """Algorithmic byte counts from the page headers."""
-    comp = uncomp = snappy_in = snappy_out = 0
+    comp = uncomp = snappy_in = snappy_out = dbp_body = dbp_values = 0
     pages = 0
     for d in descs:
         for i in range(d.n_pages):
@@ -211,7 +225,11 @@ def page_stats(descs):
             if d.codec == 1 and (p.page_type != 3 or p.is_compressed):
                 snappy_in += p.compressed_size - lvl
                 snappy_out += p.uncompressed_size - lvl
-    return dict(pages=pages, compressed=comp, uncompressed=uncomp, snappy_in=snappy_in, snappy_out=snappy_out)
+            if p.encoding == 5 and p.page_type in (0, 3):   # DELTA_BINARY_PACKED data page
+                dbp_body += p.uncompressed_size - lvl
+                dbp_values += p.num_values
+    return dict(pages=pages, compressed=comp, uncompressed=uncomp, snappy_in=snappy_in, snappy_out=snappy_out,
+                dbp_body=dbp_body, dbp_values=dbp_values)
 
 
 def chunk_decoded_bytes(col, ci):
@@ -568,7 +586,7 @@ def main():
         pmc = {"error": "skipped: bench.py is running under a profiler"}
     elif world == 1 and not args.no_pmc:
         try:
-            pmc = measure_pmc(args, "k_snappy_exec|k_snappy_index|k_snappy_chain|k_flat|k_decode")
+            pmc = measure_pmc(args, "k_snappy_exec|k_snappy_index|k_snappy_chain|k_flat|k_decode|k_delta|k_count")
         except Exception as e:
             pmc = {"error": repr(e)}
 
@@ -671,6 +689,8 @@ def main():
         "snappy_parse": st0["snappy_in"],                       # compressed read (token index)
         "flat": st0["uncompressed"] + dbytes0,                  # page bodies read + decoded bytes written
         "decode": st0["uncompressed"] + dbytes0,
+        "delta": st0["dbp_body"] + 8 * st0["dbp_values"],      # DBP values sections read + 8-B values written
+        "count": st0["uncompressed"],                            # page bodies read (levels / lengths / ids)
     }
     dom = max((k for k in iso if k in kern_bytes), key=lambda k: iso.get(k, 0.0))
     dom_ms = iso.get(dom, 0.0)
@@ -701,12 +721,26 @@ def main():
                 e2e_plan = [[[(g, p, cs[i::k]) for g, p, cs in units] for units in bl for i in range(k)]
                             for bl in e2e_plan]
             e2e_batches = [[BatchInput(pf, units, decs[0].h) for units in bl] for bl in e2e_plan]
-            e2e = measure_e2e(decs[:len(e2e_batches)], e2e_batches, pf, st_all, args.e2e_copy)
+            e2e = measure_e2e(decs[:len(e2e_batches)], e2e_batches, pf, st_all, args.e2e_copy,
+                              barrier=dist.barrier if dist else None)
             for bl in e2e_batches:
                 for bi in bl:
                     bi.host.free()
         except Exception as e:
             e2e = {"error": repr(e)}
+        if dist:   # node E2E: bytes of all ranks / slowest rank's pass (barrier-aligned passes)
+            import torch as _t
+            ok = e2e is not None and "ms_per_pass" in e2e
+            v = _t.tensor([e2e["ms_per_pass"] if ok else 0.0, e2e["decoded_bytes"] if ok else 0.0, 1.0 if ok else 0.0],
+                          dtype=_t.float64)
+            mx = v.clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(v, op=dist.ReduceOp.SUM)
+            if ok and int(v[2].item()) == world:
+                e2e["node"] = {"value": round(float(v[1].item()) / (float(mx[0].item()) * 1e-3) / 1e9, 3),
+                               "unit": "decoded GB/s, all ranks (sum of decoded bytes / max pass time)",
+                               "n_gpus": world, "ms_per_pass_max": round(float(mx[0].item()), 3),
+                               "pcie_bound_gbs_node": PCIE_GBS * world}
 
     # ---- write path: row group 0 re-encoded on the GPU and read back ----
     write = None
@@ -726,6 +760,15 @@ def main():
     elif args.workload == "sf100":
         wl = (f"lineitem SF100-shaped ({n_log} row groups of {w['rg_rows']} rows = {n_log * w['rg_rows']} rows; the "
               f"{pf.num_row_groups} distinct synthetic row groups stand for the {n_log}), Snappy + dictionary, device-resident")
+        scaling = "strong"
+    elif args.workload == "nested":
+        wl = (f"nested: {w['rows']} rows of l optional LIST<STRUCT<a INT64 DELTA_BINARY_PACKED, b UTF8 dictionary>> "
+              f"(lengths 0-4, 10% null lists, 5% null elements / leaves), v2 pages, Snappy, {pf.num_row_groups} row groups, "
+              "device-resident")
+        scaling = "strong"
+    elif args.workload == "flat":
+        wl = (f"flat: {w['rows']} rows (id INT64, x DOUBLE, n nullable INT32, s dictionary UTF8), uncompressed, "
+              f"{pf.num_row_groups} row groups, device-resident")
         scaling = "strong"
     else:
         wl = (f"wide: {w['rows']} rows x {pf.num_columns} nullable INT32/FLOAT columns, 30% nulls, 100K-value dictionaries, "
@@ -864,7 +907,7 @@ def measure_write(path, pf, dec, passes=3, decs=None):
             "passes": passes}
 
 
-def measure_e2e(decs, batches, pf, st_all, copy_mode="batch"):
+def measure_e2e(decs, batches, pf, st_all, copy_mode="batch", barrier=None):
     """Whole rank share, E2E_PASSES times: per context, per batch: pinned H2D of the batch's chunk
     bytes (inside pf_decode_row_group), decode, pf_wait, then the D2H of the decoded columns into
     pinned host memory — copy_mode "batch": pf_copy_batch_async, one copy per output arena (3 per
@@ -887,7 +930,7 @@ def measure_e2e(decs, batches, pf, st_all, copy_mode="batch"):
             row.append(infos)
         layouts.append(row)
     if copy_mode == "batch":
-        return _e2e_batch(decs, batches, layouts, pf)
+        return _e2e_batch(decs, batches, layouts, pf, barrier)
     # pinned output buffers: one per context, sized for its largest batch
     outs = []
     for ctx_i, (d, bl) in enumerate(zip(decs, batches)):
@@ -996,8 +1039,9 @@ def measure_link(nbytes, reps=3):
         return {"error": repr(e)}
 
 
-def _e2e_batch(decs, batches, layouts, pf):
-    """measure_e2e with pf_copy_batch_async: one pinned buffer per context (its largest batch)."""
+def _e2e_batch(decs, batches, layouts, pf, barrier=None):
+    """measure_e2e with pf_copy_batch_async: one pinned buffer per context (its largest batch).
+    barrier (N > 1): aligns the ranks' timed passes, so the node rate is sum(bytes) / max(time)."""
     from pfloor import _native
     from pfloor.decoder import PinnedBuffer
     L = _native.lib()
@@ -1040,9 +1084,13 @@ def _e2e_batch(decs, batches, layouts, pf):
         if errs:
             raise errs[0]
     one_pass()
+    if barrier:
+        barrier()
     t0 = time.perf_counter()
     for _ in range(E2E_PASSES):
         one_pass()
+    if barrier:
+        barrier()
     dt = (time.perf_counter() - t0) / E2E_PASSES
     for b in bufs:
         b.free()

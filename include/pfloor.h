@@ -324,7 +324,8 @@ typedef struct pf_encoded_chunk {
 /* Encode one column chunk on the context's GPU. Inputs are host memory (copied) unless
  * on_device != 0. Synchronous. */
 int pf_encode_chunk(pf_ctx* ctx, const pf_encode_column* col, int on_device, pf_encoded_chunk* out);
-/* Snappy-compress one buffer on the GPU (64 KiB blocks, one wave each). Host buffers, synchronous;
+/* Snappy-compress one buffer on the GPU: independent 8 KiB jobs (one wave each; a job's matches stay
+ * inside it, so tokens never cross a 64 KiB output boundary). Host buffers, synchronous;
  * *out_len = compressed length (cap >= 32 + n + n / 6 always suffices). */
 int pf_snappy_compress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
 

@@ -2069,7 +2069,10 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
                 const uint64_t nb = (h >> 1) * uint64_t(bw);
                 data = pos * 8u;
                 packed = 1;
-                pos += uint32_t(nb < uint64_t(dn - pos) ? nb : uint64_t(dn - pos));   // truncated (parquet-mr)
+                // a run truncated by the section end (parquet-mr reads what is there and zero-pads):
+                // the page goes to k_flat / k_decode, whose level reads are zero past the section
+                if (nb > uint64_t(dn - pos)) { ok = 0; break; }
+                pos += uint32_t(nb);
             } else {
                 cnt = h >> 1;
                 const uint32_t nbv = uint32_t(bw + 7) >> 3;

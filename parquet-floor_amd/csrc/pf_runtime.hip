@@ -24,11 +24,10 @@
 #include "pfloor.h"
 
 namespace pf {
-void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, const int2*, int, int, uint32_t*,
-                   int*, int*, DevChunkResult*, hipStream_t);
+void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, const int2*, int, uint32_t*,
+                   int*, DevChunkResult*, hipStream_t);
 void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, int*, hipStream_t);
-void launch_snappy_exec(const SnappyJob*, int, const int2*, int, int, uint32_t*, int*, int*, DevChunkResult*, hipStream_t);
-bool snappy_wg_enabled();
+void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*, DevChunkResult*, hipStream_t);
 void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
@@ -135,7 +134,6 @@ struct pf_ctx {
     std::vector<SnappyJob> jobs;
     std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode, l_runs, l_dlen, l_dba, l_lvl;
     std::vector<int2> wins, pieces;       // Snappy index windows / 64 KiB pieces (job, index)
-    int n_wg_pieces = 0;                   // pieces[0, n) are dense: the workgroup executor takes them
     std::vector<BaJob> bajobs;             // PLAIN BYTE_ARRAY walks: dictionary pages, then data pages
     std::vector<int2> ba_tiles;            // (job relative to its batch, tile)
     int n_ba_dict = 0, n_ba_dict_tiles = 0;
@@ -151,7 +149,6 @@ struct pf_ctx {
     size_t out_bytes = 0;                  // values / offsets / levels arena extent of the last decode
     size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
     size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0, off_bajobs = 0, off_batiles = 0;
-    size_t off_pdone = 0;                  // per Snappy piece: 1 = decoded by k_snappy_exec_wg
     uint64_t chars_need = 0;
     const uint8_t* d_bytes = nullptr;
     int reruns = 0;
@@ -216,7 +213,6 @@ int enqueue_kernels(pf_ctx* ctx) {
     uint32_t* d_splits = reinterpret_cast<uint32_t*>(meta + ctx->off_splits);
     int* d_fallback = reinterpret_cast<int*>(meta + ctx->off_fallback);
     const int2* d_wins = reinterpret_cast<const int2*>(meta + ctx->off_wins);
-    int* d_pdone = reinterpret_cast<int*>(meta + ctx->off_pdone);
 
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
     EVREC(ctx, ctx->ev[1], st);
@@ -226,13 +222,12 @@ int enqueue_kernels(pf_ctx* ctx) {
     if (ctx->exec_stream) {
         HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->exec_stream, ctx->ev_fork, 0));
-        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), ctx->n_wg_pieces, d_splits,
-                           d_fallback, d_pdone, d_res, ctx->exec_stream);
+        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res,
+                           ctx->exec_stream);
         HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->exec_stream));
         HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_join, 0));
     } else {
-        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), ctx->n_wg_pieces, d_splits,
-                           d_fallback, d_pdone, d_res, st);
+        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res, st);
     }
     EVREC(ctx, ctx->ev[3], st);
     BaJob* d_bajobs = reinterpret_cast<BaJob*>(meta + ctx->off_bajobs);
@@ -266,16 +261,6 @@ int enqueue_kernels(pf_ctx* ctx) {
                                d_chunks, sizeof(DevChunk) * ctx->n_chunks, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipEventRecord(ctx->ev_done, st));
     return PF_OK;
-}
-
-// Workgroup-executor routing window (compressed bytes per 64 KiB piece); PF_XW_LO / PF_XW_HI (KiB).
-uint64_t wg_lo() {
-    static const uint64_t v = [] { const char* e = std::getenv("PF_XW_LO"); return (e ? std::strtoull(e, nullptr, 10) : 12ull) << 10; }();
-    return v;
-}
-uint64_t wg_hi() {
-    static const uint64_t v = [] { const char* e = std::getenv("PF_XW_HI"); return (e ? std::strtoull(e, nullptr, 10) : 56ull) << 10; }();
-    return v;
 }
 
 // Snappy tables of the batch's jobs: 8 KiB index windows and 64 KiB pieces. d_tokmap holds, per
@@ -314,24 +299,13 @@ int plan_snappy(pf_ctx* ctx) {
             ctx->pieces[pi++] = int2{int(j), int(k)};
         }
     }
-    // Dense pieces (many tokens per 64 KiB: compressed bytes per piece in [lo, hi)) go first and to the
-    // workgroup executor (k_snappy_exec_wg, ~10x lower latency per dense piece, one piece per CU);
-    // light and incompressible pieces to the single-wave executor, which runs many pieces per CU.
-    ctx->n_wg_pieces = 0;
-    if (lpt) {   // (dense first), descending cost, ties in page order
-        const uint64_t lo = wg_lo(), hi = wg_hi();
-        auto dense = [&](uint64_t key) { const uint64_t c = key >> 32; return snappy_wg_enabled() && c >= lo && c < hi; };
-        std::sort(keyed.begin(), keyed.end(), [&](uint64_t a, uint64_t b) {
-            const bool da = dense(a), db = dense(b);
-            if (da != db) return da;
+    if (lpt) {   // descending cost, ties in page order
+        std::sort(keyed.begin(), keyed.end(), [](uint64_t a, uint64_t b) {
             const uint64_t ca = a >> 32, cb = b >> 32;
             return ca != cb ? ca > cb : uint32_t(a) < uint32_t(b);
         });
         std::vector<int2> sorted(tp);
-        for (size_t i = 0; i < tp; i++) {
-            sorted[i] = ctx->pieces[size_t(uint32_t(keyed[i]))];
-            if (dense(keyed[i])) ctx->n_wg_pieces++;
-        }
+        for (size_t i = 0; i < tp; i++) sorted[i] = ctx->pieces[size_t(uint32_t(keyed[i]))];
         ctx->pieces.swap(sorted);
     }
     const size_t tok_bytes = size_t(n_win) * SNAP_WWORDS * 4, lo_bytes = size_t(n_win) * 64 * 4;
@@ -497,7 +471,9 @@ extern "C" int pf_encode_chunk(pf_ctx* ctx, const pf_encode_column* col, int on_
     const int w = pt == PF_BOOLEAN ? 1 : type_width(pt, 0);
     int64_t page_rows = col->page_rows > 0 ? col->page_rows : 20000;
     page_rows = (page_rows + 7) / 8 * 8;   // definition levels of a page start on a validity byte
-    const int64_t dict_limit = col->dict_page_limit > 0 ? col->dict_page_limit : (1 << 20);
+    // dictionary page limit (parquet.dictionary.page.size, 1 MiB); capped so a dictionary that passes it
+    // always fits the 32-bit offsets of the dictionary kernels
+    const int64_t dict_limit = std::min<int64_t>(col->dict_page_limit > 0 ? col->dict_page_limit : (1 << 20), 0x7fffffff);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     if (ctx->copies_pending) HIPCHK(ctx, hipStreamSynchronize(st));
@@ -592,7 +568,11 @@ extern "C" int pf_encode_chunk(pf_ctx* ctx, const pf_encode_column* col, int on_
     EVREC(ctx, ctx->ev[2], st);
     if (n) HIPCHK(ctx, enc_dense(ea, temp, temp_bytes, st));
     if (str) HIPCHK(ctx, enc_plain_sizes(ea, m, temp, temp_bytes, st));
-    const bool want_dict = col->dictionary && pt != PF_BOOLEAN && m > 0;
+    // The device sums dictionary bytes in 32 bits: a BYTE_ARRAY column whose dictionary could reach 4 GiB
+    // (all values distinct: 4 m + chars) is written PLAIN (conservative: such a dictionary is over any
+    // page limit unless most values repeat; parity with parquet-mr's writer is unpinned).
+    const bool dict_fits32 = !str || 4ull * uint64_t(m) + uint64_t(col->chars_len) < (1ull << 32);
+    const bool want_dict = col->dictionary && pt != PF_BOOLEAN && m > 0 && dict_fits32;
     uint32_t hres[3] = {0, 0, 0};   // collide, dictionary entries, dictionary bytes
     float enc_ms = 0.f;
     if (want_dict) {
@@ -607,9 +587,10 @@ extern "C" int pf_encode_chunk(pf_ctx* ctx, const pf_encode_column* col, int on_
     int fallback = 0;
     if (col->dictionary && pt == PF_BOOLEAN) fallback = 3;
     else if (want_dict && hres[0]) fallback = 2;
-    else if (want_dict && int64_t(hres[2]) > dict_limit) fallback = 1;
+    else if (col->dictionary && pt != PF_BOOLEAN && m > 0 && !dict_fits32) fallback = 1;
+    else if (want_dict && (str ? int64_t(hres[2]) : int64_t(hres[1]) * w) > dict_limit) fallback = 1;   // fixed: D * w on the host
     const bool dict = want_dict && fallback == 0;
-    const uint32_t D = dict ? hres[1] : 0, dict_bytes = dict ? hres[2] : 0;
+    const uint32_t D = dict ? hres[1] : 0, dict_bytes = dict ? (str ? hres[2] : hres[1] * uint32_t(w)) : 0;
     uint32_t bw = 1;
     while (D > 1 && (uint64_t(1) << bw) < D) bw++;
 
@@ -1217,7 +1198,6 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_res = take(m, sizeof(DevChunkResult) * n_chunks);
     ctx->off_pieces = take(m, sizeof(int2) * ctx->pieces.size());
     ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);
-    ctx->off_pdone = take(m, sizeof(int) * ctx->pieces.size());
     ctx->off_fallback = take(m, sizeof(int) * ctx->jobs.size());
     ctx->off_wins = take(m, sizeof(int2) * ctx->wins.size());
     ctx->off_bajobs = take(m, sizeof(BaJob) * ctx->bajobs.size());
@@ -1508,7 +1488,6 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     size_t o_job = take(m, sizeof(SnappyJob)), o_pc = take(m, sizeof(int2) * ctx->pieces.size());
     size_t o_sp = take(m, 4 * ctx->pieces.size()), o_fb = take(m, 4), o_wn = take(m, sizeof(int2) * ctx->wins.size());
     size_t o_res = take(m, sizeof(DevChunkResult));
-    size_t o_pd = take(m, sizeof(int) * std::max<size_t>(ctx->pieces.size(), 1));
     m = align_up(m, 256);
     HIPCHK(ctx, ctx->d_meta.ensure(m));
     HIPCHK(ctx, ctx->h_meta.ensure(m));
@@ -1523,8 +1502,7 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     ctx->d_last_splits = reinterpret_cast<const uint32_t*>(d + o_sp);
     launch_snappy(reinterpret_cast<const SnappyJob*>(d + o_job), 1, reinterpret_cast<const int2*>(d + o_wn),
                   int(ctx->wins.size()), ctx->d_win, ctx->d_ent, ctx->d_lane_out, reinterpret_cast<const int2*>(d + o_pc),
-                  int(ctx->pieces.size()), ctx->n_wg_pieces, reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb),
-                  reinterpret_cast<int*>(d + o_pd),
+                  int(ctx->pieces.size()), reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb),
                   reinterpret_cast<DevChunkResult*>(d + o_res), st);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, ctx->h_res.ensure(512));

@@ -826,7 +826,7 @@ __device__ void repair_window(const SnappyJob* __restrict__ jobs, const int2 jw,
     const SnapWin sw = win[job.win_base + w];
     const uint32_t W0 = w * SNAP_WIN;
     if (sw.flags == WM_SKIP) {   // inside a literal: no token starts here (the index pass's guesses are cleared,
-                                 // so the bitmap is exact over the whole stream: k_snappy_exec_wg reads it so)
+                                 // so the bitmap is exact over the whole stream)
         reinterpret_cast<uint4*>(job.tokmap + size_t(w) * SNAP_WWORDS)[lane] = make_uint4(0, 0, 0, 0);
         return;
     }
@@ -1069,8 +1069,7 @@ constexpr uint32_t X2_LDS = X2_FBUF_OFF + XFAR * FBUF_W * 4;
 enum : uint32_t { X2_LDSADDR = 0, X2_COPY = 1 };
 
 __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
-                                                     const uint32_t* __restrict__ splits, int* __restrict__ fb,
-                                                     const int* __restrict__ pdone, int mode) {
+                                                     const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
     __shared__ __attribute__((aligned(16))) uint8_t L[X2_LDS];
     __shared__ uint16_t tokpos[XCHUNK / 2];
     __shared__ uint32_t sbits[XBATCH / 32];                               // token starts of the step's output
@@ -1081,7 +1080,6 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
     const int lane = threadIdx.x;
     int j, k;
     if (mode == 0) {
-        if (pdone && pdone[blockIdx.x]) return;   // decoded by k_snappy_exec_wg
         const int2 pc = pieces[blockIdx.x];
         j = pc.x;
         k = pc.y;
@@ -1369,33 +1367,21 @@ void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins
                        (const uint32_t*)d_lane_out, d_splits, d_fb);
 }
 
-void launch_snappy_exec_wg(const SnappyJob*, const int2*, int, const uint32_t*, int*, int*, hipStream_t);
-
-// PF_XW=0: every piece goes to the single-wave executor (A/B); default: workgroup executor first.
-bool snappy_wg_enabled() {
-    static const bool on = [] { const char* e = std::getenv("PF_XW"); return !(e && e[0] == '0'); }();
-    return on;
-}
-
-void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_pieces, int n_pieces, int n_wg,
-                        uint32_t* d_splits, int* d_fb, int* d_pdone, DevChunkResult* d_res, hipStream_t s) {
+void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
+                        int* d_fb, DevChunkResult* d_res, hipStream_t s) {
     if (n_jobs <= 0) return;
-    const bool wg = snappy_wg_enabled() && d_pdone && n_wg > 0;
-    if (wg) launch_snappy_exec_wg(d_jobs, d_pieces, n_wg, d_splits, d_fb, d_pdone, s);
-    hipLaunchKernelGGL(k_snappy_exec2, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb,
-                       (const int*)(wg ? d_pdone : nullptr), 0);
+    hipLaunchKernelGGL(k_snappy_exec2, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
     // whole-page redo of pages whose pieces were not independent
-    hipLaunchKernelGGL(k_snappy_exec2, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb,
-                       (const int*)nullptr, 1);
+    hipLaunchKernelGGL(k_snappy_exec2, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
     launch_snappy_serial(d_jobs, n_jobs, d_fb, d_res, s);
 }
 
-// All Snappy work of one batch, in stream order. fb and pdone must be zero on entry.
+// All Snappy work of one batch, in stream order. fb must be zero on entry.
 void launch_snappy(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
-                   SnapEnt* d_ent, uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, int n_wg, uint32_t* d_splits,
-                   int* d_fb, int* d_pdone, DevChunkResult* d_res, hipStream_t s) {
+                   SnapEnt* d_ent, uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
+                   int* d_fb, DevChunkResult* d_res, hipStream_t s) {
     launch_snappy_parse(d_jobs, n_jobs, d_wins, n_wins, d_win, d_ent, d_lane_out, d_splits, d_fb, s);
-    launch_snappy_exec(d_jobs, n_jobs, d_pieces, n_pieces, n_wg, d_splits, d_fb, d_pdone, d_res, s);
+    launch_snappy_exec(d_jobs, n_jobs, d_pieces, n_pieces, d_splits, d_fb, d_res, s);
 }
 
 }  // namespace pf

@@ -79,3 +79,36 @@ def test_serial_snappy_kernel_many_jobs(decoder, oracle, monkeypatch):
     forced = [j for j in range(nj) if rec[5 * j] == 3]
     assert len(forced) == nj // 3 and max(forced) >= 128
     assert _check_all(got, oracle, path, "forced-serial") > 0
+
+
+def test_nested_config5_shape(decoder, oracle, tmp_path):
+    """BASELINE config 5 at shape: 1,000,000 rows of l optional LIST<STRUCT<a INT64, b UTF8>>,
+    `a` DELTA_BINARY_PACKED, `b` dictionary, v2 pages, Snappy (4 row groups; one batch). Values,
+    validity, list offsets, list validity and the raw rep/def levels bit-exact against the oracle
+    (the reference's own reader stops at "Unexpected repetition": ParquetReader.java:199-202)."""
+    import pyarrow.parquet as pq
+    from pfloor import datagen
+    from pfloor.decoder import decode_file
+    path = str(tmp_path / "nested_1m.parquet")
+    pq.write_table(datagen.nested_table(1_000_000, seed=5), path, row_group_size=250_000, compression="snappy",
+                   data_page_version="2.0", column_encoding={"l.list.element.a": "DELTA_BINARY_PACKED"},
+                   use_dictionary=["l.list.element.b"])
+    got = decode_file(path, decoder=decoder)
+    assert got["_status"] == 0, got["_error"]
+    assert _check_all(got, oracle, path, "nested") == 8
+    g = got[(0, 0)]
+    assert g["num_rows"] == 250_000 and g["num_entries"] > g["num_rows"]   # lists of 0-4 elements
+    assert "list_offsets" in g and "rep_levels" in g
+
+
+def test_flat_config1_shape_uncompressed(decoder, oracle, tmp_path):
+    """BASELINE config 1 at shape: 1,000,000 rows (id INT64, x DOUBLE, n nullable INT32, s dictionary
+    UTF8), uncompressed (pyarrow compression='NONE'), v1 pages; bit-exact against the oracle."""
+    import pyarrow.parquet as pq
+    from pfloor import datagen
+    from pfloor.decoder import decode_file
+    path = str(tmp_path / "flat_1m.parquet")
+    pq.write_table(datagen.flat_table(1_000_000, seed=1), path, row_group_size=250_000, compression="NONE")
+    got = decode_file(path, decoder=decoder)
+    assert got["_status"] == 0, got["_error"]
+    assert _check_all(got, oracle, path, "flat") == 16
