@@ -136,7 +136,40 @@ def units_for_rank(args, pf, world, rank, S, batch=None):
         g, p, _ = units[0]
         k = max(1, min(S, len(cols)))
         units = [(g, p, cols[i::k]) for i in range(k)] + units[1:]
-    elif getattr(args, "split", "rowgroups") == "columns" and units and S > 1 and batch is None and \
+    elif getattr(args, "split", "rowgroups") == "kinds" and units and S > 2 and batch is None and \
+            WORKLOADS[args.workload]["batch"] <= 0:
+        # A context's time is the sum of its stages' latencies, and every kind of page it holds adds
+        # stages: BYTE_ARRAY columns add the value walk, the chars count and scan and the string
+        # gather; fixed-width columns add the run tables and the fixed gather. Keep the kinds apart:
+        # BYTE_ARRAY columns on `string_ctx` contexts, fixed-width columns on the others, each group
+        # dealt as in "columns" (heavy columns cut into row-group slices, longest first).
+        size = {(p, c): pf.chunk_range(p, c)[1] for _, p, _ in units for c in cols}
+        strs = [c for c in cols if pf.columns[c].physical_type == 6]
+        fixed = [c for c in cols if pf.columns[c].physical_type != 6]
+        ks = max(1, min(S - 1, getattr(args, "string_ctx", 2))) if strs and fixed else (S if strs else 0)
+        groups = [(strs, ks), (fixed, S - ks)]
+        per = []
+        for gcols, gS in groups:
+            if not gcols or gS <= 0:
+                continue
+            cost = {c: sum(size[(p, c)] for _, p, _ in units) for c in gcols}
+            share = sum(cost.values()) / gS
+            slices = []
+            for c in gcols:
+                k = max(1, min(len(units), -(-cost[c] // max(1, int(share)))))
+                for j in range(k):
+                    us = units[j::k]
+                    slices.append((sum(size[(p, c)] for _, p, _ in us), c, [(g, p) for g, p, _ in us]))
+            load = [0] * gS
+            gper = [dict() for _ in range(gS)]
+            for cst, c, gps in sorted(slices, key=lambda t: -t[0]):
+                k = min(range(gS), key=lambda k: load[k])
+                load[k] += cst
+                for gp in gps:
+                    gper[k].setdefault(gp, []).append(c)
+            per += gper
+        return [[[(g, p, sorted(cs)) for (g, p), cs in sorted(d.items())]] for d in per if d], n_log, mine
+    elif getattr(args, "split", "rowgroups") in ("columns", "kinds") and units and S > 1 and batch is None and \
             WORKLOADS[args.workload]["batch"] <= 0:
         # Each context decodes a few columns over the rank's row groups: a stage's latency is set by
         # its slowest item (a heavy column's Snappy pieces, string blocks) more than by how many items
@@ -277,7 +310,8 @@ def measure_pmc(args, kernel_re):
         d = os.path.join(out, cnt)
         cmd = [prof, "--pmc", cnt, "--kernel-include-regex", kernel_re, "--output-format", "csv", "-d", d, "-o", "run",
                "--", sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
-               "--data-dir", args.data_dir, "--streams", str(args.streams), "--split", args.split]
+               "--data-dir", args.data_dir, "--streams", str(args.streams), "--split", args.split,
+               "--string-ctx", str(args.string_ctx)]
         t0 = time.time()
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
         log(f"[bench] rocprofv3 --pmc {cnt}: rc {r.returncode} in {time.time() - t0:.1f}s")
@@ -544,8 +578,10 @@ def main():
     ap.add_argument("--data-dir", default=os.environ.get("PF_BENCH_DIR", "/tmp/pfloor_bench"))
     ap.add_argument("--streams", type=int, default=4,
                     help="decode contexts (HIP streams) per GPU; work units are dealt round-robin to them")
-    ap.add_argument("--split", choices=("columns", "rowgroups"), default="columns",
-                    help="sf1: give each context all row groups of a column subset (default) or whole row groups")
+    ap.add_argument("--split", choices=("columns", "kinds", "rowgroups"), default="columns",
+                    help="sf1: give each context all row groups of a column subset (default), the same with "
+                         "BYTE_ARRAY and fixed-width columns on separate contexts (kinds), or whole row groups")
+    ap.add_argument("--string-ctx", type=int, default=2, help="--split kinds: contexts for the BYTE_ARRAY columns")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")

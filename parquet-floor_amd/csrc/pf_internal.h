@@ -32,9 +32,22 @@ struct SnappyJob {
     uint32_t* tokmap;     // bit i = a token starts at input byte i (n_win * 256 words, index pass)
     uint32_t win_base;    // first entry of this job's 8 KiB index windows (SnapWin / lane outs)
     uint32_t n_win;       // ceil(src_len / 8192), >= 1
+    // direct pages (k_snappy_head): output bytes [dlo, dst_len) go to ddst + offset (the column's
+    // values) instead of dst + offset; bytes below dlo (the v1 level section) still go to dst.
+    // dgran: the store width (4, 8 or 16 bytes) ddst's alignment allows (flush chunks sit at 16-byte
+    // aligned output offsets). Only the
+    // block-parallel executor writes direct; the whole-page redo and the serial kernel write dst.
+    uint8_t* ddst;
+    uint32_t dlo;
+    uint32_t dgran;
+    uint32_t dflags;      // diagnostics: bit 0 = the block-parallel executor rejects the job (PF_DEBUG_FORCE_REDO)
+    uint32_t dpad;
 };
 
 enum : int32_t { DONE_FIXED = 1, DONE_FLAT = 2, DONE_NULL = 4 };
+
+// DevPage.direct (k_snappy_head): how the page's decompressed body reaches the decoders
+enum : int32_t { DIRECT_NONE = 0, DIRECT_VALUES = 1, DIRECT_INPLACE = 2 };
 
 struct DevPage {
     const uint8_t* body;      // v1: [rep][def][values] uncompressed; v2: values section
@@ -76,6 +89,14 @@ struct DevPage {
     int64_t dx_bad;
     uint32_t dx_data;
     uint32_t dx_pad;
+    // Snappy data pages: the job's fallback flag (FB_*, read after the executor), and what
+    // k_snappy_head decided (DIRECT_*): VALUES = a PLAIN fixed-width page with every level present
+    // whose values the executor wrote straight into the column (k_flat_fixed then only sets the
+    // validity bits, unless the job fell back to the redo / serial path, which writes the body);
+    // INPLACE = the stream is one literal: body points at it in the compressed input, no executor.
+    const int* jfb;
+    int32_t direct;
+    int32_t direct_pad;
 };
 
 // k_runs run table of a page: {nruns, values covered, all levels present, valid}, then nruns

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include "pf_device.h"
+#include "pf_snappy_par.h"
 
 namespace pf {
 
@@ -1447,6 +1448,72 @@ struct FlatLds {
     uint32_t dcover, vcover, vlo;
 };
 
+// ---- k_snappy_head: pages whose Snappy stream needs no executor or no scratch ----------------
+//
+// One thread per Snappy job of a data page, before the parse kernels (DecompressorStream.java:101-173
+// hands every page to snappy-java; here two common shapes skip work):
+//  * INPLACE: the stream is a single literal (incompressible pages: bit-packed dictionary ids,
+//    dictionary pages of random data): the decompressed body IS the literal's bytes in the
+//    compressed input. The page's body points there and every Snappy kernel skips the job
+//    (FB_INPLACE): no index / chain / repair / splits / executor work, no scratch copy.
+//  * VALUES: a PLAIN fixed-width page of a flat chunk whose levels are all present (v2: the level
+//    section; v1: the first literal must hold the level section, as it does for parquet-mr and
+//    Arrow pages) and whose values section is exactly num_values * width bytes: the executor
+//    writes the values straight into the column (SnappyJob.ddst) and k_flat_fixed only sets the
+//    validity bits of the page (north_star's fusion of decompression with the PLAIN decode).
+// Anything else, and every page whose stream turns out not to parse, takes the normal path.
+__global__ __launch_bounds__(64) void k_snappy_head(SnappyJob* __restrict__ jobs, int n_jobs, DevPage* __restrict__ pages,
+                                                    const DevChunk* __restrict__ chunks, int* __restrict__ fb,
+                                                    const DevChunkResult* __restrict__ res) {
+    const int j = int(blockIdx.x) * 64 + int(threadIdx.x);
+    if (j >= n_jobs || fb[j] != FB_OK) return;
+    SnappyJob& J = jobs[j];
+    DevPage& pg = pages[J.page];
+    if (pg.flags & PG_DICT) return;   // dictionary pointers (dict_data, BaJob.p) were set from the scratch body
+    const DevChunk& ck = chunks[pg.chunk];
+    if (res[pg.chunk].status != 0) return;
+    const uint8_t* in = J.src;
+    const uint64_t n = J.src_len;
+    uint64_t pos = 0, ulen = 0;
+    if (!uvarint(in, n, pos, ulen) || ulen != J.dst_len || pos >= n) return;
+    const SnapTok t = snap_tok(glb_read8(in, n, pos));
+    if (t.kind != 0) return;
+    const uint64_t data = pos + t.arg;   // the first literal's bytes: in[data, data + t.ol)
+    if (data + t.ol > n) return;
+    if (pos + t.tl == n && t.ol == J.dst_len) {   // one literal covers the page
+        pg.body = in + data;
+        pg.direct = DIRECT_INPLACE;
+        fb[j] = FB_INPLACE;
+        return;
+    }
+    // PLAIN fixed width, flat, all present
+    const int w = ck.width;
+    if (pg.encoding != 0 || ck.max_rep != 0 || ck.ptype == 0 || ck.ptype == 6 || w <= 0 || !ck.values) return;
+    const uint32_t ne = uint32_t(pg.num_values);
+    uint32_t L = 0;
+    if (ck.max_def > 0) {
+        const int bw = bit_width(uint32_t(ck.max_def));
+        if (pg.flags & PG_V2) {
+            if (!all_present(pg.lvl + pg.rep_len, pg.def_len, bw, ne, uint32_t(ck.max_def))) return;
+        } else {
+            if (pg.def_enc != 3 || t.ol < 4) return;
+            const uint32_t lv = ld32le(in + data, 0, 4);
+            if (lv > 60u || 4u + lv > t.ol) return;   // the level section must sit in the first literal
+            if (!all_present(in + data + 4, lv, bw, ne, uint32_t(ck.max_def))) return;
+            L = 4u + lv;
+        }
+    }
+    if (uint64_t(J.dst_len) != uint64_t(L) + uint64_t(ne) * uint64_t(w)) return;
+    uint8_t* dd = ck.values + uint64_t(pg.entry_start) * uint64_t(w) - L;
+    const uintptr_t al = reinterpret_cast<uintptr_t>(dd);
+    const uint32_t gran = (al & 15u) == 0 ? 16u : ((al & 7u) == 0 ? 8u : ((al & 3u) == 0 ? 4u : 0u));
+    if (gran == 0) return;
+    J.ddst = dd;
+    J.dlo = L;
+    J.dgran = gran;
+    pg.direct = DIRECT_VALUES;
+}
+
 // k_flat, all levels present, fixed-width values: value index = entry index, lane-consecutive
 // entries so every load and store of a wave is one contiguous run of memory. Returns err.
 #ifndef PF_DICT_LDS
@@ -1465,7 +1532,7 @@ struct FixedLds {
 template <class Lds>
 __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg, const Sections& s, bool dict,
                                   bool boolean, int enc, int w, const uint8_t* ids, uint64_t ids_n, int id_bw,
-                                  uint64_t slot_base, uint32_t e_begin, uint32_t e_end) {
+                                  uint64_t slot_base, uint32_t e_begin, uint32_t e_end, bool direct = false) {
     const int tid = threadIdx.x;
     const uint8_t* vend = s.val + s.val_n;
     const bool dalign = dict && (reinterpret_cast<uintptr_t>(ck.dict_data) & uintptr_t(w - 1)) == 0;
@@ -1501,7 +1568,9 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
             __syncthreads();
         }
         const bool wide = w == 4 || w == 8;
-        if (!bad && wide && ((dict && dalign) || enc == 0 || enc == 5)) {
+        if (direct) {
+            // the executor wrote this page's values into the column (k_snappy_head): validity only
+        } else if (!bad && wide && ((dict && dalign) || enc == 0 || enc == 5)) {
             // batched: the loads of FB entries per thread are in flight together
 #ifndef PF_FB_DIV
 #define PF_FB_DIV 2
@@ -1673,8 +1742,11 @@ __global__ __launch_bounds__(NT) void k_flat_fixed(const DevChunk* __restrict__ 
         }
         __syncthreads();
     }
+    // values already in place: the executor decoded the page without falling back (a redo / serial
+    // fallback writes the body to scratch instead, and the page is decoded from there)
+    const bool direct = pg.direct == DIRECT_VALUES && pg.jfb != nullptr && *pg.jfb <= FB_WHOLE;
     const int err = flat_present_fixed(S, ck, pg, s, dict, boolean, enc, w, ids, ids_n, id_bw,
-                                       uint64_t(pg.entry_start), e_begin, e_end);
+                                       uint64_t(pg.entry_start), e_begin, e_end, direct);
 #ifdef PF_STAMPS
     if (tid == 0) { const unsigned long long dt_ = __builtin_amdgcn_s_memtime() - ft0; PSTAMP(1, dt_); PSTAMP(0, 1); atomicMax(&pf_pstamps[9], dt_); }
 #endif
@@ -2443,6 +2515,12 @@ void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevC
     hipLaunchKernelGGL(k_ba_emit, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
     hipLaunchKernelGGL(k_ba_verify, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
     hipLaunchKernelGGL(k_ba_fallback, dim3(std::min(n_jobs, 64)), dim3(NT), 0, st, d_jobs, n_jobs, d_res);
+}
+void launch_snappy_head(SnappyJob* d_jobs, int n_jobs, DevPage* d_pages, const DevChunk* d_chunks, int* d_fb,
+                        const DevChunkResult* d_res, hipStream_t st) {
+    if (n_jobs > 0)
+        hipLaunchKernelGGL(k_snappy_head, dim3((n_jobs + 63) / 64), dim3(64), 0, st, d_jobs, n_jobs, d_pages, d_chunks, d_fb,
+                           d_res);
 }
 void launch_scan(DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                  uint8_t* arena, uint64_t cap, unsigned long long* used, hipStream_t st) {

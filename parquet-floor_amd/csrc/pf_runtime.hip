@@ -29,6 +29,7 @@ void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, 
 void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, int*, hipStream_t);
 void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*, DevChunkResult*, hipStream_t);
 void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t);
+void launch_snappy_head(SnappyJob*, int, DevPage*, const DevChunk*, int*, const DevChunkResult*, hipStream_t);
 void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_dba_chars(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
@@ -216,6 +217,8 @@ int enqueue_kernels(pf_ctx* ctx) {
 
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
     EVREC(ctx, ctx->ev[1], st);
+    // single-literal pages in place, PLAIN fixed-width pages straight into the column (pf_pages.hip)
+    launch_snappy_head(d_jobs, int(ctx->jobs.size()), d_pages, d_chunks, d_fallback, d_res, st);
     launch_snappy_parse(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent,
                         ctx->d_lane_out, d_splits, d_fallback, st);
     EVREC(ctx, ctx->ev[2], st);
@@ -352,6 +355,14 @@ int upload_meta(pf_ctx* ctx) {
         if (k > 0)
             for (size_t j = 0; j < ctx->jobs.size(); j++)
                 if (int(j % size_t(k)) == k - 1) fbh[j] = FB_SERIAL;
+        // PF_DEBUG_FORCE_REDO=k: the block-parallel executor rejects every k-th job (after
+        // k_snappy_head), so direct pages are also decoded through the redo path (tests)
+        const char* r = std::getenv("PF_DEBUG_FORCE_REDO");
+        const int kr = r ? std::atoi(r) : 0;
+        SnappyJob* jh = reinterpret_cast<SnappyJob*>(h + ctx->off_jobs);
+        if (kr > 0)
+            for (size_t j = 0; j < ctx->jobs.size(); j++)
+                if (int(j % size_t(kr)) == kr - 1) jh[j].dflags |= 1u;
     }
     DevChunkResult* r = reinterpret_cast<DevChunkResult*>(h + ctx->off_res);
     for (int c = 0; c < ctx->n_chunks; c++) {
@@ -1206,6 +1217,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->meta_bytes = m;
     HIPCHK(ctx, ctx->d_meta.ensure(m));
     HIPCHK(ctx, ctx->h_meta.ensure(m));
+    {   // each Snappy data page reads its job's fallback flag (k_flat_fixed: were the values written direct?)
+        const int* d_fb = reinterpret_cast<const int*>(static_cast<uint8_t*>(ctx->d_meta.p) + ctx->off_fallback);
+        for (size_t j = 0; j < ctx->jobs.size(); j++) ctx->pages[size_t(ctx->jobs[j].page)].jfb = d_fb + j;
+    }
     HIPCHK(ctx, ctx->h_res.ensure(align_up(sizeof(DevChunkResult) * n_chunks, 256) + sizeof(DevChunk) * n_chunks + 256));
     int rc = upload_meta(ctx);
     if (rc) return rc;
@@ -1637,6 +1652,23 @@ int pf_debug_snappy_fallback(pf_ctx* ctx, int* out, int n_jobs) {
         }
     }
     return nj;
+}
+
+// Diagnostics (not part of pfloor.h): per page of the last finished pf_decode_row_group, what
+// k_snappy_head decided (DIRECT_NONE / DIRECT_VALUES / DIRECT_INPLACE). Returns the page count.
+int pf_debug_page_direct(pf_ctx* ctx, int* out, int n_pages) {
+    if (!ctx || !ctx->d_meta.p || !ctx->tables_from_decode) return fail(ctx, PF_ERR_STATE, "no finished decode");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int np = int(ctx->pages.size());
+    const int m = n_pages < np ? n_pages : np;
+    if (out && m > 0) {
+        std::vector<DevPage> pg(static_cast<size_t>(m));
+        HIPCHK(ctx, hipMemcpy(pg.data(), static_cast<uint8_t*>(ctx->d_meta.p) + ctx->off_pages, sizeof(DevPage) * size_t(m),
+                              hipMemcpyDeviceToHost));
+        for (int i = 0; i < m; i++) out[i] = pg[size_t(i)].direct;
+    }
+    return np;
 }
 
 int pf_last_timing(pf_ctx* ctx, float* stage_ms, int n_stages, int* n_written) {

@@ -521,6 +521,7 @@ __global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict
     __shared__ __attribute__((aligned(16))) uint32_t sbits[SNAP_WWORDS];
     __shared__ uint32_t slo[64];
     const int2 jw = wins[blockIdx.x];
+    if (fb[jw.x] == FB_INPLACE) return;   // one literal: k_snappy_head pointed the page at it
     const SnappyJob job = jobs[jw.x];
     const int lane = threadIdx.x;
     const uint64_t n = job.src_len;
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
     const SnappyJob job = jobs[j];
-    if (fb[j] == FB_SERIAL) return;
+    if (fb[j] >= FB_SERIAL) return;
     const uint32_t nw = job.n_win;
     const uint64_t n = job.src_len;
     SnapWin* Wn = win + job.win_base;
@@ -821,7 +822,7 @@ __device__ void repair_window(const SnappyJob* __restrict__ jobs, const int2 jw,
                               uint32_t* slo) {
     const SnappyJob job = jobs[jw.x];
     const int lane = threadIdx.x;
-    if (fb[jw.x] == FB_SERIAL) return;
+    if (fb[jw.x] >= FB_SERIAL) return;
     const uint32_t w = uint32_t(jw.y);
     const SnapWin sw = win[job.win_base + w];
     const uint32_t W0 = w * SNAP_WIN;
@@ -901,7 +902,7 @@ __global__ __launch_bounds__(64) void k_snappy_splits(const SnappyJob* __restric
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
     const SnappyJob job = jobs[j];
-    if (fb[j] == FB_SERIAL) return;
+    if (fb[j] >= FB_SERIAL) return;
     const uint32_t nw = job.n_win;
     const uint64_t n = job.src_len;
     const SnapWin* Wn = win + job.win_base;
@@ -1015,13 +1016,55 @@ __device__ __forceinline__ uint64_t lane_mask_lt(uint32_t k) { return k >= 64 ? 
 // Store ring bytes [F, upto) in whole XSLOT slots (16-byte stores, XSLOT / 64 bytes per lane).
 // Returns the number of store instructions issued.
 constexpr uint32_t XST = XSLOT / 64 / 16;   // 16-byte stores per lane per slot
-__device__ __forceinline__ uint32_t flush_slots(const uint8_t* ring, uint8_t* dst, uint32_t& F, uint32_t upto, int lane) {
+
+// Where a job's output goes: dst + a, or for a direct job (k_snappy_head) ddst + a from output
+// offset dlo on (the column's values; dgran-wide stores, ddst's alignment).
+struct OutDst {
+    PF_GLOBAL uint8_t* dst;
+    PF_GLOBAL uint8_t* dd;   // null: not direct
+    uint32_t dlo, gran;
+};
+
+// Rare: a 16-byte chunk holding the end of the level section (kept out of put16's registers).
+__device__ __attribute__((noinline)) void put16_split(PF_GLOBAL uint8_t* dst, PF_GLOBAL uint8_t* dd, uint32_t dlo, uint32_t a,
+                                                     u32x4 v) {
+    for (uint32_t k = 0; k < 16; k++) {
+        const uint8_t b = uint8_t(v[k >> 2] >> (8 * (k & 3)));
+        (a + k < dlo ? dst : dd)[a + k] = b;
+    }
+}
+
+// 16 output bytes at the 16-aligned output offset a.
+__device__ __forceinline__ void put16(const OutDst& o, uint32_t a, u32x4 v) {
+    if (o.dd == nullptr || a + 16u <= o.dlo) {
+        *(PF_GLOBAL u32x4*)(o.dst + a) = v;
+    } else if (a >= o.dlo) {
+        PF_GLOBAL uint8_t* p = o.dd + a;
+        if (o.gran == 16u) {
+            *(PF_GLOBAL u32x4*)p = v;
+        } else if (o.gran == 8u) {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            reinterpret_cast<PF_GLOBAL u32x2*>(p)[0] = u32x2{v.x, v.y};
+            reinterpret_cast<PF_GLOBAL u32x2*>(p)[1] = u32x2{v.z, v.w};
+        } else {
+            PF_GLOBAL uint32_t* q = reinterpret_cast<PF_GLOBAL uint32_t*>(p);
+            q[0] = v.x; q[1] = v.y; q[2] = v.z; q[3] = v.w;
+        }
+    } else {   // straddles dlo (the end of the level section)
+        put16_split(o.dst, o.dd, o.dlo, a, v);
+    }
+}
+__device__ __forceinline__ void put1(const OutDst& o, uint32_t a, uint8_t b) {
+    (o.dd == nullptr || a < o.dlo ? o.dst : o.dd)[a] = b;
+}
+
+__device__ __forceinline__ uint32_t flush_slots(const uint8_t* ring, const OutDst& o, uint32_t& F, uint32_t upto, int lane) {
     uint32_t nsl = 0;
     while (upto - F >= XSLOT) {
         const uint32_t a0 = F + uint32_t(lane) * (XSLOT / 64);
         #pragma unroll
         for (uint32_t u = 0; u < XST; u++)
-            *(PF_GLOBAL u32x4*)(dst + a0 + 16 * u) = *reinterpret_cast<const u32x4*>(ring + ((a0 + 16 * u) & XRMASK));
+            put16(o, a0 + 16 * u, *reinterpret_cast<const u32x4*>(ring + ((a0 + 16 * u) & XRMASK)));
         F += XSLOT;
         nsl += XST;
     }
@@ -1106,6 +1149,10 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
         if (lane == 0) atomicMax(&fb[j], FB_SERIAL);
         return;
     }
+    if (mode == 0 && (job.dflags & 1u)) {   // diagnostics: forced redo
+        if (lane == 0) atomicMax(&fb[j], FB_REDO);
+        return;
+    }
     uint32_t ip, out_start, out_end = job.dst_len;
     if (whole) {
         ip = uint32_t(pos0);
@@ -1120,6 +1167,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
     const PF_GLOBAL uint16_t* tm16 = (const PF_GLOBAL uint16_t*)(job.tokmap);
     const PF_GLOBAL uint8_t* gin = gptr(in);
     PF_GLOBAL uint8_t* gdst = gptr(dst);
+    const OutDst od{gdst, mode == 0 ? gptr(job.ddst) : nullptr, job.dlo, job.dgran};
     uint32_t op = out_start, F = out_start;
     uint32_t nst = 0;   // store instructions issued by the last flush (still possibly in flight)
     bool bad = false;
@@ -1200,7 +1248,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
                         for (int u = 0; u < 16; u++)
                             if (b0 + u < c) ring[(op + d0 + b0 + u) & XRMASK] = by[u];
                     }
-                    fl_slots += flush_slots(ring, dst, F, op + d0 + c, lane);
+                    fl_slots += flush_slots(ring, od, F, op + d0 + c, lane);
                 }
                 nst = fl_slots;
                 used = 1;
@@ -1214,13 +1262,17 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
                 const bool cp = inb && kd != 0;
                 if (__any(cp && (off == 0 || off > otok - out_start))) { bad = true; break; }
                 const bool far = cp && farc;
+                // a far source straddling the direct split (level bytes | values) is not one window
+                if (od.dd != nullptr && __any(far && a < od.dlo && a + ol > od.dlo)) { bad = true; break; }
                 // far copies: their source (flushed output) into this token's LDS slot
                 if (__any(far)) {
                     if (nst == XST) wait_vmem_last_slot();   // all but the last slot's stores have landed
                     else wait_vmem();
                     if (far) {
-                        const PF_GLOBAL uint32_t* fsrc = (const PF_GLOBAL uint32_t*)(gdst + (a & ~3u));
-                        const uint32_t nwd = ((a & 3u) + ol + 3u) >> 2;
+                        const PF_GLOBAL uint8_t* fb0 = od.dd != nullptr && a >= od.dlo ? od.dd + a : gdst + a;
+                        const uintptr_t fa = reinterpret_cast<uintptr_t>(fb0);
+                        const PF_GLOBAL uint32_t* fsrc = (const PF_GLOBAL uint32_t*)(fa & ~uintptr_t(3));
+                        const uint32_t nwd = (uint32_t(fa & 3u) + ol + 3u) >> 2;
                         uint32_t fw[FBUF_W];
                         #pragma unroll
                         for (int u = 0; u < int(FBUF_W); u++) fw[u] = uint32_t(u) < nwd ? fsrc[u] : 0u;
@@ -1242,8 +1294,10 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
                     const bool near = cp && !far;
                     d0 = rel | ((near ? X2_COPY : X2_LDSADDR) << 11) | ((near && off < ol) ? (1u << 12) : 0u) |
                          (min(off, 0xffffu) << 16);
+                    const uint32_t fsh = od.dd != nullptr && a >= od.dlo
+                                             ? uint32_t((reinterpret_cast<uintptr_t>(od.dd) + a) & 3u) : (a & 3u);
                     d1 = lit ? X2_STAGE_OFF + woff + (srcv - I)
-                             : (far ? X2_FBUF_OFF + frank * (FBUF_W * 4) + (a & 3u) : a);
+                             : (far ? X2_FBUF_OFF + frank * (FBUF_W * 4) + fsh : a);
                 }
                 if (lane < int(XBATCH / 32)) sbits[lane] = 0;
                 __syncthreads();
@@ -1319,7 +1373,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
                         if (act[u]) ring[(s0 + 64u * uint32_t(u) + uint32_t(lane)) & XRMASK] = uint8_t(W[u]);
                 }
                 XT(2);
-                const uint32_t sl = flush_slots(ring, dst, F, op + btot, lane);
+                const uint32_t sl = flush_slots(ring, od, F, op + btot, lane);
                 if (sl) nst = sl;
                 XT(6);
             }
@@ -1337,8 +1391,8 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
 #endif
     // tail: bytes [F, op)
     for (uint32_t a = F + uint32_t(lane) * 16u; a + 16u <= op; a += 1024u)
-        *(PF_GLOBAL u32x4*)(gdst + a) = *reinterpret_cast<const u32x4*>(ring + (a & XRMASK));
-    for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) gdst[a] = ring[a & XRMASK];
+        put16(od, a, *reinterpret_cast<const u32x4*>(ring + (a & XRMASK)));
+    for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) put1(od, a, ring[a & XRMASK]);
 }
 
 #ifdef PF_STAMPS
