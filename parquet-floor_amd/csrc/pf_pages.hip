@@ -1435,6 +1435,35 @@ __device__ inline void copy_chars_fast(const uint32_t* coff, const uint32_t* csr
     }
 }
 
+#ifndef PF_SHORT_AVG
+#define PF_SHORT_AVG 16
+#endif
+constexpr uint32_t SHORT_AVG = PF_SHORT_AVG;   // tiles averaging at most this many chars per value: copy_chars_short
+// Short values (dictionary strings such as flags and modes: 1-16 chars): one value per thread,
+// lane-consecutive values, so a wave's byte stores cover one contiguous run of the chars arena.
+// Each 8-byte piece of a value is read as the aligned dwords around it (+ v_alignbyte); a chunk
+// copy (copy_chars_fast) would blend up to 16 values into every 16-byte chunk one at a time.
+__device__ inline void copy_chars_short(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
+                                        const uint8_t* sbase, uint8_t* obase) {
+    for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {
+        const uint32_t b = coff[v], e = v + 1 < nv ? coff[v + 1] : total;
+        const uint8_t* sp = sbase + csrc[v];
+        uint8_t* dp = obase + b;
+        for (uint32_t o = 0; o < e - b; o += 8) {
+            const uint32_t len = min(8u, e - b - o);
+            const uintptr_t a = reinterpret_cast<uintptr_t>(sp + o);
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+            const uint32_t sh = uint32_t(a & 3u);
+            const uint32_t d0 = q[0];
+            const uint32_t d1 = sh + len > 4u ? q[1] : 0u;
+            const uint32_t d2 = sh + len > 8u ? q[2] : 0u;
+            const uint64_t x = uint64_t(__builtin_amdgcn_alignbyte(d1, d0, sh)) |
+                               (uint64_t(__builtin_amdgcn_alignbyte(d2, d1, sh)) << 32);
+            for (uint32_t i = 0; i < len; i++) dp[o + i] = uint8_t(x >> (8 * i));
+        }
+    }
+}
+
 struct FlatLds {
     Run drun[RUN_CAP];
     Run vrun[RUN_CAP];
@@ -1996,7 +2025,8 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
         if (binary) {
             const uint8_t* sb = dict ? ck.dict_data : s.val;
             const uint8_t* se = dict ? pages[ck.dict_page].body + pages[ck.dict_page].body_len : s.val + s.val_n;
-            copy_chars_fast(S.coff, S.csrc, tv, tchars, sb, se, ck.chars + char_base, S.cv);
+            if (tchars <= SHORT_AVG * tv) copy_chars_short(S.coff, S.csrc, tv, tchars, sb, ck.chars + char_base);
+            else copy_chars_fast(S.coff, S.csrc, tv, tchars, sb, se, ck.chars + char_base, S.cv);
         }
         if (ck.max_def > 0 && ck.validity) flush_bits(S.vbits, slot_base + e0, want, ck.validity);
         vidx += tv;
