@@ -566,7 +566,9 @@ static int delta_binary_decode(const uint8_t* p, size_t n, int is64, uint64_t* o
     size_t i = 0; uint64_t block, nmini, total, zz;
     if (rd_uvarint(p, n, &i, &block) || rd_uvarint(p, n, &i, &nmini) || rd_uvarint(p, n, &i, &total) || rd_uvarint(p, n, &i, &zz))
         return E_CORRUPT;
-    if (nmini == 0 || block == 0 || block % 128 || (block / nmini) % 32 || nmini > block) return E_CORRUPT;
+    /* parquet-mr 1.12.2 DeltaBinaryPackingConfig: only "miniBlockSize must be multiple of 8" (the format
+     * spec's block % 128 / miniblock % 32 are writer rules it does not enforce on read) */
+    if (nmini == 0 || block == 0 || block % nmini || (block / nmini) % 8 || nmini > block) return E_CORRUPT;
     uint64_t vpm = block / nmini;
     int64_t first = (int64_t)(zz >> 1) ^ -(int64_t)(zz & 1);
     if (total_out) *total_out = (int64_t)total;

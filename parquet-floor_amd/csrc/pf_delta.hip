@@ -70,8 +70,8 @@ __device__ bool dbp_decode_wg(DbpLds& S, const uint8_t* p, uint64_t n, bool is64
         S.err = 0; S.done = 0;
         uint64_t pos = 0, block, nmini, total, zz;
         if (!uvarint(p, n, pos, block) || !uvarint(p, n, pos, nmini) || !uvarint(p, n, pos, total) ||
-            !uvarint(p, n, pos, zz) || nmini == 0 || block == 0 || block % 128 || nmini > 256 || nmini > block ||
-            (block / nmini) % 32 || (strict && total > cap)) {
+            !uvarint(p, n, pos, zz) || nmini == 0 || block == 0 || block % nmini || nmini > 256 || nmini > block ||
+            (block / nmini) % 8 || (strict && total > cap)) {   // parquet-mr: miniblock size a multiple of 8
             S.err = 1;
         } else {
             S.vpm_s = block / nmini; S.nmini_s = nmini; S.total_s = total;

@@ -1090,6 +1090,138 @@ __device__ int walk_runs(const uint8_t* p, uint64_t n, int bw, uint32_t lo, uint
     return 0;
 }
 
+// ---- wave-parallel run discovery (north_star K2: run boundaries found by wavefront scans) ------
+//
+// The run headers of an RLE/bit-packed hybrid stream form a chain (each header's position follows
+// from the previous run's length), and writers emit long stretches of identical headers: Arrow and
+// parquet-mr cut bit-packed runs at 512 values (header 0x81 0x01), so a page of random dictionary
+// ids or levels is ~40 runs with one byte stride. One round: every lane decodes the header at
+// pos (the chain position, exact), then lane i decodes the header at pos + i * stride and votes
+// whether it repeats lane 0's; the ballot's first failing lane ends the accepted prefix, and a
+// prefix scan of the (equal) run lengths gives every accepted run's first value. A stretch of k
+// equal runs costs one round instead of k dependent header loads; mixed runs still advance by
+// one run per round. Called by all 64 lanes of one wave with wave-uniform arguments.
+struct WaveRun {
+    uint64_t pos;        // header position (uniform)
+    uint32_t first;      // first value of the run at pos (uniform)
+};
+
+template <class Src>
+__device__ __forceinline__ bool hdr_decode(const Src& B, uint64_t n, uint64_t p, int bw, uint64_t& h, uint32_t& hl,
+                                           uint32_t& val) {
+    h = 0;
+    hl = 0;
+    val = 0;
+    #pragma unroll
+    for (int k = 0; k < 5; k++) {
+        if (p + uint64_t(k) >= n) return false;
+        const uint32_t c = B(p + uint64_t(k));
+        h |= uint64_t(c & 0x7fu) << (7 * k);
+        if (!(c & 0x80u)) { hl = uint32_t(k) + 1u; break; }
+    }
+    if (hl == 0) return false;   // headers above 2^35 are not runs of a page
+    if (!(h & 1)) {
+        const uint32_t nbv = uint32_t(bw + 7) >> 3;
+        if (p + hl + nbv > n) return false;
+        for (uint32_t b = 0; b < nbv; b++) val |= uint32_t(B(p + hl + b)) << (8 * b);
+    }
+    return true;
+}
+
+// One discovery round from st (uniform). Returns the accepted runs k (lanes < k hold run `r`,
+// with its count clipped at `limit`), 0 when the header at st.pos is an empty run (skipped), -1
+// when the stream ends or is corrupt there. st advances past the accepted runs.
+template <class Src>
+__device__ int wave_run_round(const Src& B, uint64_t n, int bw, uint32_t limit, WaveRun& st, Run& r, bool& trunc) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t h0;
+    uint32_t hl0, v0;
+    if (!hdr_decode(B, n, st.pos, bw, h0, hl0, v0)) return -1;
+    const bool packed = h0 & 1;
+    const uint64_t cnt0 = packed ? (h0 >> 1) * 8 : (h0 >> 1);
+    const uint64_t pay0 = packed ? (h0 >> 1) * uint64_t(bw) : uint64_t(uint32_t(bw + 7) >> 3);
+    if (cnt0 == 0) {
+        st.pos += hl0 + (packed ? 0 : pay0);
+        return 0;
+    }
+    const uint64_t stride = uint64_t(hl0) + pay0;
+    // lane i: the i-th run from st.pos, if the headers repeat
+    const uint64_t p = st.pos + uint64_t(lane) * stride;
+    bool ok = true;
+    uint32_t v = v0;
+    if (lane > 0) {
+        uint64_t h;
+        uint32_t hl;
+        ok = hdr_decode(B, n, p, bw, h, hl, v) && h == h0 && (!packed || p + hl + pay0 <= n);
+    }
+    const uint64_t fail = __ballot(!ok);
+    uint32_t k = fail ? uint32_t(__ffsll((unsigned long long)fail) - 1) : 64u;
+    // runs needed to reach `limit` (the last one clipped)
+    const uint64_t left = uint64_t(limit - st.first);
+    const uint64_t need = (left + cnt0 - 1) / cnt0;
+    if (uint64_t(k) > need) k = uint32_t(need);
+    const uint64_t f = uint64_t(st.first) + uint64_t(lane) * cnt0;
+    r.first = uint32_t(f);
+    r.count = uint32_t(min<uint64_t>(cnt0, f < limit ? uint64_t(limit) - f : 0));
+    r.packed = packed ? 1u : 0u;
+    r.data = packed ? uint32_t((p + hl0) * 8) : v;
+    // a truncated final bit-packed run (lane 0 only: the others required the whole payload)
+    uint64_t adv = uint64_t(k) * stride;
+    trunc = packed && st.pos + stride > n;
+    if (trunc) adv = n - st.pos;
+    st.pos += adv;
+    st.first = uint32_t(min<uint64_t>(uint64_t(st.first) + uint64_t(k) * cnt0, uint64_t(limit)));
+    return int(k);
+}
+
+// walk_runs for a whole wave (same contract; runs / nruns / covered / stw written by lane 0 or by the
+// lanes holding the runs). All 64 lanes call it.
+__device__ int wave_walk_runs(const uint8_t* p, uint64_t n, int bw, uint32_t lo, uint32_t limit, Run* runs, int cap,
+                              int& nruns_out, uint32_t& covered_out, RunWalk& stw) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const auto B = [p](uint64_t i) { return uint32_t(p[i]); };
+    WaveRun st{stw.pos, stw.first};
+    int nr = 0, ret = 0;
+    uint32_t covered = st.first;
+    while (st.first < limit) {
+        Run r;
+        const uint64_t pos0 = st.pos;
+        const uint32_t f0 = st.first;
+        bool trunc;
+        const int k = wave_run_round(B, n, bw, limit, st, r, trunc);
+        if (k < 0) { ret = 1; break; }
+        if (k == 0) continue;
+        // stored: runs ending after lo (a prefix of the round's runs ends at or before lo)
+        const bool keep = lane < uint32_t(k) && r.first + r.count > lo;
+        const uint64_t km = __ballot(keep);
+        const int nk = __popcll(km);
+        const int rank = __popcll(km & ((1ull << lane) - 1ull));
+        if (nr + nk > cap) {   // table full: store what fits, stop after the last stored run
+            const int room = cap - nr;
+            if (keep && rank < room) runs[nr + rank] = r;
+            // the round's runs up to the last stored one: lanes [0, first kept lane + room)
+            const uint32_t upto = uint32_t(__ffsll((unsigned long long)km) - 1) + uint32_t(room);
+            const uint64_t stride = (st.pos - pos0) / uint64_t(k);
+            st.pos = pos0 + uint64_t(upto) * stride;
+            st.first = f0 + (upto ? __shfl(r.first + r.count, int(upto) - 1, 64) - f0 : 0u);
+            covered = st.first;
+            nr = cap;
+            ret = 2;
+            break;
+        }
+        if (keep) runs[nr + rank] = r;
+        nr += nk;
+        covered = st.first;
+    }
+    if (lane == 0) {
+        nruns_out = nr;
+        covered_out = covered;
+        stw.pos = st.pos;
+        stw.first = st.first;
+    }
+    return ret;
+}
+
 // Definition levels of p[0..n): 1 if every one of the `ne` levels is max_def (RLE runs only),
 // 0 otherwise (or corrupt: the single-workgroup path reports it).
 __device__ int all_present(const uint8_t* p, uint64_t n, int bw, uint32_t ne, uint32_t max_def) {
@@ -1224,13 +1356,13 @@ __global__ __launch_bounds__(128) void k_runs(const DevChunk* __restrict__ chunk
     const int id_bw = int(s.val[0]);
     if (tid == 0) {
         s_allp = ck.max_def == 0 ? 1 : (s.def_rle ? all_present(s.def, s.def_n, bit_width(ck.max_def), ne, uint32_t(ck.max_def)) : 0);
-    } else if (tid == 64) {
-        RunWalk st{0, 0};
+    } else if (tid >= 64) {   // wave 1: the id runs, discovered wave-parallel
+        __shared__ RunWalk s_st;
+        if (tid == 64) s_st = RunWalk{0, 0};
         int nr = 0;
         uint32_t cov = 0;
-        s_res = walk_runs(s.val + 1, s.val_n - 1, id_bw, 0, ne, R, RUN_CAP, nr, cov, st);
-        s_nr = nr;
-        s_cov = cov;
+        const int rr = wave_walk_runs(s.val + 1, s.val_n - 1, id_bw, 0, ne, R, RUN_CAP, nr, cov, s_st);
+        if (tid == 64) { s_res = rr; s_nr = nr; s_cov = cov; }
     }
     __syncthreads();
     const int nr = s_nr;
@@ -1585,10 +1717,10 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
         if (dict) {
             if ((S.vlo > e0 || e0 + want > S.vcover) && S.vres == 2) {
                 __syncthreads();
-                if (tid == 0) {   // next window of runs (re-walk from the page start)
-                    S.vst = RunWalk{0, 0};
-                    S.vlo = e0;
-                    S.vres = walk_runs(ids, ids_n, id_bw, e0, e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst);
+                if (tid < 64) {   // next window of runs (re-walk from the page start), wave 0
+                    if (tid == 0) { S.vst = RunWalk{0, 0}; S.vlo = e0; }
+                    const int rr = wave_walk_runs(ids, ids_n, id_bw, e0, e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst);
+                    if (tid == 0) S.vres = rr;
                 }
                 __syncthreads();
             }
@@ -1763,11 +1895,12 @@ __global__ __launch_bounds__(NT) void k_flat_fixed(const DevChunk* __restrict__ 
                 S.vrun[i] = r;
             }
             if (tid == 0) { S.nvrun = int(nr); S.vcover = cov; S.vlo = 0; S.vres = cov >= ne ? 0 : 1; }
-        } else if (tid == 0) {
-            S.nvrun = 0; S.vcover = 0; S.vres = 0; S.vlo = e_begin;
-            S.vst = RunWalk{0, 0};
-            if (s.val_n > 0 && id_bw <= 32)
-                S.vres = walk_runs(ids, ids_n, id_bw, e_begin, e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst);
+        } else if (tid < 64) {   // wave 0 walks the id runs of this block
+            if (tid == 0) { S.nvrun = 0; S.vcover = 0; S.vres = 0; S.vlo = e_begin; S.vst = RunWalk{0, 0}; }
+            if (s.val_n > 0 && id_bw <= 32) {
+                const int rr = wave_walk_runs(ids, ids_n, id_bw, e_begin, e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst);
+                if (tid == 0) S.vres = rr;
+            }
         }
         __syncthreads();
     }
@@ -1837,17 +1970,19 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
     const unsigned long long ft0 = __builtin_amdgcn_s_memtime();
     if (tid == 0) { PSTAMP(0, 1); if (dict) PSTAMP(6, 1); if (binary) PSTAMP(7, 1); }
 #endif
-    if (tid == 0) {
-        S.ndrun = 0; S.dcover = ne; S.dres = 0;
+    if (tid < 64) {   // wave 0: definition-level runs (pages with nulls)
+        if (tid == 0) { S.ndrun = 0; S.dcover = ne; S.dres = 0; S.dst = RunWalk{0, 0}; }
         if (!split && ck.max_def > 0) {
-            S.dst = RunWalk{0, 0};
-            S.dres = walk_runs(s.def, s.def_n, bwd, 0, ne, S.drun, RUN_CAP, S.ndrun, S.dcover, S.dst);
+            const int rr = wave_walk_runs(s.def, s.def_n, bwd, 0, ne, S.drun, RUN_CAP, S.ndrun, S.dcover, S.dst);
+            if (tid == 0) S.dres = rr;
         }
-    } else if (tid == 64 && !(split && tab)) {
-        S.nvrun = 0; S.vcover = 0; S.vres = 0; S.vlo = e_begin;
-        S.vst = RunWalk{0, 0};
-        if (dict && s.val_n > 0 && id_bw <= 32)
-            S.vres = walk_runs(ids, ids_n, id_bw, e_begin, split ? e_end : ne, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst);
+    } else if (tid < 128 && !(split && tab)) {   // wave 1: dictionary-id runs
+        if (tid == 64) { S.nvrun = 0; S.vcover = 0; S.vres = 0; S.vlo = e_begin; S.vst = RunWalk{0, 0}; }
+        if (dict && s.val_n > 0 && id_bw <= 32) {
+            const int rr = wave_walk_runs(ids, ids_n, id_bw, e_begin, split ? e_end : ne, S.vrun, RUN_CAP, S.nvrun,
+                                          S.vcover, S.vst);
+            if (tid == 64) S.vres = rr;
+        }
     }
     if (split && tab) {   // the page's run table (k_runs), loaded by all threads
         const uint32_t nr = T[0], cov = T[1];
@@ -1923,11 +2058,11 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
         if (tv > 0 && dict) {
             if (split && (uint64_t(S.vlo) > vidx || vidx + tv > uint64_t(S.vcover)) && S.vres == 2) {
                 __syncthreads();
-                if (tid == 0) {   // next window of runs (re-walk from the page start)
-                    S.vst = RunWalk{0, 0};
-                    S.vlo = uint32_t(vidx);
-                    S.vres = walk_runs(ids, ids_n, id_bw, uint32_t(vidx), e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover,
-                                       S.vst);
+                if (tid < 64) {   // next window of runs (re-walk from the page start), wave 0
+                    if (tid == 0) { S.vst = RunWalk{0, 0}; S.vlo = uint32_t(vidx); }
+                    const int rr = wave_walk_runs(ids, ids_n, id_bw, uint32_t(vidx), e_end, S.vrun, RUN_CAP, S.nvrun,
+                                                  S.vcover, S.vst);
+                    if (tid == 0) S.vres = rr;
                 }
                 __syncthreads();
             }
@@ -2151,51 +2286,27 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     }
     uint32_t* runs = LT + 4;
     const uint32_t cap = pg.lvl_cap;
-    if (tid == 0) {   // the header walk (run headers are a varint chain), from LDS
-        uint32_t pos = 0, first = 0, nr = 0, ok = 1;
-        while (first < ne) {
-            uint64_t h = 0;
-            int sh = 0;
-            for (;;) {
-                if (pos >= dn || sh > 63) { ok = 0; break; }
-                const uint32_t c = stage[woff + pos++];
-                h |= uint64_t(c & 0x7fu) << sh;
-                sh += 7;
-                if (!(c & 0x80u)) break;
+    {   // the header chain, discovered wave-parallel from LDS (wave_run_round)
+        const auto B = [&](uint64_t i) { return uint32_t(stage[woff + uint32_t(i)]); };
+        WaveRun st{0, 0};
+        uint32_t nr = 0, ok = 1;
+        while (st.first < ne) {
+            Run r;
+            bool trunc;
+            const int k = wave_run_round(B, dn, bw, ne, st, r, trunc);
+            if (k < 0) { ok = 0; break; }
+            if (k == 0) continue;
+            // a run truncated by the section end (parquet-mr reads what is there and zero-pads): the
+            // page goes to k_flat / k_decode, whose level reads are zero past the section
+            if (trunc || __any(tid < k && !r.packed && r.data > maxd) || nr + uint32_t(k) > cap) { ok = 0; break; }
+            if (tid < k) {
+                runs[4 * (nr + tid) + 0] = r.first;
+                runs[4 * (nr + tid) + 1] = r.data;
+                runs[4 * (nr + tid) + 2] = r.count | (r.packed << 31);
             }
-            if (!ok) break;
-            uint32_t data, packed;
-            uint64_t cnt;
-            if (h & 1) {
-                cnt = (h >> 1) * 8;
-                const uint64_t nb = (h >> 1) * uint64_t(bw);
-                data = pos * 8u;
-                packed = 1;
-                // a run truncated by the section end (parquet-mr reads what is there and zero-pads):
-                // the page goes to k_flat / k_decode, whose level reads are zero past the section
-                if (nb > uint64_t(dn - pos)) { ok = 0; break; }
-                pos += uint32_t(nb);
-            } else {
-                cnt = h >> 1;
-                const uint32_t nbv = uint32_t(bw + 7) >> 3;
-                if (pos + nbv > dn) { ok = 0; break; }
-                data = 0;
-                for (uint32_t b = 0; b < nbv; b++) data |= uint32_t(stage[woff + pos + b]) << (8 * b);
-                pos += nbv;
-                packed = 0;
-                if (data > maxd) { ok = 0; break; }
-            }
-            if (cnt == 0) continue;
-            if (nr == cap) { ok = 0; break; }
-            const uint32_t c = uint32_t(min<uint64_t>(cnt, uint64_t(ne - first)));
-            runs[4 * nr + 0] = first;
-            runs[4 * nr + 1] = data;
-            runs[4 * nr + 2] = c | (packed << 31);
-            nr++;
-            first += c;
+            nr += uint32_t(k);
         }
-        s_nr = nr;
-        s_ok = ok;
+        if (tid == 0) { s_nr = nr; s_ok = ok; }
     }
     __syncthreads();
     if (!s_ok) {
@@ -2546,6 +2657,56 @@ void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevC
     hipLaunchKernelGGL(k_ba_verify, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
     hipLaunchKernelGGL(k_ba_fallback, dim3(std::min(n_jobs, 64)), dim3(NT), 0, st, d_jobs, n_jobs, d_res);
 }
+// Diagnostics (tests/test_gpu_runs.py): walk_runs (one lane) and wave_walk_runs (one wave) over the
+// same stream; out = {ret, nruns, covered, pos, first, runs[cap] x 4} for each.
+__global__ __launch_bounds__(64) void k_debug_walk(const uint8_t* p, uint64_t n, int bw, uint32_t lo, uint32_t limit, int cap,
+                                                    uint32_t pos0, uint32_t first0, uint32_t* out) {
+    __shared__ Run R[RUN_CAP];
+    __shared__ int s_nr;
+    __shared__ uint32_t s_cov;
+    __shared__ RunWalk s_st;
+    const int tid = threadIdx.x;
+    uint32_t* o1 = out;
+    uint32_t* o2 = out + 5 + 4 * cap;
+    if (tid == 0) {
+        RunWalk st{pos0, first0};
+        int nr = 0;
+        uint32_t cov = 0;
+        const int r = walk_runs(p, n, bw, lo, limit, R, cap, nr, cov, st);
+        o1[0] = uint32_t(r); o1[1] = uint32_t(nr); o1[2] = cov; o1[3] = uint32_t(st.pos); o1[4] = st.first;
+        for (int i = 0; i < nr; i++) { o1[5 + 4 * i] = R[i].first; o1[6 + 4 * i] = R[i].count; o1[7 + 4 * i] = R[i].data; o1[8 + 4 * i] = R[i].packed; }
+        s_st = RunWalk{pos0, first0};
+    }
+    __syncthreads();
+    const int r = wave_walk_runs(p, n, bw, lo, limit, R, cap, s_nr, s_cov, s_st);
+    __syncthreads();
+    if (tid == 0) {
+        o2[0] = uint32_t(r); o2[1] = uint32_t(s_nr); o2[2] = s_cov; o2[3] = uint32_t(s_st.pos); o2[4] = s_st.first;
+    }
+    for (int i = tid; i < s_nr; i += 64) { o2[5 + 4 * i] = R[i].first; o2[6 + 4 * i] = R[i].count; o2[7 + 4 * i] = R[i].data; o2[8 + 4 * i] = R[i].packed; }
+}
+
+extern "C" int pf_debug_walk_runs(const uint8_t* stream, uint64_t n, int bw, uint32_t lo, uint32_t limit, int cap,
+                                  uint32_t pos0, uint32_t first0, uint32_t* out) {
+    if (cap > int(RUN_CAP) || cap < 0) return -1;
+    uint8_t* d = nullptr;
+    uint32_t* o = nullptr;
+    const size_t ob = 4 * size_t(2 * (5 + 4 * cap));
+    if (hipMalloc(&d, n + 64) != hipSuccess) return -1;
+    if (hipMalloc(&o, ob) != hipSuccess) { (void)hipFree(d); return -1; }
+    int rc = 0;
+    if (hipMemset(d, 0, n + 64) != hipSuccess || hipMemcpy(d, stream, n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(o, 0, ob) != hipSuccess)
+        rc = -1;
+    if (!rc) {
+        hipLaunchKernelGGL(k_debug_walk, dim3(1), dim3(64), 0, 0, d, n, bw, lo, limit, cap, pos0, first0, o);
+        if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(out, o, ob, hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
+    }
+    (void)hipFree(d);
+    (void)hipFree(o);
+    return rc;
+}
+
 void launch_snappy_head(SnappyJob* d_jobs, int n_jobs, DevPage* d_pages, const DevChunk* d_chunks, int* d_fb,
                         const DevChunkResult* d_res, hipStream_t st) {
     if (n_jobs > 0)
