@@ -1174,13 +1174,15 @@ __device__ int wave_run_round(const Src& B, uint64_t n, int bw, uint32_t limit, 
     return int(k);
 }
 
-// walk_runs for a whole wave (same contract; runs / nruns / covered / stw written by lane 0 or by the
-// lanes holding the runs). All 64 lanes call it.
+// walk_runs for a whole wave from state st0 (same contract; runs / nruns / covered / the final state
+// are written by lane 0 or by the lanes holding the runs). All 64 lanes call it. The start state is
+// a value, not shared memory: one lane's store to LDS is not ordered before the other lanes' loads
+// without a barrier.
 __device__ int wave_walk_runs(const uint8_t* p, uint64_t n, int bw, uint32_t lo, uint32_t limit, Run* runs, int cap,
-                              int& nruns_out, uint32_t& covered_out, RunWalk& stw) {
+                              int& nruns_out, uint32_t& covered_out, RunWalk& stw, RunWalk st0) {
     const uint32_t lane = threadIdx.x & 63u;
     const auto B = [p](uint64_t i) { return uint32_t(p[i]); };
-    WaveRun st{stw.pos, stw.first};
+    WaveRun st{st0.pos, st0.first};
     int nr = 0, ret = 0;
     uint32_t covered = st.first;
     while (st.first < limit) {
@@ -1358,10 +1360,9 @@ __global__ __launch_bounds__(128) void k_runs(const DevChunk* __restrict__ chunk
         s_allp = ck.max_def == 0 ? 1 : (s.def_rle ? all_present(s.def, s.def_n, bit_width(ck.max_def), ne, uint32_t(ck.max_def)) : 0);
     } else if (tid >= 64) {   // wave 1: the id runs, discovered wave-parallel
         __shared__ RunWalk s_st;
-        if (tid == 64) s_st = RunWalk{0, 0};
         int nr = 0;
         uint32_t cov = 0;
-        const int rr = wave_walk_runs(s.val + 1, s.val_n - 1, id_bw, 0, ne, R, RUN_CAP, nr, cov, s_st);
+        const int rr = wave_walk_runs(s.val + 1, s.val_n - 1, id_bw, 0, ne, R, RUN_CAP, nr, cov, s_st, RunWalk{0, 0});
         if (tid == 64) { s_res = rr; s_nr = nr; s_cov = cov; }
     }
     __syncthreads();
@@ -1719,7 +1720,7 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
                 __syncthreads();
                 if (tid < 64) {   // next window of runs (re-walk from the page start), wave 0
                     if (tid == 0) { S.vst = RunWalk{0, 0}; S.vlo = e0; }
-                    const int rr = wave_walk_runs(ids, ids_n, id_bw, e0, e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst);
+                    const int rr = wave_walk_runs(ids, ids_n, id_bw, e0, e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst, RunWalk{0, 0});
                     if (tid == 0) S.vres = rr;
                 }
                 __syncthreads();
@@ -1898,7 +1899,7 @@ __global__ __launch_bounds__(NT) void k_flat_fixed(const DevChunk* __restrict__ 
         } else if (tid < 64) {   // wave 0 walks the id runs of this block
             if (tid == 0) { S.nvrun = 0; S.vcover = 0; S.vres = 0; S.vlo = e_begin; S.vst = RunWalk{0, 0}; }
             if (s.val_n > 0 && id_bw <= 32) {
-                const int rr = wave_walk_runs(ids, ids_n, id_bw, e_begin, e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst);
+                const int rr = wave_walk_runs(ids, ids_n, id_bw, e_begin, e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst, RunWalk{0, 0});
                 if (tid == 0) S.vres = rr;
             }
         }
@@ -1973,14 +1974,14 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
     if (tid < 64) {   // wave 0: definition-level runs (pages with nulls)
         if (tid == 0) { S.ndrun = 0; S.dcover = ne; S.dres = 0; S.dst = RunWalk{0, 0}; }
         if (!split && ck.max_def > 0) {
-            const int rr = wave_walk_runs(s.def, s.def_n, bwd, 0, ne, S.drun, RUN_CAP, S.ndrun, S.dcover, S.dst);
+            const int rr = wave_walk_runs(s.def, s.def_n, bwd, 0, ne, S.drun, RUN_CAP, S.ndrun, S.dcover, S.dst, RunWalk{0, 0});
             if (tid == 0) S.dres = rr;
         }
     } else if (tid < 128 && !(split && tab)) {   // wave 1: dictionary-id runs
         if (tid == 64) { S.nvrun = 0; S.vcover = 0; S.vres = 0; S.vlo = e_begin; S.vst = RunWalk{0, 0}; }
         if (dict && s.val_n > 0 && id_bw <= 32) {
             const int rr = wave_walk_runs(ids, ids_n, id_bw, e_begin, split ? e_end : ne, S.vrun, RUN_CAP, S.nvrun,
-                                          S.vcover, S.vst);
+                                          S.vcover, S.vst, RunWalk{0, 0});
             if (tid == 64) S.vres = rr;
         }
     }
@@ -2061,7 +2062,7 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
                 if (tid < 64) {   // next window of runs (re-walk from the page start), wave 0
                     if (tid == 0) { S.vst = RunWalk{0, 0}; S.vlo = uint32_t(vidx); }
                     const int rr = wave_walk_runs(ids, ids_n, id_bw, uint32_t(vidx), e_end, S.vrun, RUN_CAP, S.nvrun,
-                                                  S.vcover, S.vst);
+                                                  S.vcover, S.vst, RunWalk{0, 0});
                     if (tid == 0) S.vres = rr;
                 }
                 __syncthreads();
@@ -2287,7 +2288,8 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     uint32_t* runs = LT + 4;
     const uint32_t cap = pg.lvl_cap;
     {   // the header chain, discovered wave-parallel from LDS (wave_run_round)
-        const auto B = [&](uint64_t i) { return uint32_t(stage[woff + uint32_t(i)]); };
+        const uint8_t* const stw = stage + woff;
+        const auto B = [stw](uint64_t i) { return uint32_t(stw[i]); };
         WaveRun st{0, 0};
         uint32_t nr = 0, ok = 1;
         while (st.first < ne) {
@@ -2678,7 +2680,7 @@ __global__ __launch_bounds__(64) void k_debug_walk(const uint8_t* p, uint64_t n,
         s_st = RunWalk{pos0, first0};
     }
     __syncthreads();
-    const int r = wave_walk_runs(p, n, bw, lo, limit, R, cap, s_nr, s_cov, s_st);
+    const int r = wave_walk_runs(p, n, bw, lo, limit, R, cap, s_nr, s_cov, s_st, RunWalk{pos0, first0});
     __syncthreads();
     if (tid == 0) {
         o2[0] = uint32_t(r); o2[1] = uint32_t(s_nr); o2[2] = s_cov; o2[3] = uint32_t(s_st.pos); o2[4] = s_st.first;
