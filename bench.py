@@ -82,7 +82,9 @@ def log(*a):
 
 def input_path(args):
     w = WORKLOADS[args.workload]
-    return os.path.join(args.data_dir, f"{w['kind']}_{w['rows']}_seed{w['seed']}_rg{w['rg_rows']}.parquet")
+    pool = getattr(args, "pool", 100000)
+    tag = f"_pool{pool}" if w["kind"] == "wide" and pool != 100000 else ""
+    return os.path.join(args.data_dir, f"{w['kind']}_{w['rows']}_seed{w['seed']}_rg{w['rg_rows']}{tag}.parquet")
 
 
 def make_input(args):
@@ -106,7 +108,7 @@ def make_input(args):
         t = datagen.flat_table(w["rows"], seed=w["seed"])
         kw = dict(compression="NONE")
     else:
-        t = datagen.wide_table(w["rows"], seed=w["seed"])
+        t = datagen.wide_table(w["rows"], seed=w["seed"], pool=getattr(args, "pool", 100000))
     tmp = path + f".tmp{os.getpid()}"
     pq.write_table(t, tmp, row_group_size=w["rg_rows"], **kw)
     os.replace(tmp, path)
@@ -310,7 +312,7 @@ def measure_pmc(args, kernel_re):
         d = os.path.join(out, cnt)
         cmd = [prof, "--pmc", cnt, "--kernel-include-regex", kernel_re, "--output-format", "csv", "-d", d, "-o", "run",
                "--", sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
-               "--data-dir", args.data_dir, "--streams", str(args.streams), "--split", args.split,
+               "--data-dir", args.data_dir, "--streams", str(args.streams), "--split", args.split, "--pool", str(args.pool),
                "--string-ctx", str(args.string_ctx)]
         t0 = time.time()
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
@@ -582,6 +584,8 @@ def main():
                     help="sf1: give each context all row groups of a column subset (default), the same with "
                          "BYTE_ARRAY and fixed-width columns on separate contexts (kinds), or whole row groups")
     ap.add_argument("--string-ctx", type=int, default=2, help="--split kinds: contexts for the BYTE_ARRAY columns")
+    ap.add_argument("--pool", type=int, default=100000,
+                    help="wide: distinct values per column (SURVEY 8(d) sweep: 1K, 16K, 32K, 64K, 100K)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -807,7 +811,7 @@ def main():
               f"{pf.num_row_groups} row groups, device-resident")
         scaling = "strong"
     else:
-        wl = (f"wide: {w['rows']} rows x {pf.num_columns} nullable INT32/FLOAT columns, 30% nulls, 100K-value dictionaries, "
+        wl = (f"wide: {w['rows']} rows x {pf.num_columns} nullable INT32/FLOAT columns, 30% nulls, {args.pool}-value dictionaries, "
               "Snappy, device-resident")
         scaling = "strong"
     out = {

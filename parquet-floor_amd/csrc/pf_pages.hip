@@ -1844,19 +1844,18 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
 // k_flat for fixed-width pages whose levels are all present (the common case), with a small LDS
 // footprint and its own register budget: one workgroup per (page, FBLK block). Marks the page
 // done; k_flat decodes everything else (strings, pages with nulls).
-__global__ __launch_bounds__(NT) void k_flat_fixed(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                                   const int2* __restrict__ blocks, DevChunkResult* res) {
-    __shared__ FixedLds S;
-    const int2 pbk = blocks[blockIdx.x];
-    if (pbk.x < 0) return;   // padding of the XCD-grouped block list (runtime)
+// Returns whether the block took its (page, block) (block-uniform); false: k_flat's body decodes it.
+__device__ __forceinline__ bool flat_fixed_block(FixedLds& S, const DevChunk* __restrict__ chunks, DevPage* pages, const int2 pbk,
+                                 DevChunkResult* res) {
+    if (pbk.x < 0) return true;   // padding of the XCD-grouped block list (runtime)
     const int pi = pbk.x;
     const uint32_t blk = uint32_t(pbk.y);
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
-    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.ptype == 6) return;
+    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.ptype == 6 || (pg.done & DONE_NULL)) return false;
     Sections s;
-    if (!page_sections(pg, ck, s)) return;
+    if (!page_sections(pg, ck, s)) return false;
     const int enc = pg.encoding;
     const bool boolean = ck.ptype == 0, dict = is_dict_enc(enc);
     const int w = ck.width;
@@ -1865,9 +1864,9 @@ __global__ __launch_bounds__(NT) void k_flat_fixed(const DevChunk* __restrict__ 
     } else if (dict) take = take && !boolean;
     else if (enc == 5) take = take && (ck.ptype == 1 || ck.ptype == 2) && pg.aux != nullptr;
     else take = false;
-    if (!take) return;
+    if (!take) return false;
     const uint32_t ne = uint32_t(pg.num_values);
-    if (blk > 0 && blk * FBLK >= ne) return;
+    if (blk > 0 && blk * FBLK >= ne) return true;
     const int id_bw = (dict && s.val_n > 0) ? int(s.val[0]) : 0;
     const uint8_t* ids = dict && s.val_n > 0 ? s.val + 1 : s.val;
     const uint64_t ids_n = dict && s.val_n > 0 ? s.val_n - 1 : 0;
@@ -1876,7 +1875,7 @@ __global__ __launch_bounds__(NT) void k_flat_fixed(const DevChunk* __restrict__ 
     if (tid == 0)
         S.allp = tab ? 1 : (ck.max_def == 0 ? 1 : all_present(s.def, s.def_n, bit_width(ck.max_def), ne, uint32_t(ck.max_def)));
     __syncthreads();
-    if (!S.allp) return;
+    if (!S.allp) return false;
     const uint32_t e_begin = blk * FBLK;
     const uint32_t e_end = min(ne, e_begin + FBLK);
 #ifdef PF_STAMPS
@@ -1919,6 +1918,13 @@ __global__ __launch_bounds__(NT) void k_flat_fixed(const DevChunk* __restrict__ 
             atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values), (unsigned long long)(e_end - e_begin));
         atomicOr(&pg.done, DONE_FIXED);
     }
+    return true;
+}
+
+__global__ __launch_bounds__(NT, 4) void k_flat_fixed(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                   const int2* __restrict__ blocks, DevChunkResult* res) {
+    __shared__ FixedLds S;
+    flat_fixed_block(S, chunks, pages, blocks[blockIdx.x], res);
 }
 
 // One workgroup per (page, FBLK block of entries). Pages whose levels are all present (max_def
@@ -1926,10 +1932,8 @@ __global__ __launch_bounds__(NT) void k_flat_fixed(const DevChunk* __restrict__ 
 // index, each block walks the dictionary-id run headers up to its own range (windowed when a
 // block needs more than RUN_CAP runs) and takes its chars base from k_count's block table or,
 // for PLAIN BYTE_ARRAY, from the value positions. Pages with nulls are decoded by block 0 alone.
-__global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                             const int2* __restrict__ blocks, DevChunkResult* res) {
-    __shared__ FlatLds S;
-    const int2 pbk = blocks[blockIdx.x];
+__device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restrict__ chunks, DevPage* pages, const int2 pbk,
+                           DevChunkResult* res) {
     if (pbk.x < 0) return;   // padding of the XCD-grouped block list (runtime)
     const int pi = pbk.x;
     const uint32_t blk = uint32_t(pbk.y);
@@ -2186,6 +2190,28 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
                                      (unsigned long long)(vidx - e_begin));
         atomicOr(&pg.done, DONE_FLAT);
     }
+}
+
+__global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                             const int2* __restrict__ blocks, DevChunkResult* res) {
+    __shared__ FlatLds S;
+    flat_block(S, chunks, pages, blocks[blockIdx.x], res);
+}
+
+// k_flat_fixed and k_flat in one launch over the same (page, block) list: a block decodes its page
+// with the fixed-width body when that applies, else with the general body. One stage instead of
+// two in stream order (the fixed-width columns' blocks no longer wait for the string blocks or the
+// other way round); the LDS of the two bodies is shared (they never run in one block together).
+__global__ __launch_bounds__(NT, 4) void k_flat_all(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                 const int2* __restrict__ blocks, DevChunkResult* res) {
+    __shared__ union FlatAllLds {
+        FixedLds f;
+        FlatLds g;
+    } S;
+    const int2 pbk = blocks[blockIdx.x];
+    if (flat_fixed_block(S.f, chunks, pages, pbk, res)) return;
+    __syncthreads();   // the fixed body's LDS reads are done before the general body reuses it
+    flat_block(S.g, chunks, pages, pbk, res);
 }
 
 // ---- nullable flat pages: definition-level run table + block-parallel decode ------------------
@@ -2731,9 +2757,15 @@ void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
                  hipStream_t st, bool nullable) {   // d_list: n (page, block) pairs
     if (n <= 0) return;
     const int2* blocks = reinterpret_cast<const int2*>(d_list);
-    hipLaunchKernelGGL(k_flat_fixed, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
+    // pages with nulls first (k_flat_null marks them DONE_NULL), then every other page in one launch
     if (nullable) hipLaunchKernelGGL(k_flat_null, dim3(n), dim3(NTN), 0, st, d_chunks, d_pages, blocks, d_res);
-    hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
+    static const bool split = [] { const char* e = std::getenv("PF_FLAT_SPLIT"); return e && e[0] == '1'; }();
+    if (split) {   // A/B: the two kernels in stream order
+        hipLaunchKernelGGL(k_flat_fixed, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
+        hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
+    } else {
+        hipLaunchKernelGGL(k_flat_all, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
+    }
 }
 void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int n_first,
                    DevChunkResult* d_res, hipStream_t st) {
