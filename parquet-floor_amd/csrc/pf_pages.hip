@@ -429,13 +429,32 @@ __global__ __launch_bounds__(NT) void k_ba_cand(BaJob* __restrict__ jobs, const 
     __syncthreads();
     const uint32_t wi = t0 / 32 + threadIdx.x;
     const uint32_t q0 = t0 + threadIdx.x * 32u;
-    uint64_t m = 0;   // plausible positions q0 .. q0 + 32
-    for (int b = 0; b <= 32; b++) {
+    // lengths that fit the stream, for all 33 positions q0 .. q0 + 32 at once: the 36 bytes from q0
+    // as 9 byte-aligned dwords, each position's little-endian length one v_alignbyte away (text
+    // almost never passes: its "lengths" are 4 characters, far larger than the page)
+    uint64_t fit = 0;
+    {
+        const uint32_t a = woff + threadIdx.x * 32u;
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(stg + (a & ~3u));
+        const uint32_t s = a & 3u;
+        uint32_t D[10], E[9];
+        #pragma unroll
+        for (int i = 0; i < 10; i++) D[i] = (a & ~3u) + 4u * i + 4u <= BA_STAGE ? d[i] : 0u;
+        #pragma unroll
+        for (int i = 0; i < 9; i++) E[i] = __builtin_amdgcn_alignbyte(D[i + 1], D[i], s);
+        const int64_t room = int64_t(n) - int64_t(q0) - 4;   // a length at q0 + b fits if <= room - b
+        #pragma unroll
+        for (int b = 0; b <= 32; b++) {
+            const uint32_t l = (b & 3) == 0 ? E[b >> 2] : __builtin_amdgcn_alignbyte(E[(b >> 2) + 1], E[b >> 2], b & 3);
+            fit |= uint64_t(int64_t(l) <= room - b) << b;
+        }
+    }
+    uint64_t m = 0;   // plausible positions: the length fits and the next value's length fits too
+    for (uint64_t f = fit; f;) {
+        const int b = __ffsll((unsigned long long)f) - 1;
+        f &= f - 1;
         const uint32_t q = q0 + uint32_t(b);
-        if (uint64_t(q) + 4 > n) break;
-        const uint32_t l = lds_le32(stg, woff + (q - t0));
-        if (l > n - q - 4) continue;
-        const uint32_t sv = q + 4 + l;
+        const uint32_t sv = q + 4 + lds_le32(stg, woff + (q - t0));
         bool ok = sv == n;
         if (!ok && uint64_t(sv) + 4 <= n) {
             const uint32_t ls = sv - t0 + 4 <= BA_TILE + 8 ? lds_le32(stg, woff + (sv - t0)) : ld32le(p, sv, n);
