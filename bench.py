@@ -133,6 +133,8 @@ def units_for_rank(args, pf, world, rank, S, batch=None):
     n_log = logical_row_groups(args, n_phys, world)
     mine = row_groups_for_rank(n_log, rank, world)
     cols = list(range(pf.num_columns))
+    if getattr(args, "columns", None):   # analysis: a column subset (not a bench line of BASELINE's config)
+        cols = [int(c) for c in args.columns.split(",")]
     units = [(g, g % n_phys, cols) for g in mine]
     if args.workload == "wide" and units:   # one row group: split its columns over the contexts
         g, p, _ = units[0]
@@ -228,6 +230,8 @@ class BatchInput:
             if n:
                 pf.read_into(s, n, self.host.ptr.value + o)
         self.descs = [pf.chunk_desc(p, c, o) for p, c, _s, _n, o in items]
+        from pfloor._native import ChunkDesc
+        self.arr = (ChunkDesc * max(1, len(self.descs)))(*self.descs)   # built once: the timed decodes pass it as is
         self.dev = None
 
     def upload(self, dec):
@@ -518,7 +522,7 @@ class ContextPool:
 
     def _decode(self, d, bi):
         t0 = time.perf_counter()
-        d.decode(bi.descs, (bi.dev if self.on_device else bi.host.ptr).value, bi.nbytes, on_device=self.on_device)
+        d.decode(bi.arr, (bi.dev if self.on_device else bi.host.ptr).value, bi.nbytes, on_device=self.on_device)
         t1 = time.perf_counter()
         with self._lock:
             self.host_s += t1 - t0
@@ -584,6 +588,7 @@ def main():
                     help="sf1: give each context all row groups of a column subset (default), the same with "
                          "BYTE_ARRAY and fixed-width columns on separate contexts (kinds), or whole row groups")
     ap.add_argument("--string-ctx", type=int, default=2, help="--split kinds: contexts for the BYTE_ARRAY columns")
+    ap.add_argument("--columns", default=None, help=argparse.SUPPRESS)   # analysis only: comma-separated column subset
     ap.add_argument("--pool", type=int, default=100000,
                     help="wide: distinct values per column (SURVEY 8(d) sweep: 1K, 16K, 32K, 64K, 100K)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

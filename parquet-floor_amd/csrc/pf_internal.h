@@ -41,7 +41,7 @@ struct SnappyJob {
     uint32_t dlo;
     uint32_t dgran;
     uint32_t dflags;      // diagnostics: bit 0 = the block-parallel executor rejects the job (PF_DEBUG_FORCE_REDO)
-    uint32_t dpad;
+    uint32_t lit;         // FB_LITCOPY: where the page's one literal starts in src
 };
 
 enum : int32_t { DONE_FIXED = 1, DONE_FLAT = 2, DONE_NULL = 4 };

@@ -1124,6 +1124,7 @@ struct WaveRun {
     uint64_t pos;        // header position (uniform)
     uint32_t first;      // first value of the run at pos (uniform)
 };
+constexpr int WAVE_SERIAL_RUNS = 8;   // after a prediction fails at lane 1: this many runs without predicting
 
 template <class Src>
 __device__ __forceinline__ bool hdr_decode(const Src& B, uint64_t n, uint64_t p, int bw, uint64_t& h, uint32_t& hl,
@@ -1150,8 +1151,11 @@ __device__ __forceinline__ bool hdr_decode(const Src& B, uint64_t n, uint64_t p,
 // One discovery round from st (uniform). Returns the accepted runs k (lanes < k hold run `r`,
 // with its count clipped at `limit`), 0 when the header at st.pos is an empty run (skipped), -1
 // when the stream ends or is corrupt there. st advances past the accepted runs.
+// spec = false: only the run at st.pos (no prediction; used after a round the prediction failed at
+// lane 1, so streams of mixed runs cost one header decode per run instead of 64).
 template <class Src>
-__device__ int wave_run_round(const Src& B, uint64_t n, int bw, uint32_t limit, WaveRun& st, Run& r, bool& trunc) {
+__device__ int wave_run_round(const Src& B, uint64_t n, int bw, uint32_t limit, WaveRun& st, Run& r, bool& trunc,
+                              bool spec = true) {
     const uint32_t lane = threadIdx.x & 63u;
     uint64_t h0;
     uint32_t hl0, v0;
@@ -1171,7 +1175,7 @@ __device__ int wave_run_round(const Src& B, uint64_t n, int bw, uint32_t limit, 
     if (lane > 0) {
         uint64_t h;
         uint32_t hl;
-        ok = hdr_decode(B, n, p, bw, h, hl, v) && h == h0 && (!packed || p + hl + pay0 <= n);
+        ok = spec && hdr_decode(B, n, p, bw, h, hl, v) && h == h0 && hl == hl0 && (!packed || p + hl + pay0 <= n);
     }
     const uint64_t fail = __ballot(!ok);
     uint32_t k = fail ? uint32_t(__ffsll((unsigned long long)fail) - 1) : 64u;
@@ -1204,14 +1208,16 @@ __device__ int wave_walk_runs(const uint8_t* p, uint64_t n, int bw, uint32_t lo,
     WaveRun st{st0.pos, st0.first};
     int nr = 0, ret = 0;
     uint32_t covered = st.first;
+    int serial = 0;   // runs left to take one at a time after a failed prediction
     while (st.first < limit) {
         Run r;
         const uint64_t pos0 = st.pos;
         const uint32_t f0 = st.first;
         bool trunc;
-        const int k = wave_run_round(B, n, bw, limit, st, r, trunc);
+        const int k = wave_run_round(B, n, bw, limit, st, r, trunc, serial == 0);
         if (k < 0) { ret = 1; break; }
         if (k == 0) continue;
+        serial = serial > 0 ? serial - 1 : (k == 1 && st.first < limit ? WAVE_SERIAL_RUNS : 0);
         // stored: runs ending after lo (a prefix of the round's runs ends at or before lo)
         const bool keep = lane < uint32_t(k) && r.first + r.count > lo;
         const uint64_t km = __ballot(keep);
@@ -1650,7 +1656,6 @@ __global__ __launch_bounds__(64) void k_snappy_head(SnappyJob* __restrict__ jobs
     if (j >= n_jobs || fb[j] != FB_OK) return;
     SnappyJob& J = jobs[j];
     DevPage& pg = pages[J.page];
-    if (pg.flags & PG_DICT) return;   // dictionary pointers (dict_data, BaJob.p) were set from the scratch body
     const DevChunk& ck = chunks[pg.chunk];
     if (res[pg.chunk].status != 0) return;
     const uint8_t* in = J.src;
@@ -1661,6 +1666,15 @@ __global__ __launch_bounds__(64) void k_snappy_head(SnappyJob* __restrict__ jobs
     if (t.kind != 0) return;
     const uint64_t data = pos + t.arg;   // the first literal's bytes: in[data, data + t.ol)
     if (data + t.ol > n) return;
+    if (pg.flags & PG_DICT) {
+        // dictionary pointers (dict_data, BaJob.p) were set from the scratch body, and gathers want it
+        // aligned: a one-literal dictionary page is copied there by k_snappy_litcopy, without a parse
+        if (pos + t.tl == n && t.ol == J.dst_len) {
+            J.lit = uint32_t(data);
+            fb[j] = FB_LITCOPY;
+        }
+        return;
+    }
     if (pos + t.tl == n && t.ol == J.dst_len) {   // one literal covers the page
         pg.body = in + data;
         pg.direct = DIRECT_INPLACE;
@@ -2241,7 +2255,7 @@ __global__ __launch_bounds__(NT, 4) void k_flat_all(const DevChunk* __restrict__
 // and scans them, so that every 4096-entry block of the page knows the value index of its first
 // present entry. k_flat_null then decodes the blocks in parallel: levels -> present bits -> block
 // scan -> value index -> dictionary gather / PLAIN load; null slots are zero.
-constexpr uint32_t LVL_STAGE = 8192;   // level sections up to this size are walked from LDS
+constexpr uint32_t LVL_STAGE = 4096;   // level sections up to this size are decoded from LDS (k_lvl)
 
 // Bits [bit, bit + k) (k <= 32) of an LDS byte array (LSB-first), from the two aligned dwords around it.
 __device__ __forceinline__ uint32_t lds_bits(const uint8_t* st, uint32_t bit, uint32_t k) {
@@ -2292,12 +2306,19 @@ __device__ __forceinline__ uint32_t id_run_at(const uint32_t* T, uint32_t nr, ui
     return lo;
 }
 
-constexpr int LT_NT = 64;   // k_lvl: one wave per page (the header walk is one lane's work)
+constexpr int LT_NT = 64;   // k_lvl: one wave per page
+constexpr uint32_t LVL_RUNS_LDS = 256;   // level runs k_lvl keeps in LDS (pages with more read them from HBM)
+constexpr uint32_t LVL_NXT = 4096;        // = LVL_STAGE: k_lvl's all-positions header chain covers its sections
 __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
                                                DevChunkResult* res) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[LVL_STAGE + 48];
     __shared__ uint32_t scan_tmp[1];
     __shared__ uint32_t s_nr, s_ok;
+    // LDS copies of the page's level runs and of its dictionary-id runs (k_runs): the block-table
+    // pass below scans them serially, one dependent load per run, which from HBM cost ~1 us each
+    __shared__ uint32_t s_runs[4 * LVL_RUNS_LDS];
+    __shared__ uint32_t s_T[4 + 2 * RUN_CAP];
+    __shared__ uint16_t s_nxt[LVL_NXT];   // position of the next run header, per byte position
     const int pi = list[blockIdx.x];
     DevPage& pg = pages[pi];
     uint32_t* LT = pg.lvltab;
@@ -2332,27 +2353,86 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     }
     uint32_t* runs = LT + 4;
     const uint32_t cap = pg.lvl_cap;
-    {   // the header chain, discovered wave-parallel from LDS (wave_run_round)
+    {   // (dn <= LVL_STAGE == LVL_NXT) all-positions chain: every byte position is decoded as a header in parallel (the position
+        // of the next header, 0xffff when it is not one), the chain from 0 is then one LDS load per
+        // run, and the runs are decoded at their headers in parallel, their first entries a prefix
+        // scan of the counts (north_star K2: run boundaries by wavefront scans)
         const uint8_t* const stw = stage + woff;
-        const auto B = [stw](uint64_t i) { return uint32_t(stw[i]); };
-        WaveRun st{0, 0};
-        uint32_t nr = 0, ok = 1;
-        while (st.first < ne) {
-            Run r;
-            bool trunc;
-            const int k = wave_run_round(B, dn, bw, ne, st, r, trunc);
-            if (k < 0) { ok = 0; break; }
-            if (k == 0) continue;
-            // a run truncated by the section end (parquet-mr reads what is there and zero-pads): the
-            // page goes to k_flat / k_decode, whose level reads are zero past the section
-            if (trunc || __any(tid < k && !r.packed && r.data > maxd) || nr + uint32_t(k) > cap) { ok = 0; break; }
-            if (tid < k) {
-                runs[4 * (nr + tid) + 0] = r.first;
-                runs[4 * (nr + tid) + 1] = r.data;
-                runs[4 * (nr + tid) + 2] = r.count | (r.packed << 31);
+        for (uint32_t p = tid; p < dn; p += LT_NT) {
+            uint32_t h = 0, hl = 0, nx = 0xffffu;
+            #pragma unroll
+            for (uint32_t k = 0; k < 3; k++) {   // headers over 2^21 are no runs of a <= 4 KiB section
+                const uint32_t c = p + k < dn ? uint32_t(stw[p + k]) : 0x80u;
+                h |= (c & 0x7fu) << (7 * k);
+                if (!(c & 0x80u)) { hl = k + 1; break; }
             }
-            nr += uint32_t(k);
+            if (hl) {
+                const uint32_t pay = (h & 1u) ? (h >> 1) * uint32_t(bw) : (uint32_t(bw) + 7u) >> 3;
+                if (p + hl + pay <= dn) nx = p + hl + pay;   // a truncated run ends the chain
+            }
+            s_nxt[p] = uint16_t(nx);
         }
+        __syncthreads();
+        uint32_t nh = 0;
+        {
+            uint32_t p = 0;
+            while (p < dn && nh < cap) {
+                if (tid == 0) runs[4 * nh + 1] = p;   // header positions, decoded below
+                nh++;
+                const uint32_t q = s_nxt[p];
+                if (q == 0xffffu) break;
+                p = q;
+            }
+        }
+        __syncthreads();   // lane 0's header positions are visible to the wave
+        uint64_t carry = 0;
+        uint32_t nr = 0, ok = 1;
+        for (uint32_t c0 = 0; c0 < nh && carry < ne; c0 += LT_NT) {
+            const uint32_t k = c0 + uint32_t(tid);
+            uint32_t cnt = 0, data = 0, packed = 0;
+            bool bad = false;
+            if (k < nh && s_nxt[runs[4 * k + 1]] != 0xffffu) {   // (the chain's last position may be no header)
+                const uint32_t P = runs[4 * k + 1];
+                uint32_t h = 0, hl = 0;
+                for (uint32_t b = 0; b < 3; b++) {
+                    const uint32_t c = stw[P + b];
+                    h |= (c & 0x7fu) << (7 * b);
+                    if (!(c & 0x80u)) { hl = b + 1; break; }
+                }
+                packed = h & 1u;
+                cnt = packed ? (h >> 1) * 8u : (h >> 1);
+                if (packed) data = (P + hl) * 8u;
+                else for (uint32_t b = 0; b < ((uint32_t(bw) + 7u) >> 3); b++) data |= uint32_t(stw[P + hl + b]) << (8 * b);
+            }
+            // first entry of each run: exclusive prefix of the counts (64-bit: counts up to 2^21 each)
+            uint64_t x = cnt;
+            #pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint64_t y = __shfl_up(x, d, 64);
+                if (tid >= d) x += y;
+            }
+            const uint64_t first = carry + x - cnt;
+            const bool emit = k < nh && cnt > 0 && first < ne;
+            if (emit && !packed && data > maxd) bad = true;
+            const uint64_t em = __ballot(emit);
+            const uint32_t rank = nr + uint32_t(__popcll(em & ((1ull << tid) - 1ull)));
+            if (__any(bad) || nr + uint32_t(__popcll(em)) > cap) { ok = 0; break; }
+            __threadfence_block();   // every lane read its header position before the slots are rewritten
+            if (emit) {
+                const uint32_t c = uint32_t(min<uint64_t>(cnt, uint64_t(ne) - first));
+                runs[4 * rank + 0] = uint32_t(first);
+                runs[4 * rank + 1] = data;
+                runs[4 * rank + 2] = c | (packed << 31);
+                if (rank < LVL_RUNS_LDS) {
+                    s_runs[4 * rank + 0] = uint32_t(first);
+                    s_runs[4 * rank + 1] = data;
+                    s_runs[4 * rank + 2] = c | (packed << 31);
+                }
+            }
+            nr += uint32_t(__popcll(em));
+            carry += __shfl(x, 63, 64);
+        }
+        if (carry < ne) ok = 0;   // the chain ended (or broke) before the page's levels
         if (tid == 0) { s_nr = nr; s_ok = ok; }
     }
     __syncthreads();
@@ -2362,12 +2442,13 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     }
     __threadfence_block();
     const uint32_t nr = s_nr;
+    uint32_t* const R = nr <= LVL_RUNS_LDS ? s_runs : runs;   // the scans below read this copy
     uint32_t carry = 0;
     for (uint32_t r0 = 0; r0 < nr; r0 += LT_NT) {
         const uint32_t r = r0 + uint32_t(tid);
         uint32_t pc = 0;
         if (r < nr) {
-            const uint32_t data = runs[4 * r + 1], cw = runs[4 * r + 2];
+            const uint32_t data = R[4 * r + 1], cw = R[4 * r + 2];
             const uint32_t cnt = cw & 0x7fffffffu;
             if (!(cw >> 31)) pc = data == maxd ? cnt : 0u;
             else {
@@ -2389,7 +2470,10 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
         }
         uint32_t tot;
         const uint32_t ex = block_excl_scan<LT_NT>(pc, scan_tmp, tot);
-        if (r < nr) runs[4 * r + 3] = carry + ex;
+        if (r < nr) {
+            runs[4 * r + 3] = carry + ex;
+            if (R != runs) R[4 * r + 3] = carry + ex;
+        }
         carry += tot;
     }
     // per FBLK block (k_flat_null): the runs it overlaps [r0, r1), the value indices of its first and
@@ -2399,35 +2483,39 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     uint32_t* BT = runs + 4 * cap;
     const uint32_t nblk = (ne + FBLK - 1) / FBLK;
     // dictionary id runs (k_runs, same stream): value index -> bit offset in the id stream
-    const uint32_t* T = pg.runtab;
-    const bool dict = is_dict_enc(pg.encoding) && T != nullptr && T[2] == 1u && T[0] <= uint32_t(RUN_CAP) && s.val_n > 0;
-    const uint32_t tnr = dict ? T[0] : 0u, tcov = dict ? T[1] : 0u;
+    const uint32_t* TG = pg.runtab;
+    const bool dict = is_dict_enc(pg.encoding) && TG != nullptr && TG[2] == 1u && TG[0] <= uint32_t(RUN_CAP) && s.val_n > 0;
+    const uint32_t tnr = dict ? TG[0] : 0u, tcov = dict ? TG[1] : 0u;
+    if (dict)
+        for (uint32_t i = tid; i < 4 + 2 * tnr; i += LT_NT) s_T[i] = TG[i];
+    __syncthreads();
+    const uint32_t* T = s_T;
     const uint32_t id_bw = dict ? uint32_t(s.val[0]) : 0u;
     uint32_t fit = 1;
     for (uint32_t b = tid; b < nblk; b += LT_NT) {
         const uint32_t eb = b * FBLK, ee = min(ne, eb + FBLK);
-        const uint32_t lo = lvl_run_at(runs, nr, eb);
+        const uint32_t lo = lvl_run_at(R, nr, eb);
         uint32_t a = lo, z = nr;    // first run with first >= ee
         while (a < z) {
             const uint32_t m = (a + z) >> 1;
-            if (runs[4 * m] < ee) a = m + 1; else z = m;
+            if (R[4 * m] < ee) a = m + 1; else z = m;
         }
-        const uint32_t vb = lvl_values_before(runs, lo, eb, stage, woff, bw, maxd);
-        const uint32_t ve = ee == ne ? carry : lvl_values_before(runs, lvl_run_at(runs, nr, ee), ee, stage, woff, bw, maxd);
+        const uint32_t vb = lvl_values_before(R, lo, eb, stage, woff, bw, maxd);
+        const uint32_t ve = ee == ne ? carry : lvl_values_before(R, lvl_run_at(R, nr, ee), ee, stage, woff, bw, maxd);
         // level bytes: from the first packed run's first bit to the last packed run's end
         uint32_t d0 = 0, d1 = 0;
         for (uint32_t r = lo; r < a; r++) {
-            const uint32_t cw = runs[4 * r + 2];
+            const uint32_t cw = R[4 * r + 2];
             if (!(cw >> 31)) continue;
-            const uint32_t f = runs[4 * r];
-            d0 = (runs[4 * r + 1] + (max(eb, f) - f) * uint32_t(bw)) >> 3;
+            const uint32_t f = R[4 * r];
+            d0 = (R[4 * r + 1] + (max(eb, f) - f) * uint32_t(bw)) >> 3;
             break;
         }
         for (uint32_t r = a; r > lo; r--) {
-            const uint32_t cw = runs[4 * (r - 1) + 2];
+            const uint32_t cw = R[4 * (r - 1) + 2];
             if (!(cw >> 31)) continue;
-            const uint32_t f = runs[4 * (r - 1)], end = min(ee, f + (cw & 0x7fffffffu));
-            d1 = (runs[4 * (r - 1) + 1] + (end - f) * uint32_t(bw) + 7u) >> 3;
+            const uint32_t f = R[4 * (r - 1)], end = min(ee, f + (cw & 0x7fffffffu));
+            d1 = (R[4 * (r - 1) + 1] + (end - f) * uint32_t(bw) + 7u) >> 3;
             break;
         }
         // dictionary-id bytes of values [vb, ve)
@@ -2754,6 +2842,40 @@ extern "C" int pf_debug_walk_runs(const uint8_t* stream, uint64_t n, int bw, uin
     return rc;
 }
 
+// Dictionary pages that are one Snappy literal (k_snappy_head: FB_LITCOPY): the literal's bytes to
+// the page's 16-byte aligned scratch body, 16 bytes per thread per step (aligned dword loads +
+// v_alignbyte), LC_SPLIT workgroups per page.
+constexpr int LC_SPLIT = 16;
+__global__ __launch_bounds__(NT) void k_snappy_litcopy(const SnappyJob* __restrict__ jobs, const int* __restrict__ list,
+                                                       const int* __restrict__ fb) {
+    const int j = list[blockIdx.x];
+    if (fb[j] != FB_LITCOPY) return;
+    const SnappyJob& J = jobs[j];
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(J.src) + J.lit;
+    const uint32_t sh = uint32_t(sa & 3u);
+    const PF_GLOBAL uint32_t* q = (const PF_GLOBAL uint32_t*)(sa & ~uintptr_t(3));
+    const uintptr_t send = reinterpret_cast<uintptr_t>(J.src) + J.src_len;   // aligned dwords below it are readable
+    PF_GLOBAL uint8_t* d = gptr(J.dst);
+    const uint32_t n = J.dst_len;
+    for (uint32_t c = (blockIdx.y * NT + threadIdx.x) * 16u; c < n; c += LC_SPLIT * NT * 16u) {
+        uint32_t w[5];
+        #pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const uintptr_t a = (sa & ~uintptr_t(3)) + c + 4u * uint32_t(k);
+            w[k] = a < send ? q[c / 4u + uint32_t(k)] : 0u;
+        }
+        const u32x4 v = {__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
+                         __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh)};
+        if (c + 16u <= n) {
+            *(PF_GLOBAL u32x4*)(d + c) = v;
+        } else {
+            for (uint32_t k = 0; c + k < n; k++) d[c + k] = uint8_t(v[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+}
+void launch_snappy_litcopy(const SnappyJob* d_jobs, const int* d_list, int n, const int* d_fb, hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(k_snappy_litcopy, dim3(n, LC_SPLIT), dim3(NT), 0, st, d_jobs, d_list, d_fb);
+}
 void launch_snappy_head(SnappyJob* d_jobs, int n_jobs, DevPage* d_pages, const DevChunk* d_chunks, int* d_fb,
                         const DevChunkResult* d_res, hipStream_t st) {
     if (n_jobs > 0)

@@ -30,6 +30,7 @@ void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, Snap
 void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*, DevChunkResult*, hipStream_t);
 void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_snappy_head(SnappyJob*, int, DevPage*, const DevChunk*, int*, const DevChunkResult*, hipStream_t);
+void launch_snappy_litcopy(const SnappyJob*, const int*, int, const int*, hipStream_t);
 void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_dba_chars(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
@@ -133,7 +134,7 @@ struct pf_ctx {
     std::vector<DevChunk> chunks;          // host copies (device pointers)
     std::vector<DevPage> pages;
     std::vector<SnappyJob> jobs;
-    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode, l_runs, l_dlen, l_dba, l_lvl;
+    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode, l_runs, l_dlen, l_dba, l_lvl, l_djobs;
     std::vector<int2> wins, pieces;       // Snappy index windows / 64 KiB pieces (job, index)
     std::vector<BaJob> bajobs;             // PLAIN BYTE_ARRAY walks: dictionary pages, then data pages
     std::vector<int2> ba_tiles;            // (job relative to its batch, tile)
@@ -209,6 +210,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     int* d_dlen = lists + lo; lo += ctx->l_dlen.size();
     int* d_dba = lists + lo; lo += ctx->l_dba.size();
     int* d_lvl = lists + lo; lo += ctx->l_lvl.size();
+    int* d_djobs = lists + lo; lo += ctx->l_djobs.size();
     unsigned long long* used = reinterpret_cast<unsigned long long*>(meta + ctx->meta_bytes - 256);
     const int2* d_pieces = reinterpret_cast<const int2*>(meta + ctx->off_pieces);
     uint32_t* d_splits = reinterpret_cast<uint32_t*>(meta + ctx->off_splits);
@@ -219,6 +221,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     EVREC(ctx, ctx->ev[1], st);
     // single-literal pages in place, PLAIN fixed-width pages straight into the column (pf_pages.hip)
     launch_snappy_head(d_jobs, int(ctx->jobs.size()), d_pages, d_chunks, d_fallback, d_res, st);
+    launch_snappy_litcopy(d_jobs, d_djobs, int(ctx->l_djobs.size()), d_fallback, st);
     launch_snappy_parse(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent,
                         ctx->d_lane_out, d_splits, d_fallback, st);
     EVREC(ctx, ctx->ev[2], st);
@@ -302,13 +305,14 @@ int plan_snappy(pf_ctx* ctx) {
             ctx->pieces[pi++] = int2{int(j), int(k)};
         }
     }
-    if (lpt) {   // descending cost, ties in page order
-        std::sort(keyed.begin(), keyed.end(), [](uint64_t a, uint64_t b) {
-            const uint64_t ca = a >> 32, cb = b >> 32;
-            return ca != cb ? ca > cb : uint32_t(a) < uint32_t(b);
-        });
+    if (lpt) {   // descending cost in 64-byte buckets (counting sort: O(pieces)), ties in page order
+        constexpr uint32_t NB = 4096;
+        std::vector<uint32_t> start(NB + 1, 0);
+        auto bucket = [](uint64_t k) { return NB - 1 - uint32_t(std::min<uint64_t>((k >> 32) >> 6, NB - 1)); };
+        for (size_t i = 0; i < tp; i++) start[bucket(keyed[i]) + 1]++;
+        for (uint32_t b = 0; b < NB; b++) start[b + 1] += start[b];
         std::vector<int2> sorted(tp);
-        for (size_t i = 0; i < tp; i++) sorted[i] = ctx->pieces[size_t(uint32_t(keyed[i]))];
+        for (size_t i = 0; i < tp; i++) sorted[start[bucket(keyed[i])]++] = ctx->pieces[size_t(uint32_t(keyed[i]))];
         ctx->pieces.swap(sorted);
     }
     const size_t tok_bytes = size_t(n_win) * SNAP_WWORDS * 4, lo_bytes = size_t(n_win) * 64 * 4;
@@ -343,7 +347,7 @@ int upload_meta(pf_ctx* ctx) {
     int* lists = reinterpret_cast<int*>(h + ctx->off_lists);
     size_t lo = 0;
     for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_flat, &ctx->l_decode, &ctx->l_runs,
-                    &ctx->l_dlen, &ctx->l_dba, &ctx->l_lvl}) {
+                    &ctx->l_dlen, &ctx->l_dba, &ctx->l_lvl, &ctx->l_djobs}) {
         std::copy(v->begin(), v->end(), lists + lo);
         lo += v->size();
     }
@@ -877,7 +881,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->chunks.assign(n_chunks, DevChunk{});
     ctx->pages.clear(); ctx->jobs.clear();
     ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_flat.clear(); ctx->l_decode.clear();
-    ctx->l_runs.clear(); ctx->l_dlen.clear(); ctx->l_dba.clear(); ctx->l_lvl.clear();
+    ctx->l_runs.clear(); ctx->l_dlen.clear(); ctx->l_dba.clear(); ctx->l_lvl.clear(); ctx->l_djobs.clear();
     ctx->wins.clear(); ctx->pieces.clear(); ctx->n_splits = 0;
     ctx->host_status.assign(n_chunks, 0);
     ctx->info.assign(n_chunks, pf_column_info{});
@@ -1192,6 +1196,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         }
     }
     mark();
+    for (size_t j = 0; j < ctx->jobs.size(); j++)   // dictionary pages: k_snappy_litcopy candidates
+        if (ctx->pages[size_t(ctx->jobs[j].page)].flags & PG_DICT) ctx->l_djobs.push_back(int(j));
     // ---- Snappy tables: 8 KiB index windows, 64 KiB pieces ----
     {
         int rc = plan_snappy(ctx);
@@ -1205,7 +1211,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_jobs = take(m, sizeof(SnappyJob) * ctx->jobs.size());
     ctx->off_lists = take(m, sizeof(int) * (ctx->l_dictbin.size() + ctx->l_delta.size() + ctx->l_count.size() +
                                             ctx->l_scan.size() + ctx->l_flat.size() + ctx->l_decode.size() + ctx->l_runs.size() +
-                                            ctx->l_dlen.size() + ctx->l_dba.size() + ctx->l_lvl.size()));
+                                            ctx->l_dlen.size() + ctx->l_dba.size() + ctx->l_lvl.size() + ctx->l_djobs.size()));
     ctx->off_res = take(m, sizeof(DevChunkResult) * n_chunks);
     ctx->off_pieces = take(m, sizeof(int2) * ctx->pieces.size());
     ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);

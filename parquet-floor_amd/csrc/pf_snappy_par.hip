@@ -521,7 +521,7 @@ __global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict
     __shared__ __attribute__((aligned(16))) uint32_t sbits[SNAP_WWORDS];
     __shared__ uint32_t slo[64];
     const int2 jw = wins[blockIdx.x];
-    if (fb[jw.x] == FB_INPLACE) return;   // one literal: k_snappy_head pointed the page at it
+    if (fb[jw.x] >= FB_INPLACE) return;   // one literal: in place, or copied by k_snappy_litcopy
     const SnappyJob job = jobs[jw.x];
     const int lane = threadIdx.x;
     const uint64_t n = job.src_len;

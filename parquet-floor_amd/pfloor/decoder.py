@@ -173,7 +173,8 @@ class GpuDecoder:
         return self._staging
 
     def decode(self, descs, buf_ptr, nbytes, on_device=False):
-        arr = (ChunkDesc * max(1, len(descs)))(*descs)
+        """descs: ChunkDesc list, or a prebuilt ctypes ChunkDesc array (no per-call copy)."""
+        arr = descs if isinstance(descs, C.Array) else (ChunkDesc * max(1, len(descs)))(*descs)
         self._keep = arr
         check(lib().pf_decode_row_group(self.h, arr, len(descs), C.c_void_p(buf_ptr), nbytes, 1 if on_device else 0),
               self.h, "pf_decode_row_group")
