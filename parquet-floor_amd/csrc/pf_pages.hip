@@ -1887,6 +1887,28 @@ __device__ __forceinline__ bool flat_fixed_block(FixedLds& S, const DevChunk* __
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
     if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.ptype == 6 || (pg.done & DONE_NULL)) return false;
+    if (pg.direct == DIRECT_VALUES && pg.jfb != nullptr && *pg.jfb <= FB_WHOLE) {
+        // the executor wrote the values (k_snappy_head checked the levels): this block's validity bits
+        const uint32_t ne = uint32_t(pg.num_values), e_begin = uint32_t(pbk.y) * FBLK;
+        if (e_begin >= ne && pbk.y > 0) return true;
+        const uint32_t e_end = min(ne, e_begin + FBLK);
+        if (ck.max_def > 0 && ck.validity && e_end > e_begin) {
+            const uint64_t b0 = uint64_t(pg.entry_start) + e_begin, b1 = uint64_t(pg.entry_start) + e_end;
+            uint32_t* vw = reinterpret_cast<uint32_t*>(ck.validity);
+            for (uint64_t wd = (b0 >> 5) + threadIdx.x; wd <= ((b1 - 1) >> 5); wd += NT) {
+                const uint64_t lo = max(b0, wd << 5), hi = min(b1, (wd + 1) << 5);
+                const uint32_t m = uint32_t((hi - lo >= 32 ? 0xffffffffull : ((1ull << (hi - lo)) - 1ull)) << (lo & 31));
+                if (lo == (wd << 5) && hi == ((wd + 1) << 5)) vw[wd] = m;
+                else atomicOr(vw + wd, m);
+            }
+        }
+        if (threadIdx.x == 0) {
+            if (ck.needs_count == 0)
+                atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values), (unsigned long long)(e_end - e_begin));
+            atomicOr(&pg.done, DONE_FIXED);
+        }
+        return true;
+    }
     Sections s;
     if (!page_sections(pg, ck, s)) return false;
     const int enc = pg.encoding;

@@ -146,20 +146,26 @@ __device__ __forceinline__ uint64_t stage_tok(const uint8_t* stage, uint32_t a, 
 // Walk the chain from c while positions stay below re (bits relative to rs).
 __device__ void lane_walk(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t rs, uint32_t re,
                           uint32_t c, WinLane& L) {
-    L.b0 = L.b1 = L.b2 = L.b3 = 0;
-    L.out = 0;
+    // token-start bits in two 64-bit halves (one shift and one select per token instead of four)
+    uint64_t lo = 0, hi = 0;
+    uint32_t out = 0;
     L.c = c;
     uint64_t p = c;
     bool bad = false;
     while (p < re) {
         uint32_t ol;
         const uint64_t tl = stage_tok(stage, woff + uint32_t(p - W0), ol);
-        bit_set(L, uint32_t(p) - rs);
-        const uint32_t o = L.out + ol;
-        L.out = o < L.out ? 0xffffffffu : o;
+        const uint32_t i = uint32_t(p) - rs;
+        const uint64_t m = 1ull << (i & 63u);
+        lo |= i < 64 ? m : 0ull;
+        hi |= i < 64 ? 0ull : m;
+        const uint32_t o = out + ol;
+        out = o < out ? 0xffffffffu : o;
         p += tl;
         if (p > n) { bad = true; break; }
     }
+    L.b0 = uint32_t(lo); L.b1 = uint32_t(lo >> 32); L.b2 = uint32_t(hi); L.b3 = uint32_t(hi >> 32);
+    L.out = out;
     L.x = bad ? SNAP_INVALID : uint32_t(p);
 }
 
