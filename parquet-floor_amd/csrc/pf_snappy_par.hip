@@ -1123,6 +1123,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
     __shared__ uint16_t tokpos[XCHUNK / 2];
     __shared__ uint32_t sbits[XBATCH / 32];                               // token starts of the step's output
     __shared__ uint32_t wpre[XBATCH / 32];                                // tokens starting in earlier words
+    __shared__ uint16_t jv[256];                                          // pointer-jumping words of a window
     uint8_t* const ring = L;
     uint8_t* const stage = L + X2_STAGE_OFF;
     uint32_t* const fbuf = reinterpret_cast<uint32_t*>(L + X2_FBUF_OFF);
@@ -1357,20 +1358,18 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
                         const uint32_t v = uint32_t(L[addr[u]]);
                         W[u] = pend[u] ? W[u] : (act[u] ? v : 0u);
                     }
-                    // pointer jumping over the window's 256 bytes (a source always precedes its reader)
+                    // pointer jumping over the window's 256 bytes (a source always precedes its reader):
+                    // every round publishes the window's words to LDS (byte x of the window at jv[x]) and
+                    // each pending byte takes the word it points at. A single wave's LDS operations run in
+                    // order, so the reads see this round's writes; one LDS read per byte and round instead
+                    // of two permutes plus the half-word selects (~20 instead of ~60 VALU per round).
                     while (__any(((W[0] | W[1] | W[2] | W[3]) & 0x100u) != 0u)) {
                         if (lane == 0) STAMP_ADD(5, 1);
-                        const uint32_t R01 = W[0] | (W[1] << 16), R23 = W[2] | (W[3] << 16);
+                        #pragma unroll
+                        for (int u = 0; u < 4; u++) jv[64u * uint32_t(u) + uint32_t(lane)] = uint16_t(W[u]);
                         uint32_t G[4];
                         #pragma unroll
-                        for (int u = 0; u < 4; u++) {
-                            const uint32_t pl = W[u] & 0xffu;
-                            const uint32_t g01 = uint32_t(__builtin_amdgcn_ds_bpermute(int((pl & 63u) << 2), int(R01)));
-                            const uint32_t g23 = uint32_t(__builtin_amdgcn_ds_bpermute(int((pl & 63u) << 2), int(R23)));
-                            const uint32_t sl = pl >> 6;
-                            const uint32_t g = sl < 2 ? g01 : g23;
-                            G[u] = (sl & 1u) ? (g >> 16) : (g & 0xffffu);
-                        }
+                        for (int u = 0; u < 4; u++) G[u] = jv[W[u] & 0xffu];
                         #pragma unroll
                         for (int u = 0; u < 4; u++) W[u] = (W[u] & 0x100u) ? G[u] : W[u];
                     }
