@@ -1043,8 +1043,8 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
 #define PF_FT 1024   // 1024: SF1 step 3.82-3.84 vs 3.94-3.97 ms with 2048, 4.04-4.06 with 512 (tools/gpu_ab_libs.sh)
 #endif
 constexpr int FT = PF_FT;            // entries per tile (fewer registers per thread, more blocks resident)
-static_assert(FT <= 2048 && FBLK % FT == 0, "FT = 4096 fails the multi-block parity test; tiles must divide blocks");
 constexpr int FEPT = FT / NT;        // consecutive entries per thread
+static_assert(FT <= int(FBLK) && FBLK % FT == 0 && FEPT <= 32, "tiles divide blocks; a thread's entries fit a 32-bit mask");
 #ifndef PF_RUN_CAP
 #define PF_RUN_CAP 256
 #endif
@@ -1745,8 +1745,8 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
         }
         __syncthreads();
     }
-    for (uint32_t e0 = e_begin; e0 < e_end; e0 += FT) {
-        const uint32_t want = min(uint32_t(FT), e_end - e0);
+    for (uint32_t e0 = e_begin, want = 0; e0 < e_end; e0 += want) {
+        want = min(uint32_t(FT), e_end - e0);
         int bad = 0;
         if (dict) {
             if ((S.vlo > e0 || e0 + want > S.vcover) && S.vres == 2) {
@@ -1757,6 +1757,9 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
                     if (tid == 0) S.vres = rr;
                 }
                 __syncthreads();
+                // a tile whose ids need more runs than the table holds (runs shorter than FT / RUN_CAP
+                // values): this tile is the part the table covers, the next window starts after it
+                if (S.vres == 2 && S.vcover > e0 && e0 + want > S.vcover) want = S.vcover - e0;
             }
             if (id_bw > 32 || s.val_n == 0 || ck.dict_data == nullptr || e0 + want > S.vcover || S.vlo > e0) bad = 1;
             if (!bad && uint32_t(tid) < (want + 63) / 64) S.coff[tid] = uint32_t(run_find(S.vrun, S.nvrun, e0 + tid * 64));
@@ -2088,8 +2091,21 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
     int err = 0;
 
 
-    for (uint32_t e0 = e_begin; e0 < e_end; e0 += FT) {
-        const uint32_t want = min(uint32_t(FT), e_end - e0);
+    for (uint32_t e0 = e_begin, want = 0; e0 < e_end; e0 += want) {
+        want = min(uint32_t(FT), e_end - e0);
+        if (split && dict && S.vres == 2 && (uint64_t(S.vlo) > uint64_t(e0) || e0 + want > S.vcover)) {
+            // all levels present: value index = entry index. Next window of id runs before the levels,
+            // and a tile needing more runs than the table holds shrinks to what it covers
+            __syncthreads();
+            if (tid < 64) {
+                if (tid == 0) { S.vst = RunWalk{0, 0}; S.vlo = e0; }
+                const int rr = wave_walk_runs(ids, ids_n, id_bw, e0, e_end, S.vrun, RUN_CAP, S.nvrun, S.vcover, S.vst,
+                                              RunWalk{0, 0});
+                if (tid == 0) S.vres = rr;
+            }
+            __syncthreads();
+            if (S.vres == 2 && S.vcover > e0 && e0 + want > S.vcover) want = S.vcover - e0;
+        }
         const uint32_t eb = uint32_t(tid) * FEPT;
         for (uint32_t i = tid; i < FT / 32 + 2; i += NT) S.vbits[i] = 0;
         // ---- definition levels -> present bits of this thread's entries
