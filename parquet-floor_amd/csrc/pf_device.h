@@ -134,10 +134,14 @@ __device__ __forceinline__ void rle_init(RleState& s) {
 }
 
 // Walk runs to cover up to `want` values (or until `max_pieces` pieces); returns values covered.
-__device__ inline uint32_t rle_walk(RleState& s, const uint8_t* p, uint64_t n, int bw, uint32_t want,
-                                    Piece* pieces, int max_pieces, int& npieces) {
+// The state lives in LDS in every caller and `pieces` does too: the walk runs on a register copy
+// (otherwise every piece store forces the state to be re-read from LDS — ~10 dependent LDS round
+// trips per piece) and writes it back once.
+__device__ inline uint32_t rle_walk(RleState& s_io, const uint8_t* p, uint64_t n, int bw, uint32_t want,
+                                    Piece* pieces, int max_pieces, int& npieces_io) {
+    RleState s = s_io;
     uint32_t got = 0;
-    npieces = 0;
+    int npieces = 0;
     while (got < want && npieces < max_pieces) {
         if (s.run_left == 0) {
             uint64_t h;
@@ -173,6 +177,8 @@ __device__ inline uint32_t rle_walk(RleState& s, const uint8_t* p, uint64_t n, i
         s.run_left -= c;
         got += c;
     }
+    s_io = s;
+    npieces_io = npieces;
     return got;
 }
 

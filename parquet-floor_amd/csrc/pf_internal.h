@@ -97,7 +97,29 @@ struct DevPage {
     const int* jfb;
     int32_t direct;
     int32_t direct_pad;
+    // nested data pages split into segments of seg_len entries (k_nest_*, pf_pages.hip), else null:
+    // {RleState ck[3][nseg] (rep, def, value stream state at each segment's start), SegRec rec[nseg]}
+    uint8_t* seg;
+    int32_t nseg;
+    int32_t seg_len;
+    int32_t seg_ok;           // k_nest_lvl: 1 = the segment kernels decode the page (k_count / k_decode skip it)
+    int32_t seg_pad;
 };
+
+// One segment of a nested page: its level counts (k_count_seg), their exclusive prefixes over the
+// page (k_nest_scan), the chars of its values and their prefix (k_nest_ids / k_nest_chars).
+struct SegRec {
+    uint32_t ns, nv, nr, pad;
+    uint64_t chars;
+    uint32_t sb, vb, rb, pad2;
+    uint64_t cb;
+};
+constexpr uint32_t NEST_CK_BYTES = 40;      // sizeof(RleState) (pf_device.h)
+constexpr uint32_t NEST_SEG = 8192;         // default entries per segment
+constexpr uint32_t NEST_MAX_SEGS = 1024;    // segments per page (k_nest_scan keeps their targets in LDS)
+__host__ __device__ inline uint64_t nest_seg_bytes(int32_t nseg) {
+    return uint64_t(nseg) * (3ull * NEST_CK_BYTES + sizeof(SegRec));
+}
 
 // k_runs run table of a page: {nruns, values covered, all levels present, valid}, then nruns
 // entries {first | packed << 31, RLE value or bit offset}; a run's count is the next first - first.

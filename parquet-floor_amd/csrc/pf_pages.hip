@@ -623,7 +623,7 @@ __global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunk
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     if (res[pg.chunk].status != 0) return;   // an earlier stage failed this chunk
-    if (pg.counted == 1) return;                 // counted by k_count_flat
+    if (pg.counted == 1 || pg.seg_ok == 1) return;   // counted by k_count_flat / k_count_seg
     Sections s;
     const bool ok = page_sections(pg, ck, s);
     if (threadIdx.x == 0) {
@@ -794,17 +794,28 @@ __device__ inline void flush_bits(const uint32_t* bits, uint64_t b0, uint32_t nb
     }
 }
 
-__device__ void decode_page(const DevChunk* __restrict__ chunks, DevPage* pages, const int pi, DevChunkResult* res,
-                            DecodeLds& S) {
+// One segment of a nested page (k_decode_seg): its entries, where its slots / rows / chars / values
+// start within the page and the rep, def and value stream states at its first entry.
+struct DecodeRange {
+    uint64_t e_b, e_e;
+    uint64_t slot_base, row_base, char_base, vidx;
+    const RleState* st;   // [3], segment-strided (st[k * nseg])
+    int nseg;
+};
+
+__device__ __forceinline__ void decode_page(const DevChunk* __restrict__ chunks, DevPage* pages, const int pi, DevChunkResult* res,
+                            DecodeLds& S, const DecodeRange* R = nullptr) {
     LevelLds& L = S.L;
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
     if (pg.done != 0 || res[pg.chunk].status != 0) return;   // k_flat[_fixed] took it / an earlier stage failed this chunk
+    if (!R && pg.seg_ok == 1) return;                         // k_decode_seg's
     Sections s;
     const bool ok = page_sections(pg, ck, s);
     if (tid == 0) {
-        rle_init(L.srep); rle_init(L.sdef); rle_init(S.sval);
+        if (R) { L.srep = R->st[0]; L.sdef = R->st[R->nseg]; S.sval = R->st[2 * R->nseg]; }
+        else { rle_init(L.srep); rle_init(L.sdef); rle_init(S.sval); }
         L.err = ok ? 0 : 1; S.verr = 0;
     }
     __syncthreads();
@@ -820,10 +831,10 @@ __device__ void decode_page(const DevChunk* __restrict__ chunks, DevPage* pages,
     int id_bw = 0;
     if (dict) {
         id_bw = s.val_n > 0 ? int(s.val[0]) : 0;
-        if (tid == 0) S.sval.pos = 1;
+        if (tid == 0 && !R) S.sval.pos = 1;
     } else if (boolean && enc == 3) {
         // RLE booleans: 4-byte length prefix, then a bit-width-1 hybrid stream
-        if (tid == 0) S.sval.pos = 0;
+        if (tid == 0 && !R) S.sval.pos = 0;
     }
     const uint8_t* rle_bool_p = nullptr; uint64_t rle_bool_n = 0;
     if (boolean && enc == 3) {
@@ -849,10 +860,14 @@ __device__ void decode_page(const DevChunk* __restrict__ chunks, DevPage* pages,
     uint64_t char_base = counted ? uint64_t(pg.char_start) : 0;
     uint64_t vidx = 0;   // page-relative index of the next present value
     const uint64_t bss_total = (enc == 9 && w > 0) ? s.val_n / uint64_t(w) : 0;
-    if (enc == 9 && pg.num_values > 0 && tid == 0) { /* validated per value below */ }
+    uint64_t e_b = 0, e_e = uint64_t(pg.num_values);
+    if (R) {
+        e_b = R->e_b; e_e = R->e_e;
+        slot_base += R->slot_base; row_base += R->row_base; char_base += R->char_base; vidx = R->vidx;
+    }
 
-    for (uint64_t e0 = 0; e0 < uint64_t(pg.num_values); e0 += TILE) {
-        uint32_t want = uint32_t(min<uint64_t>(TILE, uint64_t(pg.num_values) - e0));
+    for (uint64_t e0 = e_b; e0 < e_e; e0 += TILE) {
+        uint32_t want = uint32_t(min<uint64_t>(TILE, e_e - e0));
         decode_level_tile(L, s, ck, e0, want);
         if (L.err) break;
         // per-thread: EPT consecutive entries
@@ -2811,7 +2826,325 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     }
 }
 
+// ---- nested pages in segments (k_nest_*) --------------------------------------------------------
+// A nested page's levels are walked run by run from its first entry, so k_count / k_decode take it in
+// ONE workgroup tile after tile: a 520K-entry page (one per chunk in config 5) runs ~1000 tiles in
+// series on one CU. Here the page is cut into segments of seg_len entries, each decoded by its own
+// workgroup from checkpoints of the three hybrid streams (rep, def, dictionary ids):
+//   k_nest_lvl   (page x {rep, def}, one wave): the stream's run headers, walked from LDS windows,
+//                give the state at every segment start;
+//   k_count_seg  (page x segment): slots / values / rows of the segment's levels;
+//   k_nest_scan  (page, one wave): their prefixes over the page, the page totals (k_scan), and the
+//                dictionary-id stream's state at each segment's first value;
+//   k_nest_ids   (page x segment, BYTE_ARRAY dictionary): ids kept for k_decode_seg, chars;
+//   k_nest_chars (page, one wave): the segments' chars prefix, the page's chars;
+//   k_decode_seg (page x segment): decode_page over the segment.
+// Checkpoint states are exactly rle_walk's state after the segment's first t values (mid-run when t
+// falls inside a run), so each segment's decode is the serial walk's, from t on.
+constexpr uint32_t NW_BYTES = 8192;   // k_nest_* LDS window over a stream
+static_assert(sizeof(RleState) == NEST_CK_BYTES, "checkpoint size (host plans the segment tables)");
+
+__device__ __forceinline__ RleState* nest_ck(const DevPage& pg, int k) {
+    return reinterpret_cast<RleState*>(pg.seg) + size_t(k) * size_t(pg.nseg);
+}
+__device__ __forceinline__ SegRec* nest_rec(const DevPage& pg) {
+    return reinterpret_cast<SegRec*>(pg.seg + 3ull * NEST_CK_BYTES * uint64_t(pg.nseg));
+}
+__device__ __forceinline__ RleState rle_sentinel() {   // a target the stream never reached: walking from it fails
+    RleState s;
+    rle_init(s);
+    s.pos = ~uint64_t(0);
+    s.err = 1;
+    return s;
+}
+
+// One wave: walk the hybrid stream p[0, n) (bit width bw) from byte pos0 (a run header), and store in
+// out[k] the state after target(k) values, k < nt (targets non-decreasing). Targets the stream does
+// not reach (it ends, breaks, or holds fewer values) get rle_sentinel(). All lanes walk in step (the
+// LDS reads broadcast); lane 0 writes.
+template <typename Target>
+__device__ void nest_walk(uint32_t* st, const uint8_t* p, uint64_t n, int bw, uint64_t pos0, int nt, Target target,
+                          RleState* out) {
+    const int lane = threadIdx.x & 63;
+    int k = 0;
+    uint64_t e = 0, pos = pos0;
+    uint64_t wb = ~uint64_t(0);   // stream offset of the window's first byte (st byte woff)
+    uint32_t woff = 0;
+    const uint8_t* W = reinterpret_cast<const uint8_t*>(st);
+    const int nbv = (bw + 7) >> 3;
+    uint64_t t = nt > 0 ? target(0) : 0;
+    while (k < nt && pos < n) {
+        if (wb == ~uint64_t(0) || pos < wb || pos + 16 > wb + NW_BYTES) {
+            __syncthreads();
+            wb = pos;
+            woff = stage_bytes(st, p, n, uint32_t(pos), uint32_t(min<uint64_t>(n, pos + NW_BYTES)));
+            __syncthreads();
+        }
+        // header (uvarint, <= 10 bytes) and an RLE value (<= 4 bytes) lie inside the window
+        const uint8_t* q = W + woff + (pos - wb);
+        uint64_t h = 0;
+        uint32_t hl = 0;
+        bool hok = false;
+        for (uint32_t sh = 0; sh < 70; sh += 7) {
+            if (pos + hl >= n) break;
+            const uint32_t c = q[hl++];
+            h |= uint64_t(c & 0x7f) << sh;
+            if (!(c & 0x80)) { hok = true; break; }
+        }
+        if (!hok) break;
+        const uint64_t a = pos + hl;
+        uint64_t cnt, next, bit0 = 0;
+        uint32_t val = 0;
+        const uint32_t packed = uint32_t(h & 1);
+        if (packed) {
+            const uint64_t groups = h >> 1;
+            cnt = groups * 8;
+            bit0 = a * 8;
+            const uint64_t nb = groups * uint64_t(bw), avail = n - a;
+            next = a + (nb < avail ? nb : avail);
+        } else {
+            cnt = h >> 1;
+            if (a + nbv > n) break;
+            for (int b = 0; b < nbv; b++) val |= uint32_t(q[hl + b]) << (8 * b);
+            next = a + nbv;
+        }
+        while (k < nt && t < e + cnt) {
+            if (lane == 0) {
+                RleState r;
+                r.pos = next;
+                r.run_left = e + cnt - t;
+                r.run_bit = packed ? bit0 + (t - e) * uint64_t(bw) : 0;
+                r.run_val = val;
+                r.run_packed = int32_t(packed);
+                r.err = 0;
+                out[k] = r;
+            }
+            k++;
+            if (k < nt) t = target(k);
+        }
+        e += cnt;
+        pos = next;
+    }
+    for (; k < nt; k++)
+        if (lane == 0) out[k] = rle_sentinel();
+}
+
+// the page's segment path applies: rep / def sections parse and are RLE hybrid streams
+__device__ __forceinline__ bool nest_sections(const DevPage& pg, const DevChunk& ck, Sections& s) {
+    return pg.seg != nullptr && ck.max_rep > 0 && page_sections(pg, ck, s) && s.rep_rle && (ck.max_def == 0 || s.def_rle);
+}
+
+__global__ __launch_bounds__(64) void k_nest_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
+                                                 DevChunkResult* res) {
+    __shared__ __attribute__((aligned(16))) uint32_t st[(NW_BYTES + 64) / 4];
+    const int pi = list[blockIdx.x];
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    Sections s;
+    if (res[pg.chunk].status != 0 || !nest_sections(pg, ck, s)) return;   // (seg_ok stays 0: k_count / k_decode)
+    const int which = blockIdx.y;   // 0 = rep, 1 = def
+    const int nseg = pg.nseg;
+    const uint32_t sl = uint32_t(pg.seg_len);
+    RleState* out = nest_ck(pg, which);
+    if (which == 1 && ck.max_def == 0) {
+        for (int k = threadIdx.x; k < nseg; k += 64) { RleState r; rle_init(r); out[k] = r; }
+    } else {
+        const uint8_t* p = which == 0 ? s.rep : s.def;
+        const uint64_t n = which == 0 ? s.rep_n : s.def_n;
+        nest_walk(st, p, n, bit_width(uint32_t(which == 0 ? ck.max_rep : ck.max_def)), 0, nseg,
+                  [sl](int k) { return uint64_t(k) * sl; }, out);
+    }
+    if (which == 0 && threadIdx.x == 0) pg.seg_ok = 1;
+}
+
+__global__ __launch_bounds__(NT) void k_count_seg(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                  const int2* __restrict__ list, DevChunkResult* res) {
+    __shared__ LevelLds L;
+    __shared__ uint32_t scan_tmp[NT / 64];
+    const int pi = list[blockIdx.x].x, sg = list[blockIdx.x].y;
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    if (pg.seg_ok != 1 || res[pg.chunk].status != 0) return;
+    Sections s;
+    page_sections(pg, ck, s);   // (parsed by k_nest_lvl)
+    const uint64_t e_b = uint64_t(sg) * uint32_t(pg.seg_len);
+    const uint64_t e_e = min<uint64_t>(uint64_t(pg.num_values), e_b + uint32_t(pg.seg_len));
+    if (threadIdx.x == 0) { L.srep = nest_ck(pg, 0)[sg]; L.sdef = nest_ck(pg, 1)[sg]; L.err = 0; }
+    __syncthreads();
+    uint64_t slots = 0, vals = 0, rows = 0;
+    for (uint64_t e0 = e_b; e0 < e_e; e0 += TILE) {
+        const uint32_t want = uint32_t(min<uint64_t>(TILE, e_e - e0));
+        decode_level_tile(L, s, ck, e0, want);
+        if (L.err) break;
+        uint32_t ns = 0, nv = 0, nr = 0;
+        for (uint32_t i = threadIdx.x; i < want; i += NT) {
+            const int d = L.def[i];
+            ns += d >= ck.repeated_def;
+            nv += d == ck.max_def;
+            nr += L.rep[i] == 0;
+        }
+        uint32_t t;
+        block_excl_scan<NT>(ns, scan_tmp, t); slots += t;
+        block_excl_scan<NT>(nr, scan_tmp, t); rows += t;
+        block_excl_scan<NT>(nv, scan_tmp, t); vals += t;
+        __syncthreads();
+    }
+    if (L.err) { if (threadIdx.x == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
+    if (threadIdx.x == 0) {
+        SegRec& r = nest_rec(pg)[sg];
+        r.ns = uint32_t(slots); r.nv = uint32_t(vals); r.nr = uint32_t(rows); r.chars = 0;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_nest_scan(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
+                                                  DevChunkResult* res) {
+    __shared__ __attribute__((aligned(16))) uint32_t st[(NW_BYTES + 64) / 4];
+    __shared__ uint32_t vb[NEST_MAX_SEGS];
+    const int pi = list[blockIdx.x];
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    if (pg.seg_ok != 1 || res[pg.chunk].status != 0) return;
+    const int nseg = pg.nseg, lane = threadIdx.x;
+    SegRec* R = nest_rec(pg);
+    uint64_t cs = 0, cv = 0, cr = 0;
+    for (int k0 = 0; k0 < nseg; k0 += 64) {
+        const int k = k0 + lane;
+        uint64_t ns = 0, nv = 0, nr = 0;
+        if (k < nseg) { ns = R[k].ns; nv = R[k].nv; nr = R[k].nr; }
+        uint64_t xs = ns, xv = nv, xr = nr;
+        #pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t ys = __shfl_up(xs, d, 64), yv = __shfl_up(xv, d, 64), yr = __shfl_up(xr, d, 64);
+            if (lane >= d) { xs += ys; xv += yv; xr += yr; }
+        }
+        if (k < nseg) {
+            R[k].sb = uint32_t(cs + xs - ns); R[k].vb = uint32_t(cv + xv - nv); R[k].rb = uint32_t(cr + xr - nr);
+            vb[k] = uint32_t(cv + xv - nv);
+        }
+        cs += __shfl(xs, 63, 64); cv += __shfl(xv, 63, 64); cr += __shfl(xr, 63, 64);
+    }
+    if (lane == 0) { pg.n_slots = int64_t(cs); pg.n_values = int64_t(cv); pg.n_rows = int64_t(cr); pg.n_chars = 0; }
+    __syncthreads();
+    // dictionary ids: the stream's state at each segment's first value
+    if (is_dict_enc(pg.encoding)) {
+        Sections s;
+        page_sections(pg, ck, s);
+        RleState* out = nest_ck(pg, 2);
+        const int id_bw = s.val_n > 0 ? int(s.val[0]) : 0;
+        if (s.val_n == 0 || id_bw > 32) {
+            for (int k = lane; k < nseg; k += 64) out[k] = rle_sentinel();   // (decode reports it)
+        } else {
+            nest_walk(st, s.val, s.val_n, id_bw, 1, nseg, [](int k) { return uint64_t(vb[k]); }, out);
+        }
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_nest_ids(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                 const int2* __restrict__ list, DevChunkResult* res) {
+    __shared__ Piece pval[TILE];
+    __shared__ uint32_t ids[TILE];
+    __shared__ RleState sval;
+    __shared__ int npval, verr;
+    __shared__ unsigned long long chars_acc;
+    const int pi = list[blockIdx.x].x, sg = list[blockIdx.x].y;
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    if (pg.seg_ok != 1 || res[pg.chunk].status != 0 || ck.ptype != 6 || !is_dict_enc(pg.encoding)) return;
+    Sections s;
+    page_sections(pg, ck, s);
+    SegRec& rec = nest_rec(pg)[sg];
+    const uint64_t v_b = rec.vb, v_e = v_b + rec.nv;
+    const int id_bw = s.val_n > 0 ? int(s.val[0]) : 0;
+    if (threadIdx.x == 0) { sval = nest_ck(pg, 2)[sg]; verr = 0; chars_acc = 0; }
+    __syncthreads();
+    for (uint64_t v0 = v_b; v0 < v_e; v0 += TILE) {
+        const uint32_t t = uint32_t(min<uint64_t>(TILE, v_e - v0));
+        if (threadIdx.x == 0) {
+            if (id_bw > 32 || !ck.dict_len) verr = 1;
+            else {
+                const uint32_t got = rle_walk(sval, s.val, s.val_n, id_bw, t, pval, TILE, npval);
+                if (got != t || sval.err) verr = 1;
+            }
+        }
+        __syncthreads();
+        if (verr) break;
+        rle_expand<uint32_t>(pval, npval, s.val, s.val_n, id_bw, ids);
+        __syncthreads();
+        uint64_t acc = 0;
+        int bad = 0;
+        for (uint32_t i = threadIdx.x; i < t; i += NT) {
+            const uint32_t id = ids[i];
+            if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
+            acc += ck.dict_len[id];
+            pg.aux[v0 + i] = id;
+        }
+        if (__syncthreads_or(bad)) { if (threadIdx.x == 0) verr = 1; __syncthreads(); break; }
+        atomicAdd(&chars_acc, (unsigned long long)acc);
+        __syncthreads();
+    }
+    if (verr) { if (threadIdx.x == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
+    __syncthreads();
+    if (threadIdx.x == 0) rec.chars = chars_acc;
+}
+
+__global__ __launch_bounds__(64) void k_nest_chars(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
+                                                   DevChunkResult* res) {
+    const int pi = list[blockIdx.x];
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    if (pg.seg_ok != 1 || res[pg.chunk].status != 0 || ck.ptype != 6) return;
+    const int nseg = pg.nseg, lane = threadIdx.x;
+    SegRec* R = nest_rec(pg);
+    uint64_t cc = 0;
+    for (int k0 = 0; k0 < nseg; k0 += 64) {
+        const int k = k0 + lane;
+        const uint64_t c = k < nseg ? R[k].chars : 0;
+        uint64_t x = c;
+        #pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (k < nseg) R[k].cb = cc + x - c;
+        cc += __shfl(x, 63, 64);
+    }
+    if (lane == 0) pg.n_chars = int64_t(cc);
+}
+
+__global__ __launch_bounds__(NT) void k_decode_seg(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                   const int2* __restrict__ list, DevChunkResult* res) {
+    __shared__ DecodeLds S;
+    const int pi = list[blockIdx.x].x, sg = list[blockIdx.x].y;
+    const DevPage& pg = pages[pi];
+    if (pg.seg_ok != 1) return;
+    const SegRec& rec = nest_rec(pg)[sg];
+    DecodeRange R;
+    R.e_b = uint64_t(sg) * uint32_t(pg.seg_len);
+    R.e_e = min<uint64_t>(uint64_t(pg.num_values), R.e_b + uint32_t(pg.seg_len));
+    R.slot_base = rec.sb; R.row_base = rec.rb; R.vidx = rec.vb;
+    R.char_base = chunks[pg.chunk].ptype == 6 ? rec.cb : 0;
+    R.st = nest_ck(pg, 0) + sg;
+    R.nseg = pg.nseg;
+    decode_page(chunks, pages, pi, res, S, &R);
+}
+
 // ---- launchers -------------------------------------------------------------------------------
+void launch_nest_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
+                     hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(k_nest_lvl, dim3(n, 2), dim3(64), 0, st, d_chunks, d_pages, d_list, d_res);
+}
+void launch_nest_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, const int2* d_segs, int n_segs,
+                       DevChunkResult* d_res, hipStream_t st) {
+    if (n <= 0 || n_segs <= 0) return;
+    hipLaunchKernelGGL(k_count_seg, dim3(n_segs), dim3(NT), 0, st, d_chunks, d_pages, d_segs, d_res);
+    hipLaunchKernelGGL(k_nest_scan, dim3(n), dim3(64), 0, st, d_chunks, d_pages, d_list, d_res);
+    hipLaunchKernelGGL(k_nest_ids, dim3(n_segs), dim3(NT), 0, st, d_chunks, d_pages, d_segs, d_res);
+    hipLaunchKernelGGL(k_nest_chars, dim3(n), dim3(64), 0, st, d_chunks, d_pages, d_list, d_res);
+}
+void launch_nest_decode(const DevChunk* d_chunks, DevPage* d_pages, const int2* d_segs, int n_segs, DevChunkResult* d_res,
+                        hipStream_t st) {
+    if (n_segs > 0) hipLaunchKernelGGL(k_decode_seg, dim3(n_segs), dim3(NT), 0, st, d_chunks, d_pages, d_segs, d_res);
+}
 void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                   BaJob* d_bajobs, hipStream_t st) {
     if (n <= 0) return;

@@ -40,6 +40,9 @@ void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hi
 void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
+void launch_nest_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_nest_count(const DevChunk*, DevPage*, const int*, int, const int2*, int, DevChunkResult*, hipStream_t);
+void launch_nest_decode(const DevChunk*, DevPage*, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_page_scan(const ScanChunk*, int, pf_page_desc*, ScanCrc*, ScanResult*, hipStream_t);
 void launch_page_crc(const ScanCrc*, const int*, int, ScanResult*, int32_t*, hipStream_t);
 }  // namespace pf
@@ -134,7 +137,7 @@ struct pf_ctx {
     std::vector<DevChunk> chunks;          // host copies (device pointers)
     std::vector<DevPage> pages;
     std::vector<SnappyJob> jobs;
-    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode, l_runs, l_dlen, l_dba, l_lvl, l_djobs;
+    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode, l_runs, l_dlen, l_dba, l_lvl, l_djobs, l_nest, l_nseg;
     std::vector<int2> wins, pieces;       // Snappy index windows / 64 KiB pieces (job, index)
     std::vector<BaJob> bajobs;             // PLAIN BYTE_ARRAY walks: dictionary pages, then data pages
     std::vector<int2> ba_tiles;            // (job relative to its batch, tile)
@@ -211,6 +214,9 @@ int enqueue_kernels(pf_ctx* ctx) {
     int* d_dba = lists + lo; lo += ctx->l_dba.size();
     int* d_lvl = lists + lo; lo += ctx->l_lvl.size();
     int* d_djobs = lists + lo; lo += ctx->l_djobs.size();
+    int* d_nest = lists + lo; lo += ctx->l_nest.size();
+    const int2* d_nseg = reinterpret_cast<const int2*>(lists + lo); lo += ctx->l_nseg.size();
+    const int n_nest = int(ctx->l_nest.size()), n_nseg = int(ctx->l_nseg.size() / 2);
     unsigned long long* used = reinterpret_cast<unsigned long long*>(meta + ctx->meta_bytes - 256);
     const int2* d_pieces = reinterpret_cast<const int2*>(meta + ctx->off_pieces);
     uint32_t* d_splits = reinterpret_cast<uint32_t*>(meta + ctx->off_splits);
@@ -247,7 +253,9 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st);
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
     EVREC(ctx, ctx->ev[5], st);
+    launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, d_res, st);
     launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st);
+    launch_nest_count(d_chunks, d_pages, d_nest, n_nest, d_nseg, n_nseg, d_res, st);
     launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
               d_res, st);
     EVREC(ctx, ctx->ev[6], st);
@@ -257,6 +265,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty());
     EVREC(ctx, ctx->ev[8], st);
     launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), ctx->n_decode_first, d_res, st);
+    launch_nest_decode(d_chunks, d_pages, d_nseg, n_nseg, d_res, st);
     launch_dba_chars(d_chunks, d_pages, d_dba, int(ctx->l_dba.size()), d_res, st);
     EVREC(ctx, ctx->ev[9], st);
     HIPCHK(ctx, hipGetLastError());
@@ -347,7 +356,7 @@ int upload_meta(pf_ctx* ctx) {
     int* lists = reinterpret_cast<int*>(h + ctx->off_lists);
     size_t lo = 0;
     for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_flat, &ctx->l_decode, &ctx->l_runs,
-                    &ctx->l_dlen, &ctx->l_dba, &ctx->l_lvl, &ctx->l_djobs}) {
+                    &ctx->l_dlen, &ctx->l_dba, &ctx->l_lvl, &ctx->l_djobs, &ctx->l_nest, &ctx->l_nseg}) {
         std::copy(v->begin(), v->end(), lists + lo);
         lo += v->size();
     }
@@ -882,6 +891,16 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->pages.clear(); ctx->jobs.clear();
     ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_flat.clear(); ctx->l_decode.clear();
     ctx->l_runs.clear(); ctx->l_dlen.clear(); ctx->l_dba.clear(); ctx->l_lvl.clear(); ctx->l_djobs.clear();
+    ctx->l_nest.clear(); ctx->l_nseg.clear();
+    // nested pages: entries per segment (k_nest_*); PF_NEST_SEG=n (tests) sets it and sends every
+    // eligible nested page, one segment or more, down the segment path (0: none)
+    int64_t nest_seg_len = NEST_SEG;
+    bool nest_seg_forced = false;
+    if (const char* e = std::getenv("PF_NEST_SEG")) {
+        nest_seg_len = std::atoll(e);
+        nest_seg_forced = nest_seg_len > 0;
+        if (nest_seg_len <= 0) nest_seg_len = int64_t(1) << 40;   // every page stays on k_count / k_decode
+    }
     ctx->wins.clear(); ctx->pieces.clear(); ctx->n_splits = 0;
     ctx->host_status.assign(n_chunks, 0);
     ctx->info.assign(n_chunks, pf_column_info{});
@@ -899,7 +918,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->d_bytes = d_bytes;
 
     // ---- plan: sizes of scratch / outputs ----
-    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; uint64_t lt_off; };
+    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; uint64_t lt_off; uint64_t seg_off; int32_t nseg, seg_len; };
     std::vector<PagePlan> pplan;
     size_t scratch = 0, out = 0, bits = 0;
     uint64_t chars_hint = 0;
@@ -947,7 +966,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     hs = PF_ERR_CORRUPT_PAGE; break;
                 }
                 bool compressed = cd.codec == PF_CODEC_SNAPPY && (!v2 || pd.is_compressed);
-                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull, ~0ull};
+                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull, ~0ull, ~0ull, 0, 0};
                 if (v2) { pg.lvl = src; pg.rep_len = uint32_t(pd.rep_bytes); pg.def_len = uint32_t(pd.def_bytes); }
                 if (compressed) {
                     pp.scratch_off = take(scratch, pd.uncompressed_size - lvl, 16);
@@ -991,6 +1010,21 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                         (pd.encoding == PF_ENC_PLAIN || pd.encoding == PF_ENC_PLAIN_DICTIONARY || pd.encoding == PF_ENC_RLE_DICTIONARY))
                         pp.lt_off = take(scratch, 16 + 16ull * lvl_table_cap(pd.num_values) +
                                                       4ull * LT_BT_WORDS * (uint64_t(pd.num_values) / FLAT_BLK + 1), 256);   // k_lvl tables
+                    {   // nested pages decoded in segments (k_nest_*): PLAIN fixed width, dictionary, DELTA_BINARY_PACKED ints
+                        const int e = pd.encoding;
+                        const bool enc_ok = (e == PF_ENC_PLAIN && cd.physical_type != PF_BYTE_ARRAY) ||
+                                            e == PF_ENC_PLAIN_DICTIONARY || e == PF_ENC_RLE_DICTIONARY ||
+                                            (e == PF_ENC_DELTA_BINARY_PACKED && (cd.physical_type == PF_INT32 || cd.physical_type == PF_INT64));
+                        if (cd.max_rep > 0 && cd.physical_type != PF_BOOLEAN && enc_ok && pd.num_values > 0) {
+                            const int64_t sl = std::max<int64_t>(nest_seg_len, (int64_t(pd.num_values) + NEST_MAX_SEGS - 1) / NEST_MAX_SEGS);
+                            const int64_t ns = (int64_t(pd.num_values) + sl - 1) / sl;
+                            if (ns >= 2 || nest_seg_forced) {
+                                pp.seg_len = int32_t(sl);
+                                pp.nseg = int32_t(ns);
+                                pp.seg_off = take(scratch, nest_seg_bytes(pp.nseg), 256);
+                            }
+                        }
+                    }
                 }
                 pplan.push_back(pp);
                 ctx->pages.push_back(pg);
@@ -1082,6 +1116,13 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                 pg.lvltab = reinterpret_cast<uint32_t*>(S + pp.lt_off);
                 pg.lvl_cap = lvl_table_cap(pg.num_values);
                 ctx->l_lvl.push_back(int(i));
+            }
+            if (pp.seg_off != ~0ull) {
+                pg.seg = S + pp.seg_off;
+                pg.nseg = pp.nseg;
+                pg.seg_len = pp.seg_len;
+                ctx->l_nest.push_back(int(i));
+                for (int k = 0; k < pp.nseg; k++) { ctx->l_nseg.push_back(int(i)); ctx->l_nseg.push_back(k); }
             }
             if (pp.dx_off != ~0ull) {
                 pg.dx = reinterpret_cast<uint64_t*>(S + pp.dx_off);
@@ -1211,7 +1252,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_jobs = take(m, sizeof(SnappyJob) * ctx->jobs.size());
     ctx->off_lists = take(m, sizeof(int) * (ctx->l_dictbin.size() + ctx->l_delta.size() + ctx->l_count.size() +
                                             ctx->l_scan.size() + ctx->l_flat.size() + ctx->l_decode.size() + ctx->l_runs.size() +
-                                            ctx->l_dlen.size() + ctx->l_dba.size() + ctx->l_lvl.size() + ctx->l_djobs.size()));
+                                            ctx->l_dlen.size() + ctx->l_dba.size() + ctx->l_lvl.size() + ctx->l_djobs.size() +
+                                            ctx->l_nest.size() + ctx->l_nseg.size()));
     ctx->off_res = take(m, sizeof(DevChunkResult) * n_chunks);
     ctx->off_pieces = take(m, sizeof(int2) * ctx->pieces.size());
     ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);
