@@ -19,6 +19,7 @@ namespace pf {
 
 constexpr int DNT = 256;
 constexpr int MB_CAP = 1024;   // miniblocks per round
+constexpr int DVPT = 8;        // values per thread per tile
 
 struct MiniBlock {
     uint64_t bitpos;     // absolute bit position of the miniblock's packed data
@@ -121,36 +122,53 @@ __device__ bool dbp_decode_wg(DbpLds& S, const uint8_t* p, uint64_t n, bool is64
         if (S.err) break;
         const uint64_t r0 = S.have_s, r1 = S.rend;
         const int nk = S.nmb;
-        // ---- all threads: deltas -> values, tile by tile with a carried prefix ----
-        for (uint64_t t0 = r0; t0 < r1; t0 += DNT) {
-            const uint64_t i = t0 + threadIdx.x;
-            uint64_t d = 0;
-            if (i < r1) {
-                const uint64_t j = i - r0;                       // delta index within this round
-                const uint64_t m = j / vpm, q = j % vpm;
-                if (m < uint64_t(nk)) {
-                    const MiniBlock& b = S.mb[m];
-                    d = uint64_t(b.min_delta) + bits_le64(p, n, b.bitpos + q * uint64_t(b.width), b.width);
+        // ---- all threads: deltas -> values, tile by tile with a carried prefix; DVPT consecutive
+        // values per thread (one workgroup scan per DNT * DVPT values) ----
+        for (uint64_t t0 = r0; t0 < r1; t0 += uint64_t(DNT) * DVPT) {
+            const uint64_t i0 = t0 + uint64_t(threadIdx.x) * DVPT;
+            uint64_t d[DVPT];
+            uint64_t tsum = 0;
+            #pragma unroll
+            for (int k = 0; k < DVPT; k++) {
+                const uint64_t i = i0 + k;
+                uint64_t dk = 0;
+                if (i < r1) {
+                    const uint64_t j = i - r0;                       // delta index within this round
+                    const uint64_t m = j / vpm, q = j % vpm;
+                    if (m < uint64_t(nk)) {
+                        const MiniBlock& b = S.mb[m];
+                        dk = uint64_t(b.min_delta) + bits_le64(p, n, b.bitpos + q * uint64_t(b.width), b.width);
+                    }
                 }
+                tsum += dk;
+                d[k] = tsum;                                         // inclusive within the thread
             }
-            // inclusive scan of d across the workgroup
+            // exclusive scan of the thread sums across the workgroup
             const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-            uint64_t x = d;
+            uint64_t x = tsum;
             #pragma unroll
             for (int sh = 1; sh < 64; sh <<= 1) {
                 const uint64_t y = __shfl_up(x, sh, 64);
                 if (lane >= sh) x += y;
             }
-            __syncthreads();
             if (lane == 63) S.wsum[wid] = x;
             __syncthreads();
-            uint64_t base = S.carry;
-            for (int w2 = 0; w2 < wid; w2++) base += S.wsum[w2];
-            uint64_t v = base + x;
-            if (!is64) v = uint64_t(uint32_t(v));
-            if (i < r1 && i < cap) out[i] = v;
-            __syncthreads();
-            if (i < r1 && i + 1 == min<uint64_t>(r1, t0 + DNT)) S.carry = v;
+            uint64_t base = S.carry, all = 0;
+            for (int w2 = 0; w2 < DNT / 64; w2++) {
+                const uint64_t ws = S.wsum[w2];
+                if (w2 < wid) base += ws;
+                all += ws;
+            }
+            base += x - tsum;
+            #pragma unroll
+            for (int k = 0; k < DVPT; k++) {
+                const uint64_t i = i0 + k;
+                uint64_t v = base + d[k];
+                if (!is64) v = uint64_t(uint32_t(v));
+                if (i < r1 && i < cap) out[i] = v;
+            }
+            __syncthreads();   // every thread read carry and wsum
+            if (threadIdx.x == 0) S.carry = S.carry + all;
             __syncthreads();
         }
         if (threadIdx.x == 0) S.have_s = r1;

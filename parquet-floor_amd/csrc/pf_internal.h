@@ -103,8 +103,20 @@ struct DevPage {
     int32_t nseg;
     int32_t seg_len;
     int32_t seg_ok;           // k_nest_lvl: 1 = the segment kernels decode the page (k_count / k_decode skip it)
-    int32_t seg_pad;
+    int32_t nwin;             // k_nest_lvl windows per level stream (the page's bytes / NEST_WIN, rounded up)
+    struct WinPub* npub;      // [2][nwin]: what each window of the rep / def stream passes to the next (zeroed per batch)
 };
+
+// k_nest_lvl: a window's hand-over to the next window of its stream: the position of the first run
+// header at or past the window's end, the entries before it, and whether the chain ended (st = 1).
+struct WinPub {
+    uint32_t flag;            // 0 until published
+    uint32_t st;
+    uint64_t p;
+    uint64_t e;
+    uint64_t pad;
+};
+constexpr uint32_t NEST_WIN = 8192;         // k_nest_lvl window bytes
 
 // One segment of a nested page: its level counts (k_count_seg), their exclusive prefixes over the
 // page (k_nest_scan), the chars of its values and their prefix (k_nest_ids / k_nest_chars).
@@ -115,7 +127,7 @@ struct SegRec {
     uint64_t cb;
 };
 constexpr uint32_t NEST_CK_BYTES = 40;      // sizeof(RleState) (pf_device.h)
-constexpr uint32_t NEST_SEG = 8192;         // default entries per segment
+constexpr uint32_t NEST_SEG = 2048;         // default entries per segment
 constexpr uint32_t NEST_MAX_SEGS = 1024;    // segments per page (k_nest_scan keeps their targets in LDS)
 __host__ __device__ inline uint64_t nest_seg_bytes(int32_t nseg) {
     return uint64_t(nseg) * (3ull * NEST_CK_BYTES + sizeof(SegRec));

@@ -742,6 +742,61 @@ __global__ __launch_bounds__(64) void k_scan(DevChunk* chunks, DevPage* pages, c
     if (ck.max_rep == 1 && ck.list_offsets) ck.list_offsets[r] = int32_t(s);
 }
 
+// Stage bytes [b0, b1) of stream p[0, n) into LDS words st: byte b0 + i of the stream is byte
+// off + i of st (off = the 16-byte misalignment of p + b0); stream bytes at or past n read as zero
+// (parquet-mr zero-pads a truncated bit-packed run), as do the 16 bytes after the range.
+__device__ __forceinline__ uint32_t stage_bytes(uint32_t* st, const uint8_t* p, uint64_t n, uint32_t b0, uint32_t b1) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p) + b0;
+    const uint32_t off = uint32_t(a & 15u);
+    if (b1 <= b0) return off;
+    const uint32_t nchunk = (off + (b1 - b0) + 15u) / 16u;
+    const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(a - off);
+    const int64_t base = int64_t(b0) - int64_t(off);   // stream offset of st byte 0
+    for (uint32_t c = threadIdx.x; c <= nchunk; c += blockDim.x) {
+        u32x4 v = {0u, 0u, 0u, 0u};
+        const int64_t cb = base + 16 * int64_t(c);   // stream offset of the chunk
+        if (c < nchunk && cb < int64_t(n)) {
+            v = src[c];
+            if (cb + 16 > int64_t(n)) {
+                #pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int64_t keep = int64_t(n) - (cb + 4 * q);   // valid bytes of word q
+                    const uint32_t mask = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
+                    v[q] &= mask;
+                }
+            }
+        }
+        reinterpret_cast<u32x4*>(st)[c] = v;
+    }
+    return off;
+}
+
+// Segment path (k_nest_*): the bytes of hybrid stream p[0, n) one segment reads, from the state at
+// its first entry (a) to the next segment's (b: the header after the run holding the next segment's
+// first entry; null or a sentinel = the stream's end), staged in LDS buffer buf of cap bytes. On
+// success p / n become the LDS copy (stream byte lo + i at p[i]; bytes past the staged range read as
+// zero but the segment's walk never needs them) and lo is returned: the caller rebases its walk
+// state with rle_rebase. Returns 0 and leaves p / n alone when the range does not fit. All threads call.
+__device__ __forceinline__ uint64_t stage_seg(uint32_t* buf, uint32_t cap, const uint8_t*& p, uint64_t& n,
+                                              const RleState& a, const RleState* b) {
+    if (a.err || n == 0 || n > 0xffffffffull) return 0;
+    const uint64_t lo = (a.run_packed && a.run_left > 0) ? (a.run_bit >> 3) : a.pos;
+    uint64_t hi = (b && !b->err) ? b->pos : n;
+    if (lo >= n) return 0;
+    hi = min<uint64_t>(n, hi + 16);
+    if (hi <= lo || hi - lo + 48 > cap) return 0;
+    const uint32_t off = stage_bytes(buf, p, n, uint32_t(lo), uint32_t(hi));
+    __syncthreads();
+    p = reinterpret_cast<const uint8_t*>(buf) + off;
+    n = hi - lo;
+    return lo;
+}
+__device__ __forceinline__ void rle_rebase(RleState& s, uint64_t lo) {
+    if (lo == 0) return;
+    s.pos -= lo;
+    if (s.run_packed && s.run_left > 0) s.run_bit -= 8 * lo;
+}
+
 // ---- k_decode ----------------------------------------------------------------------------------
 struct DecodeLds {
     LevelLds L;
@@ -800,8 +855,11 @@ struct DecodeRange {
     uint64_t e_b, e_e;
     uint64_t slot_base, row_base, char_base, vidx;
     const RleState* st;   // [3], segment-strided (st[k * nseg])
+    const RleState* nx;   // the next segment's, or null
     int nseg;
+    uint32_t* buf[3];     // LDS for the segment's rep / def / dictionary-id bytes (stage_seg)
 };
+constexpr uint32_t SEG_LVL_CAP = 8192, SEG_VAL_CAP = 16384;
 
 __device__ __forceinline__ void decode_page(const DevChunk* __restrict__ chunks, DevPage* pages, const int pi, DevChunkResult* res,
                             DecodeLds& S, const DecodeRange* R = nullptr) {
@@ -853,6 +911,14 @@ __device__ __forceinline__ void decode_page(const DevChunk* __restrict__ chunks,
     if (!supported) { if (tid == 0) set_status(res, pg.chunk, dict ? ST_CORRUPT : ST_ENCODING, pi); return; }
     if (dict && id_bw > 32) { if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
     if (binary && !ck.chars) return;   // capacity error already recorded by k_scan
+    if (R) {   // the segment's stream bytes in LDS: the walks below read one run header per dependent load
+        const int n3 = R->nseg;
+        const uint64_t lr = stage_seg(R->buf[0], SEG_LVL_CAP, s.rep, s.rep_n, R->st[0], R->nx ? &R->nx[0] : nullptr);
+        const uint64_t ld = ck.max_def > 0 ? stage_seg(R->buf[1], SEG_LVL_CAP, s.def, s.def_n, R->st[n3], R->nx ? &R->nx[n3] : nullptr) : 0;
+        const uint64_t lv = (dict && !binary) ? stage_seg(R->buf[2], SEG_VAL_CAP, s.val, s.val_n, R->st[2 * n3], R->nx ? &R->nx[2 * n3] : nullptr) : 0;
+        if (tid == 0) { rle_rebase(L.srep, lr); rle_rebase(L.sdef, ld); rle_rebase(S.sval, lv); }
+        __syncthreads();
+    }
 
     // bases
     uint64_t slot_base = counted ? uint64_t(pg.slot_start) : uint64_t(pg.entry_start);
@@ -2616,35 +2682,6 @@ struct NullLds {
     uint32_t scan_tmp[NTN / 64];
 };
 
-// Stage bytes [b0, b1) of stream p[0, n) into LDS words st: byte b0 + i of the stream is byte
-// off + i of st (off = the 16-byte misalignment of p + b0); stream bytes at or past n read as zero
-// (parquet-mr zero-pads a truncated bit-packed run), as do the 16 bytes after the range.
-__device__ __forceinline__ uint32_t stage_bytes(uint32_t* st, const uint8_t* p, uint64_t n, uint32_t b0, uint32_t b1) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p) + b0;
-    const uint32_t off = uint32_t(a & 15u);
-    if (b1 <= b0) return off;
-    const uint32_t nchunk = (off + (b1 - b0) + 15u) / 16u;
-    const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(a - off);
-    const int64_t base = int64_t(b0) - int64_t(off);   // stream offset of st byte 0
-    for (uint32_t c = threadIdx.x; c <= nchunk; c += blockDim.x) {
-        u32x4 v = {0u, 0u, 0u, 0u};
-        const int64_t cb = base + 16 * int64_t(c);   // stream offset of the chunk
-        if (c < nchunk && cb < int64_t(n)) {
-            v = src[c];
-            if (cb + 16 > int64_t(n)) {
-                #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int64_t keep = int64_t(n) - (cb + 4 * q);   // valid bytes of word q
-                    const uint32_t mask = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
-                    v[q] &= mask;
-                }
-            }
-        }
-        reinterpret_cast<u32x4*>(st)[c] = v;
-    }
-    return off;
-}
-
 __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ chunks, DevPage* pages,
                                                    const int2* __restrict__ blocks, DevChunkResult* res) {
     __shared__ __attribute__((aligned(16))) NullLds S;
@@ -2934,27 +2971,201 @@ __device__ __forceinline__ bool nest_sections(const DevPage& pg, const DevChunk&
     return pg.seg != nullptr && ck.max_rep > 0 && page_sections(pg, ck, s) && s.rep_rle && (ck.max_def == 0 || s.def_rle);
 }
 
-__global__ __launch_bounds__(64) void k_nest_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
-                                                 DevChunkResult* res) {
-    __shared__ __attribute__((aligned(16))) uint32_t st[(NW_BYTES + 64) / 4];
-    const int pi = list[blockIdx.x];
+// One hybrid-stream run header at stream position p (q = its bytes, >= 14 readable): false when p
+// holds no run the serial walk (rle_walk) would accept.
+struct HybRun {
+    uint64_t cnt, next, bit0;
+    uint32_t val, packed;
+};
+__device__ __forceinline__ bool hyb_header(const uint8_t* q, uint64_t p, uint64_t n, int bw, HybRun& r) {
+    uint64_t h = 0;
+    uint32_t hl = 0;
+    bool hok = false;
+    for (uint32_t sh = 0; sh < 70; sh += 7) {
+        if (p + hl >= n) break;
+        const uint32_t c = q[hl++];
+        h |= uint64_t(c & 0x7f) << sh;
+        if (!(c & 0x80)) { hok = true; break; }
+    }
+    if (!hok) return false;
+    const uint64_t a = p + hl;
+    r.packed = uint32_t(h & 1);
+    r.val = 0;
+    r.bit0 = 0;
+    if (r.packed) {
+        const uint64_t groups = h >> 1;
+        r.cnt = groups * 8;
+        r.bit0 = a * 8;
+        const uint64_t nb = groups * uint64_t(bw), avail = n - a;
+        r.next = a + (nb < avail ? nb : avail);
+    } else {
+        const int nbv = (bw + 7) >> 3;
+        r.cnt = h >> 1;
+        if (a + nbv > n) return false;
+        for (int b = 0; b < nbv; b++) r.val |= uint32_t(q[hl + b]) << (8 * b);
+        r.next = a + nbv;
+    }
+    return true;
+}
+__device__ __forceinline__ RleState hyb_state(const HybRun& r, uint64_t e_start, uint64_t t, int bw) {
+    RleState x;
+    x.pos = r.next;
+    x.run_left = e_start + r.cnt - t;
+    x.run_bit = r.packed ? r.bit0 + (t - e_start) * uint64_t(bw) : 0;
+    x.run_val = r.val;
+    x.run_packed = int32_t(r.packed);
+    x.err = 0;
+    return x;
+}
+
+// k_nest_lvl: NL_NT threads per NEST_WIN-byte window of a page's rep or def stream. Run headers can
+// only be found by walking from the stream's start, so every byte position of the window is decoded
+// as a header at once, and pointer jumping (log2(NEST_WIN) rounds in LDS) gives, for every position,
+// where the chain from it leaves the window and the entries it covers on the way (north_star K2: run
+// boundaries by parallel scans). The true chain's entry position and count then come from the
+// previous window (single-pass hand-over through npub: one lookup per window on the critical path),
+// and the window walks its part of the true chain to store the checkpoints inside it (states at
+// multiples of seg_len entries) after publishing its exit.
+constexpr int NL_NT = 256;
+constexpr uint32_t NL_END = 0xFFFFFFu;        // exit field: the chain ends inside the window (no run at its last position)
+constexpr uint32_t NL_FAR = 0xFFFFFEu;        // exit field: leaves the window for a position >= w0 + NL_FAR (exact exit by a walk)
+constexpr uint64_t NL_CMAX = (1ull << 40) - 1;   // count field saturates (the exact count is then walked)
+__global__ __launch_bounds__(NL_NT) void k_nest_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
+                                                    DevChunkResult* res) {
+    __shared__ __attribute__((aligned(16))) uint32_t st[(NEST_WIN + 64) / 4];
+    __shared__ uint64_t X[NEST_WIN];   // per position: entries to the exit << 24 | exit (window-relative, NL_END, NL_FAR)
+    __shared__ uint64_t J[NEST_WIN];   // the same after 5 rounds: jumps over >= 32 runs (or to the exit), for the checkpoint walk
+    __shared__ uint64_t s_hand[3];
+    const int tid = threadIdx.x;
+    const int pi = list[blockIdx.z];
+    const int which = blockIdx.y;   // 0 = rep, 1 = def
+    const uint32_t w = blockIdx.x;
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     Sections s;
-    if (res[pg.chunk].status != 0 || !nest_sections(pg, ck, s)) return;   // (seg_ok stays 0: k_count / k_decode)
-    const int which = blockIdx.y;   // 0 = rep, 1 = def
+    if (res[pg.chunk].status != 0 || !nest_sections(pg, ck, s) || w >= uint32_t(pg.nwin)) return;   // (seg_ok stays 0)
     const int nseg = pg.nseg;
-    const uint32_t sl = uint32_t(pg.seg_len);
+    const uint64_t sl = uint64_t(uint32_t(pg.seg_len));
     RleState* out = nest_ck(pg, which);
+    if (which == 0 && w == 0 && tid == 0) pg.seg_ok = 1;
     if (which == 1 && ck.max_def == 0) {
-        for (int k = threadIdx.x; k < nseg; k += 64) { RleState r; rle_init(r); out[k] = r; }
-    } else {
-        const uint8_t* p = which == 0 ? s.rep : s.def;
-        const uint64_t n = which == 0 ? s.rep_n : s.def_n;
-        nest_walk(st, p, n, bit_width(uint32_t(which == 0 ? ck.max_rep : ck.max_def)), 0, nseg,
-                  [sl](int k) { return uint64_t(k) * sl; }, out);
+        if (w == 0) for (int k = tid; k < nseg; k += NL_NT) { RleState r; rle_init(r); out[k] = r; }
+        return;
     }
-    if (which == 0 && threadIdx.x == 0) pg.seg_ok = 1;
+    const uint8_t* p = which == 0 ? s.rep : s.def;
+    const uint64_t n = which == 0 ? s.rep_n : s.def_n;
+    const int bw = bit_width(uint32_t(which == 0 ? ck.max_rep : ck.max_def));
+    const uint64_t w0 = uint64_t(w) * NEST_WIN, w1 = w0 + NEST_WIN;
+    if (w0 >= n && w > 0) return;                  // past the stream (no one waits on it)
+    const bool last = w1 >= n;                     // writes the sentinels of targets the chain never reached
+    WinPub* pub = pg.npub + size_t(which) * size_t(pg.nwin);
+    // ---- stage the window (+ 16 bytes: a header and an RLE value that start inside it) ----
+    const uint32_t woff = stage_bytes(st, p, n, uint32_t(min<uint64_t>(w0, n)), uint32_t(min<uint64_t>(w1 + 16, n)));
+    __syncthreads();
+    const uint8_t* W = reinterpret_cast<const uint8_t*>(st) + woff;   // W[i] = stream byte w0 + i
+    // ---- every position as a header, then pointer jumping to the window's exit ----
+    for (uint32_t i = tid; i < NEST_WIN; i += NL_NT) {
+        const uint64_t pp = w0 + i;
+        HybRun r;
+        uint64_t x = NL_END;
+        if (pp < n && hyb_header(W + i, pp, n, bw, r)) {
+            const uint64_t rel = r.next - w0;
+            x = (min<uint64_t>(r.cnt, NL_CMAX) << 24) | (rel < NL_FAR ? rel : uint64_t(NL_FAR));
+        }
+        X[i] = x;
+    }
+    __syncthreads();
+    for (uint32_t span = 1; span < NEST_WIN; span <<= 1) {
+        for (uint32_t i = tid; i < NEST_WIN; i += NL_NT) {
+            const uint64_t x = X[i];
+            const uint32_t e = uint32_t(x & 0xFFFFFFu);
+            if (e < NEST_WIN) {   // (in place: a successor already advanced this round only jumps further)
+                const uint64_t y = X[e];
+                const uint64_t c = min<uint64_t>((x >> 24) + (y >> 24), NL_CMAX);
+                X[i] = (c << 24) | (y & 0xFFFFFFu);
+            }
+        }
+        __syncthreads();
+        if (span == 16) {
+            for (uint32_t i = tid; i < NEST_WIN; i += NL_NT) J[i] = X[i];
+        }
+    }
+    __syncthreads();
+    // ---- the true chain's entry from the previous window; exit to the next ----
+    if (tid == 0) {
+        uint64_t tp = 0, te = 0;
+        uint32_t tst = 0;
+        bool ok = true;
+        if (w > 0) {
+            const WinPub& pv = pub[w - 1];
+            uint32_t spins = 0;   // (bounded: a hand-over that never comes fails the chunk instead of hanging)
+            while (__hip_atomic_load(&pv.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 && ++spins < (1u << 22))
+                __builtin_amdgcn_s_sleep(2);
+            ok = spins < (1u << 22);
+            tp = __hip_atomic_load(&pv.p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            te = __hip_atomic_load(&pv.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tst = __hip_atomic_load(&pv.st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_hand[0] = tp; s_hand[1] = te; s_hand[2] = uint64_t(tst) | (ok ? 0u : 2u);
+        uint64_t xp = tp, xe = te;
+        uint32_t xst = tst;
+        if (ok && tst == 0 && tp < w1) {
+            const uint64_t x = X[tp - w0];
+            const uint32_t e = uint32_t(x & 0xFFFFFFu);
+            const uint64_t c = x >> 24;
+            if (e == NL_FAR || c == NL_CMAX) {   // exact exit / count by walking (a run of > 16 MB, or counts near 2^40)
+                while (xp < w1) {
+                    HybRun r;
+                    if (xp >= n || !hyb_header(W + (xp - w0), xp, n, bw, r)) { xst = 1; break; }
+                    xe += r.cnt;
+                    xp = r.next;
+                }
+            } else {
+                xe = te + c;
+                if (e == NL_END) { xst = 1; xp = w1; }   // (where it ended does not matter once it has)
+                else xp = w0 + e;
+            }
+        }
+        WinPub& me = pub[w];
+        if (!ok) set_status(res, pg.chunk, ST_CORRUPT, pi);
+        __hip_atomic_store(&me.p, xp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&me.e, xe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&me.st, xst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&me.flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (s_hand[2] & 2u) return;
+    // ---- checkpoints inside the window: one wave walks its part of the true chain ----
+    uint64_t tp = s_hand[0], te = s_hand[1];
+    uint32_t tst = uint32_t(s_hand[2]);
+    if (tid < 64) {   // (all 64 lanes walk in step; lane 0 stores)
+        uint64_t k = (te + sl - 1) / sl;   // first target >= te
+        if (tst == 0) {
+            while (k < uint64_t(nseg) && tp < w1) {
+                const uint64_t t = k * sl;
+                // jump over runs before the target: >= 32 at a time
+                while (true) {
+                    const uint64_t x = J[tp - w0];
+                    const uint32_t e = uint32_t(x & 0xFFFFFFu);
+                    if (e >= NEST_WIN || te + (x >> 24) > t) break;
+                    te += x >> 24;
+                    tp = w0 + e;
+                }
+                HybRun r;
+                if (tp >= n || !hyb_header(W + (tp - w0), tp, n, bw, r)) { tst = 1; break; }
+                if (t < te + r.cnt) {   // the target's run
+                    if (tid == 0) out[k] = hyb_state(r, te, t, bw);
+                    k++;
+                    continue;
+                }
+                te += r.cnt;
+                tp = r.next;
+            }
+        }
+        // targets the chain never reached: the stream's last window, or the window where it ended
+        if (last || tst == 1)
+            for (uint64_t q = k + tid; q < uint64_t(nseg); q += 64) out[q] = rle_sentinel();
+    }
 }
 
 __global__ __launch_bounds__(NT) void k_count_seg(const DevChunk* __restrict__ chunks, DevPage* pages,
@@ -2965,11 +3176,22 @@ __global__ __launch_bounds__(NT) void k_count_seg(const DevChunk* __restrict__ c
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     if (pg.seg_ok != 1 || res[pg.chunk].status != 0) return;
+    __shared__ uint32_t bufR[SEG_LVL_CAP / 4], bufD[SEG_LVL_CAP / 4];
     Sections s;
     page_sections(pg, ck, s);   // (parsed by k_nest_lvl)
     const uint64_t e_b = uint64_t(sg) * uint32_t(pg.seg_len);
     const uint64_t e_e = min<uint64_t>(uint64_t(pg.num_values), e_b + uint32_t(pg.seg_len));
-    if (threadIdx.x == 0) { L.srep = nest_ck(pg, 0)[sg]; L.sdef = nest_ck(pg, 1)[sg]; L.err = 0; }
+    {
+        const RleState* cr = nest_ck(pg, 0);
+        const RleState* cd = nest_ck(pg, 1);
+        const bool last = sg + 1 >= pg.nseg;
+        const uint64_t lr = stage_seg(bufR, SEG_LVL_CAP, s.rep, s.rep_n, cr[sg], last ? nullptr : &cr[sg + 1]);
+        const uint64_t ld = ck.max_def > 0 ? stage_seg(bufD, SEG_LVL_CAP, s.def, s.def_n, cd[sg], last ? nullptr : &cd[sg + 1]) : 0;
+        if (threadIdx.x == 0) {
+            L.srep = cr[sg]; L.sdef = cd[sg]; L.err = 0;
+            rle_rebase(L.srep, lr); rle_rebase(L.sdef, ld);
+        }
+    }
     __syncthreads();
     uint64_t slots = 0, vals = 0, rows = 0;
     for (uint64_t e0 = e_b; e0 < e_e; e0 += TILE) {
@@ -3055,7 +3277,10 @@ __global__ __launch_bounds__(NT) void k_nest_ids(const DevChunk* __restrict__ ch
     SegRec& rec = nest_rec(pg)[sg];
     const uint64_t v_b = rec.vb, v_e = v_b + rec.nv;
     const int id_bw = s.val_n > 0 ? int(s.val[0]) : 0;
-    if (threadIdx.x == 0) { sval = nest_ck(pg, 2)[sg]; verr = 0; chars_acc = 0; }
+    __shared__ uint32_t bufV[SEG_VAL_CAP / 4];
+    const RleState* cv = nest_ck(pg, 2);
+    const uint64_t lv = v_e > v_b ? stage_seg(bufV, SEG_VAL_CAP, s.val, s.val_n, cv[sg], sg + 1 < pg.nseg ? &cv[sg + 1] : nullptr) : 0;
+    if (threadIdx.x == 0) { sval = cv[sg]; rle_rebase(sval, lv); verr = 0; chars_acc = 0; }
     __syncthreads();
     for (uint64_t v0 = v_b; v0 < v_e; v0 += TILE) {
         const uint32_t t = uint32_t(min<uint64_t>(TILE, v_e - v0));
@@ -3114,6 +3339,7 @@ __global__ __launch_bounds__(64) void k_nest_chars(const DevChunk* __restrict__ 
 __global__ __launch_bounds__(NT) void k_decode_seg(const DevChunk* __restrict__ chunks, DevPage* pages,
                                                    const int2* __restrict__ list, DevChunkResult* res) {
     __shared__ DecodeLds S;
+    __shared__ uint32_t bufR[SEG_LVL_CAP / 4], bufD[SEG_LVL_CAP / 4], bufV[SEG_VAL_CAP / 4];
     const int pi = list[blockIdx.x].x, sg = list[blockIdx.x].y;
     const DevPage& pg = pages[pi];
     if (pg.seg_ok != 1) return;
@@ -3124,14 +3350,18 @@ __global__ __launch_bounds__(NT) void k_decode_seg(const DevChunk* __restrict__ 
     R.slot_base = rec.sb; R.row_base = rec.rb; R.vidx = rec.vb;
     R.char_base = chunks[pg.chunk].ptype == 6 ? rec.cb : 0;
     R.st = nest_ck(pg, 0) + sg;
+    R.nx = sg + 1 < pg.nseg ? R.st + 1 : nullptr;
     R.nseg = pg.nseg;
+    R.buf[0] = bufR; R.buf[1] = bufD; R.buf[2] = bufV;
     decode_page(chunks, pages, pi, res, S, &R);
 }
 
 // ---- launchers -------------------------------------------------------------------------------
-void launch_nest_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
+void launch_nest_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int max_nwin, DevChunkResult* d_res,
                      hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_nest_lvl, dim3(n, 2), dim3(64), 0, st, d_chunks, d_pages, d_list, d_res);
+    // windows in blockIdx.x: a window waits on the one before it, which the dispatcher starts first
+    if (n > 0 && max_nwin > 0)
+        hipLaunchKernelGGL(k_nest_lvl, dim3(max_nwin, 2, n), dim3(NL_NT), 0, st, d_chunks, d_pages, d_list, d_res);
 }
 void launch_nest_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, const int2* d_segs, int n_segs,
                        DevChunkResult* d_res, hipStream_t st) {

@@ -40,7 +40,7 @@ void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hi
 void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
-void launch_nest_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_nest_lvl(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
 void launch_nest_count(const DevChunk*, DevPage*, const int*, int, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_nest_decode(const DevChunk*, DevPage*, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_page_scan(const ScanChunk*, int, pf_page_desc*, ScanCrc*, ScanResult*, hipStream_t);
@@ -151,6 +151,8 @@ struct pf_ctx {
     std::vector<pf_column_info> info;
     size_t bits_bytes = 0;
     int n_decode_first = 0;                // l_decode: pages that will need k_decode come first
+    size_t off_npub = 0, npub_bytes = 0;   // k_nest_lvl window hand-overs (scratch), zeroed before the batch
+    int max_nwin = 0;
     size_t out_bytes = 0;                  // values / offsets / levels arena extent of the last decode
     size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
     size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0, off_bajobs = 0, off_batiles = 0;
@@ -224,6 +226,8 @@ int enqueue_kernels(pf_ctx* ctx) {
     const int2* d_wins = reinterpret_cast<const int2*>(meta + ctx->off_wins);
 
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
+    if (ctx->npub_bytes)
+        HIPCHK(ctx, hipMemsetAsync(static_cast<uint8_t*>(ctx->d_scratch.p) + ctx->off_npub, 0, ctx->npub_bytes, st));
     EVREC(ctx, ctx->ev[1], st);
     // single-literal pages in place, PLAIN fixed-width pages straight into the column (pf_pages.hip)
     launch_snappy_head(d_jobs, int(ctx->jobs.size()), d_pages, d_chunks, d_fallback, d_res, st);
@@ -253,7 +257,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st);
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
     EVREC(ctx, ctx->ev[5], st);
-    launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, d_res, st);
+    launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, ctx->max_nwin, d_res, st);
     launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st);
     launch_nest_count(d_chunks, d_pages, d_nest, n_nest, d_nseg, n_nseg, d_res, st);
     launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
@@ -918,9 +922,11 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->d_bytes = d_bytes;
 
     // ---- plan: sizes of scratch / outputs ----
-    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; uint64_t lt_off; uint64_t seg_off; int32_t nseg, seg_len; };
+    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; uint64_t lt_off; uint64_t seg_off; int32_t nseg, seg_len, nwin; uint64_t pub_off; };
     std::vector<PagePlan> pplan;
     size_t scratch = 0, out = 0, bits = 0;
+    uint64_t nest_pub = 0;
+    ctx->max_nwin = 0;
     uint64_t chars_hint = 0;
     struct OutPlan { size_t values, validity, offsets, list_offsets, list_validity, def, rep; };
     std::vector<OutPlan> oplan(n_chunks);
@@ -966,7 +972,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     hs = PF_ERR_CORRUPT_PAGE; break;
                 }
                 bool compressed = cd.codec == PF_CODEC_SNAPPY && (!v2 || pd.is_compressed);
-                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull, ~0ull, ~0ull, 0, 0};
+                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull, ~0ull, ~0ull, 0, 0, 0, 0};
                 if (v2) { pg.lvl = src; pg.rep_len = uint32_t(pd.rep_bytes); pg.def_len = uint32_t(pd.def_bytes); }
                 if (compressed) {
                     pp.scratch_off = take(scratch, pd.uncompressed_size - lvl, 16);
@@ -1022,6 +1028,9 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                                 pp.seg_len = int32_t(sl);
                                 pp.nseg = int32_t(ns);
                                 pp.seg_off = take(scratch, nest_seg_bytes(pp.nseg), 256);
+                                pp.nwin = int32_t((uint64_t(std::max(pd.uncompressed_size, pd.compressed_size)) + NEST_WIN - 1) / NEST_WIN + 1);
+                                pp.pub_off = nest_pub;   // (the window hand-overs of all pages: one block, zeroed per batch)
+                                nest_pub += 2ull * uint64_t(pp.nwin) * sizeof(WinPub);
                             }
                         }
                     }
@@ -1085,6 +1094,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     if (ctx->copies_pending && (out > ctx->d_out.cap || bits > ctx->d_bits.cap || chars_cap > ctx->d_chars.cap))
         HIPCHK(ctx, hipStreamSynchronize(st));   // a growing output arena must not be freed under a pending D2H copy
     ctx->copies_pending = false;
+    ctx->npub_bytes = size_t(nest_pub);
+    ctx->off_npub = take(scratch, ctx->npub_bytes, 256);
     HIPCHK(ctx, ctx->d_scratch.ensure(std::max<size_t>(scratch, 1)));
     HIPCHK(ctx, ctx->d_out.ensure(std::max<size_t>(out, 1)));
     HIPCHK(ctx, ctx->d_bits.ensure(std::max<size_t>(bits, 1)));
@@ -1121,6 +1132,9 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                 pg.seg = S + pp.seg_off;
                 pg.nseg = pp.nseg;
                 pg.seg_len = pp.seg_len;
+                pg.nwin = pp.nwin;
+                pg.npub = reinterpret_cast<WinPub*>(S + ctx->off_npub + pp.pub_off);
+                ctx->max_nwin = std::max(ctx->max_nwin, pp.nwin);
                 ctx->l_nest.push_back(int(i));
                 for (int k = 0; k < pp.nseg; k++) { ctx->l_nseg.push_back(int(i)); ctx->l_nseg.push_back(k); }
             }
