@@ -117,16 +117,19 @@ __device__ __forceinline__ uint32_t bitpacked_be(const uint8_t* p, uint64_t n, u
 }
 
 // Decode the levels of entries [e0, e0 + want) into L.rep / L.def; returns count (== want) or
-// sets L.err. Must be called by all threads.
+// sets L.err. Must be called by all threads (blockDim.x >= 128).
 __device__ inline uint32_t decode_level_tile(LevelLds& L, const Sections& s, const DevChunk& ck,
                                              uint64_t e0, uint32_t want) {
     const int bwr = bit_width(ck.max_rep), bwd = bit_width(ck.max_def);
+    // the two walks run concurrently on lanes of different waves
     if (threadIdx.x == 0) {
-        L.nprep = L.npdef = 0;
+        L.nprep = 0;
         if (ck.max_rep > 0 && s.rep_rle) {
             uint32_t got = rle_walk(L.srep, s.rep, s.rep_n, bwr, want, L.prep, TILE, L.nprep);
             if (got != want || L.srep.err) L.err = 1;
         }
+    } else if (threadIdx.x == 64) {
+        L.npdef = 0;
         if (ck.max_def > 0 && s.def_rle) {
             uint32_t got = rle_walk(L.sdef, s.def, s.def_n, bwd, want, L.pdef, TILE, L.npdef);
             if (got != want || L.sdef.err) L.err = 1;
