@@ -182,6 +182,271 @@ __device__ bool dbp_decode_wg(DbpLds& S, const uint8_t* p, uint64_t n, bool is64
     return ok;
 }
 
+// ---- block-parallel DELTA_BINARY_PACKED (large INT32 / INT64 pages) -----------------------------
+// k_delta walks block headers on one lane (one dependent header read per block: ~250 us for a
+// 494 K-value page). Blocks hold `block` values each (the last one fewer), so block b's first value
+// is 1 + b * block: only the blocks' byte positions form a chain. k_dbp_pos finds them the way
+// k_nest_lvl finds level runs (pf_pages.hip): per DBP_WIN-byte window every position is decoded as
+// a block header (next = position + header + sum of the miniblocks' bytes), pointer jumping gives
+// each position's window exit, windows hand over the true chain's entry in one pass, then walk their
+// part of it storing the positions. k_dbp_blk (one wave per block) sums each block's deltas,
+// k_dbp_scan turns the sums into block bases, k_dbp_blk (again) writes the values. Any check the
+// one-lane walk would fail (header, widths and data of the miniblocks consumed) sets dbp_ok = 2 and
+// k_delta, launched last, decodes the page from scratch (and reports it).
+constexpr int DP_NT = 256;
+constexpr uint32_t DP_END = 0xFFFFFFu;
+constexpr uint32_t DP_FAR = 0xFFFFFEu;
+constexpr uint32_t DP_MAXMINI = 16;   // pages with more miniblocks per block stay on k_delta
+
+struct DbpHdr {
+    uint64_t block, nmini, total, first, pos0, vpm, nblocks;
+    bool ok;
+};
+// The page header, checked as dbp_decode_wg checks it (strict: total <= cap).
+__device__ __forceinline__ DbpHdr dbp_header(const uint8_t* p, uint64_t n, bool is64, uint64_t cap) {
+    DbpHdr h{};
+    uint64_t pos = 0, zz;
+    h.ok = uvarint(p, n, pos, h.block) && uvarint(p, n, pos, h.nmini) && uvarint(p, n, pos, h.total) &&
+           uvarint(p, n, pos, zz) && h.nmini > 0 && h.block > 0 && h.block % h.nmini == 0 && h.nmini <= DP_MAXMINI &&
+           h.nmini <= h.block && (h.block / h.nmini) % 8 == 0 && h.total <= cap;
+    if (!h.ok) return h;
+    h.first = uint64_t(unzigzag(zz));
+    if (!is64) h.first = uint64_t(uint32_t(h.first));
+    h.pos0 = pos;
+    h.vpm = h.block / h.nmini;
+    h.nblocks = h.total > 1 ? (h.total - 1 + h.block - 1) / h.block : 0;
+    return h;
+}
+// block header at stream position q (bytes b = the stream from q, >= 10 + nmini readable): the
+// position after its miniblocks (all nmini of them), or false when no header fits there
+__device__ __forceinline__ bool dbp_next(const uint8_t* b, uint64_t q, uint64_t n, uint64_t nmini, uint64_t vpm, uint64_t& next) {
+    uint32_t hl = 0;
+    bool ok = false;
+    for (uint32_t sh = 0; sh < 70; sh += 7) {
+        if (q + hl >= n) break;
+        const uint32_t c = b[hl++];
+        if (!(c & 0x80)) { ok = true; break; }
+    }
+    if (!ok || q + hl + nmini > n) return false;
+    uint64_t bits = 0;
+    for (uint32_t m = 0; m < nmini; m++) bits += b[hl + m];
+    next = q + hl + nmini + bits * vpm / 8;
+    return true;
+}
+__device__ __forceinline__ void dbp_fail(DevPage& pg) {
+    __hip_atomic_store(&pg.dbp_ok, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(DP_NT) void k_dbp_pos(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list) {
+    __shared__ __attribute__((aligned(16))) uint32_t st[(DBP_WIN + 64 + 32) / 4];
+    __shared__ uint64_t X[DBP_WIN];
+    __shared__ uint64_t s_hand[3];
+    const int tid = threadIdx.x;
+    DevPage& pg = pages[list[blockIdx.z]];
+    const DevChunk& ck = chunks[pg.chunk];
+    const uint32_t w = blockIdx.x;
+    if (!pg.dbp || w >= uint32_t(pg.dbp_nwin)) return;
+    const uint8_t* p;
+    uint64_t n;
+    if (!values_section(pg, ck, p, n)) { if (w == 0 && tid == 0) dbp_fail(pg); return; }
+    const DbpHdr H = dbp_header(p, n, ck.ptype == 2, uint64_t(pg.aux_cap));
+    if (!H.ok || H.nblocks == 0 || H.nblocks > pg.dbp_bcap) { if (w == 0 && tid == 0) dbp_fail(pg); return; }
+    if (w == 0 && tid == 0) __hip_atomic_fetch_max(&pg.dbp_ok, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t* bpos = reinterpret_cast<uint32_t*>(pg.dbp);
+    const uint64_t w0 = H.pos0 + uint64_t(w) * DBP_WIN, w1 = w0 + DBP_WIN;
+    if (w0 >= n && w > 0) return;
+    const bool last = w1 >= n;
+    WinPub* pub = pg.dbp_pub;
+    const uint32_t look = 10 + uint32_t(H.nmini) + 8;
+    const uint32_t woff = stage_bytes(st, p, n, uint32_t(min<uint64_t>(w0, n)), uint32_t(min<uint64_t>(w1 + look, n)));
+    __syncthreads();
+    const uint8_t* W = reinterpret_cast<const uint8_t*>(st) + woff;
+    for (uint32_t i = tid; i < DBP_WIN; i += DP_NT) {
+        const uint64_t q = w0 + i;
+        uint64_t nx, x = DP_END;
+        if (q < n && dbp_next(W + i, q, n, H.nmini, H.vpm, nx)) {
+            const uint64_t rel = nx - w0;
+            x = (1ull << 24) | (rel < DP_FAR ? rel : uint64_t(DP_FAR));
+        }
+        X[i] = x;
+    }
+    __syncthreads();
+    for (uint32_t span = 1; span < DBP_WIN; span <<= 1) {
+        for (uint32_t i = tid; i < DBP_WIN; i += DP_NT) {
+            const uint64_t x = X[i];
+            const uint32_t e = uint32_t(x & 0xFFFFFFu);
+            if (e < DBP_WIN) {
+                const uint64_t y = X[e];
+                X[i] = (((x >> 24) + (y >> 24)) << 24) | (y & 0xFFFFFFu);
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        uint64_t tp = H.pos0, tb = 0;
+        uint32_t tst = 0;
+        bool ok = true;
+        if (w > 0) {
+            const WinPub& pv = pub[w - 1];
+            uint32_t spins = 0;
+            while (__hip_atomic_load(&pv.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 && ++spins < (1u << 22))
+                __builtin_amdgcn_s_sleep(2);
+            ok = spins < (1u << 22);
+            tp = __hip_atomic_load(&pv.p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tb = __hip_atomic_load(&pv.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tst = __hip_atomic_load(&pv.st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_hand[0] = tp; s_hand[1] = tb; s_hand[2] = uint64_t(tst) | (ok ? 0u : 2u);
+        uint64_t xp = tp, xb = tb;
+        uint32_t xst = tst;
+        if (ok && tst == 0 && tb < H.nblocks && tp < w1) {
+            const uint64_t x = X[tp - w0];
+            const uint32_t e = uint32_t(x & 0xFFFFFFu);
+            if (e == DP_FAR) {   // a block of > 16 MB: walk to the exit
+                while (xp < w1) {
+                    uint64_t nx;
+                    if (xp >= n || !dbp_next(W + (xp - w0), xp, n, H.nmini, H.vpm, nx)) { xst = 1; break; }
+                    xb++;
+                    xp = nx;
+                }
+            } else {
+                xb = tb + (x >> 24);
+                if (e == DP_END) { xst = 1; xp = w1; }
+                else xp = w0 + e;
+            }
+        }
+        if (!ok) dbp_fail(pg);
+        WinPub& me = pub[w];
+        __hip_atomic_store(&me.p, xp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&me.e, xb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&me.st, xst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&me.flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (s_hand[2] & 2u) return;
+    if (tid < 64) {   // the window's blocks of the true chain (all 64 lanes walk in step)
+        uint64_t tp = s_hand[0], tb = s_hand[1];
+        uint32_t tst = uint32_t(s_hand[2]);
+        if (tst == 0) {
+            while (tb < H.nblocks && tp < w1) {
+                uint64_t nx;
+                if (tp >= n || !dbp_next(W + (tp - w0), tp, n, H.nmini, H.vpm, nx)) { tst = 1; break; }
+                if (tid == 0) bpos[tb] = uint32_t(tp);
+                tb++;
+                tp = nx;
+            }
+        }
+        // the chain ended before the page's last block, or the stream did
+        if (tid == 0 && tb < H.nblocks && (tst == 1 || last)) dbp_fail(pg);
+    }
+}
+
+__device__ bool dbp_block(DevPage& pg, const uint8_t* p, uint64_t n, const DbpHdr& H, bool is64, uint64_t b, int lane, int mode);
+// mode 0: each block's delta sum -> sum[b]; mode 1: values from the block bases (k_dbp_scan) -> aux.
+// One wave per block (grid-stride), 64 values at a time.
+__global__ __launch_bounds__(DP_NT) void k_dbp_blk(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
+                                                   int mode) {
+    DevPage& pg = pages[list[blockIdx.y]];
+    const DevChunk& ck = chunks[pg.chunk];
+    if (!pg.dbp || __hip_atomic_load(&pg.dbp_ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1) return;
+    const uint8_t* p;
+    uint64_t n;
+    values_section(pg, ck, p, n);
+    const bool is64 = ck.ptype == 2;
+    const DbpHdr H = dbp_header(p, n, is64, uint64_t(pg.aux_cap));
+    const int lane = threadIdx.x & 63;
+    for (uint64_t b = uint64_t(blockIdx.x) * (DP_NT / 64) + (threadIdx.x >> 6); b < H.nblocks;
+         b += uint64_t(gridDim.x) * (DP_NT / 64))
+        if (!dbp_block(pg, p, n, H, is64, b, lane, mode)) return;
+}
+
+// one block, one wave (k_dbp_blk); false after a failed check
+__device__ bool dbp_block(DevPage& pg, const uint8_t* p, uint64_t n, const DbpHdr& H, bool is64, uint64_t b, int lane, int mode) {
+    const uint32_t* bpos = reinterpret_cast<const uint32_t*>(pg.dbp);
+    uint64_t* bsum = reinterpret_cast<uint64_t*>(pg.dbp + 4ull * pg.dbp_bcap + 8 - ((4ull * pg.dbp_bcap) & 7));
+    uint64_t pos = bpos[b], md;
+    if (!uvarint(p, n, pos, md)) { if (lane == 0) dbp_fail(pg); return false; }
+    int64_t mind = unzigzag(md);
+    if (!is64) mind = int32_t(mind);
+    const uint64_t wpos = pos, dpos = pos + H.nmini;   // widths, then miniblock data
+    const uint64_t v0 = 1 + b * H.block, v1 = min<uint64_t>(H.total, v0 + H.block);
+    const uint32_t maxw = is64 ? 64u : 32u;
+    // miniblocks consumed: ceil((v1 - v0) / vpm); their widths and data must be in the stream
+    const uint64_t nm = (v1 - v0 + H.vpm - 1) / H.vpm;
+    if (wpos + H.nmini > n) { if (lane == 0) dbp_fail(pg); return false; }
+    // lane m < nmini: miniblock m's width and bit offset (exclusive prefix over the lanes)
+    const uint32_t wl = uint64_t(lane) < H.nmini ? uint32_t(p[wpos + lane]) : 0u;
+    uint64_t ol = uint64_t(wl) * H.vpm;
+    #pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+        const uint64_t y = __shfl_up(ol, sh, 64);
+        if (lane >= sh) ol += y;
+    }
+    ol = dpos * 8 + ol - uint64_t(wl) * H.vpm;   // bit offset of miniblock `lane`
+    const bool bad = uint64_t(lane) < nm && (wl > maxw || (ol + uint64_t(wl) * H.vpm + 7) / 8 > n);
+    if (__any(bad)) { if (lane == 0) dbp_fail(pg); return false; }
+    uint64_t carry = mode == 1 ? bsum[b] : 0, acc = 0;
+    uint64_t* out = reinterpret_cast<uint64_t*>(pg.aux);
+    for (uint64_t c0 = v0; c0 < v1; c0 += 64) {
+        const uint64_t i = c0 + lane;
+        const uint64_t j = min<uint64_t>(i, v1 - 1) - v0, q = j % H.vpm;
+        const int m = int(j / H.vpm);   // (shuffles with every lane active)
+        const uint32_t wm = uint32_t(__shfl(int(wl), m, 64));
+        const uint64_t om = __shfl(ol, m, 64);
+        uint64_t d = 0;
+        if (i < v1) d = uint64_t(mind) + bits_le64(p, n, om + q * wm, int(wm));
+        uint64_t x = d;
+        #pragma unroll
+        for (int sh = 1; sh < 64; sh <<= 1) {
+            const uint64_t y = __shfl_up(x, sh, 64);
+            if (lane >= sh) x += y;
+        }
+        if (mode == 1 && i < v1) {
+            uint64_t v = carry + x;
+            if (!is64) v = uint64_t(uint32_t(v));
+            out[i] = v;
+        }
+        const uint64_t tot = __shfl(x, 63, 64);
+        carry += tot;
+        acc += tot;
+    }
+    if (mode == 0 && lane == 0) bsum[b] = acc;
+    return true;
+}
+
+// one workgroup per page: exclusive prefix of the block sums from the first value -> block bases
+__global__ __launch_bounds__(DP_NT) void k_dbp_scan(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list) {
+    __shared__ uint64_t wsum[DP_NT / 64];
+    DevPage& pg = pages[list[blockIdx.x]];
+    const DevChunk& ck = chunks[pg.chunk];
+    if (!pg.dbp || __hip_atomic_load(&pg.dbp_ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1) return;
+    const uint8_t* p;
+    uint64_t n;
+    values_section(pg, ck, p, n);
+    const DbpHdr H = dbp_header(p, n, ck.ptype == 2, uint64_t(pg.aux_cap));
+    uint64_t* bsum = reinterpret_cast<uint64_t*>(pg.dbp + 4ull * pg.dbp_bcap + 8 - ((4ull * pg.dbp_bcap) & 7));
+    if (threadIdx.x == 0 && H.total > 0) reinterpret_cast<uint64_t*>(pg.aux)[0] = H.first;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t carry = H.first;
+    for (uint64_t b0 = 0; b0 < H.nblocks; b0 += DP_NT) {
+        const uint64_t b = b0 + threadIdx.x;
+        const uint64_t s = b < H.nblocks ? bsum[b] : 0;
+        uint64_t x = s;
+        #pragma unroll
+        for (int sh = 1; sh < 64; sh <<= 1) {
+            const uint64_t y = __shfl_up(x, sh, 64);
+            if (lane >= sh) x += y;
+        }
+        if (lane == 63) wsum[wid] = x;
+        __syncthreads();
+        uint64_t base = carry, all = 0;
+        for (int k = 0; k < DP_NT / 64; k++) { if (k < wid) base += wsum[k]; all += wsum[k]; }
+        if (b < H.nblocks) bsum[b] = base + x - s;
+        carry += all;
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(DNT) void k_delta(const DevChunk* __restrict__ chunks, DevPage* pages, const int* page_list,
                                                DevChunkResult* res) {
     __shared__ DbpLds S;
@@ -189,6 +454,7 @@ __global__ __launch_bounds__(DNT) void k_delta(const DevChunk* __restrict__ chun
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     if (res[pg.chunk].status != 0) return;
+    if (pg.dbp && pg.dbp_ok == 1) return;   // k_dbp_* decoded it
     const uint8_t* p;
     uint64_t n, total, end;
     if (!values_section(pg, ck, p, n)) { if (threadIdx.x == 0) set_status(res, pg.chunk, ST_CORRUPT, pi); return; }
@@ -344,9 +610,18 @@ __global__ __launch_bounds__(64) void k_dba_chars(const DevChunk* __restrict__ c
     }
 }
 
-void launch_delta(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
+void launch_delta(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int max_dbp_nwin, DevChunkResult* d_res,
                   hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_delta, dim3(n), dim3(DNT), 0, st, d_chunks, d_pages, d_list, d_res);
+    if (n <= 0) return;
+    if (max_dbp_nwin > 0) {   // block-parallel pages first (k_delta then skips them, or redoes the ones that failed)
+        // block grid: DP_NT / 64 blocks per workgroup, sized for the largest table (pages with fewer exit early)
+        constexpr int dbp_grid_blocks = 64;   // workgroups per page (4 waves each, grid-stride over blocks)
+        hipLaunchKernelGGL(k_dbp_pos, dim3(max_dbp_nwin, 1, n), dim3(DP_NT), 0, st, d_chunks, d_pages, d_list);
+        hipLaunchKernelGGL(k_dbp_blk, dim3(dbp_grid_blocks, n), dim3(DP_NT), 0, st, d_chunks, d_pages, d_list, 0);
+        hipLaunchKernelGGL(k_dbp_scan, dim3(n), dim3(DP_NT), 0, st, d_chunks, d_pages, d_list);
+        hipLaunchKernelGGL(k_dbp_blk, dim3(dbp_grid_blocks, n), dim3(DP_NT), 0, st, d_chunks, d_pages, d_list, 1);
+    }
+    hipLaunchKernelGGL(k_delta, dim3(n), dim3(DNT), 0, st, d_chunks, d_pages, d_list, d_res);
 }
 void launch_dlen(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                  hipStream_t st) {

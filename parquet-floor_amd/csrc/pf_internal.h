@@ -105,6 +105,14 @@ struct DevPage {
     int32_t seg_ok;           // k_nest_lvl: 1 = the segment kernels decode the page (k_count / k_decode skip it)
     int32_t nwin;             // k_nest_lvl windows per level stream (the page's bytes / NEST_WIN, rounded up)
     struct WinPub* npub;      // [2][nwin]: what each window of the rep / def stream passes to the next (zeroed per batch)
+    // large DELTA_BINARY_PACKED INT32 / INT64 pages decoded block-parallel (k_dbp_*, pf_delta.hip), else null:
+    // {uint32_t pos[dbp_bcap] (block header positions), uint64_t sum[dbp_bcap] (block delta sums, then bases)}
+    uint8_t* dbp;
+    struct WinPub* dbp_pub;   // [dbp_nwin] window hand-overs of the block chain (zeroed per batch)
+    int32_t dbp_nwin;
+    int32_t dbp_ok;           // 1: k_dbp_* decoded the page; 0 / 2 (not taken / failed): k_delta decodes it
+    uint32_t dbp_bcap;        // blocks the tables hold
+    uint32_t dbp_pad;
 };
 
 // k_nest_lvl: a window's hand-over to the next window of its stream: the position of the first run
@@ -117,6 +125,8 @@ struct WinPub {
     uint64_t pad;
 };
 constexpr uint32_t NEST_WIN = 8192;         // k_nest_lvl window bytes
+constexpr uint32_t DBP_WIN = 8192;          // k_dbp_pos window bytes
+constexpr int32_t DBP_PAR_MIN = 16384;      // DELTA_BINARY_PACKED pages with at least this many entries go block-parallel
 
 // One segment of a nested page: its level counts (k_count_seg), their exclusive prefixes over the
 // page (k_nest_scan), the chars of its values and their prefix (k_nest_ids / k_nest_chars).

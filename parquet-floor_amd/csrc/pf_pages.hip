@@ -745,35 +745,6 @@ __global__ __launch_bounds__(64) void k_scan(DevChunk* chunks, DevPage* pages, c
     if (ck.max_rep == 1 && ck.list_offsets) ck.list_offsets[r] = int32_t(s);
 }
 
-// Stage bytes [b0, b1) of stream p[0, n) into LDS words st: byte b0 + i of the stream is byte
-// off + i of st (off = the 16-byte misalignment of p + b0); stream bytes at or past n read as zero
-// (parquet-mr zero-pads a truncated bit-packed run), as do the 16 bytes after the range.
-__device__ __forceinline__ uint32_t stage_bytes(uint32_t* st, const uint8_t* p, uint64_t n, uint32_t b0, uint32_t b1) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p) + b0;
-    const uint32_t off = uint32_t(a & 15u);
-    if (b1 <= b0) return off;
-    const uint32_t nchunk = (off + (b1 - b0) + 15u) / 16u;
-    const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(a - off);
-    const int64_t base = int64_t(b0) - int64_t(off);   // stream offset of st byte 0
-    for (uint32_t c = threadIdx.x; c <= nchunk; c += blockDim.x) {
-        u32x4 v = {0u, 0u, 0u, 0u};
-        const int64_t cb = base + 16 * int64_t(c);   // stream offset of the chunk
-        if (c < nchunk && cb < int64_t(n)) {
-            v = src[c];
-            if (cb + 16 > int64_t(n)) {
-                #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int64_t keep = int64_t(n) - (cb + 4 * q);   // valid bytes of word q
-                    const uint32_t mask = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
-                    v[q] &= mask;
-                }
-            }
-        }
-        reinterpret_cast<u32x4*>(st)[c] = v;
-    }
-    return off;
-}
-
 // Segment path (k_nest_*): the bytes of hybrid stream p[0, n) one segment reads, from the state at
 // its first entry (a) to the next segment's (b: the header after the run holding the next segment's
 // first entry; null or a sentinel = the stream's end), staged in LDS buffer buf of cap bytes. On

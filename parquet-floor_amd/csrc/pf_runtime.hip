@@ -31,7 +31,7 @@ void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*
 void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_snappy_head(SnappyJob*, int, DevPage*, const DevChunk*, int*, const DevChunkResult*, hipStream_t);
 void launch_snappy_litcopy(const SnappyJob*, const int*, int, const int*, hipStream_t);
-void launch_delta(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_delta(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
 void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_dba_chars(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, BaJob*, hipStream_t);
@@ -151,8 +151,8 @@ struct pf_ctx {
     std::vector<pf_column_info> info;
     size_t bits_bytes = 0;
     int n_decode_first = 0;                // l_decode: pages that will need k_decode come first
-    size_t off_npub = 0, npub_bytes = 0;   // k_nest_lvl window hand-overs (scratch), zeroed before the batch
-    int max_nwin = 0;
+    size_t off_npub = 0, npub_bytes = 0;   // k_nest_lvl / k_dbp_pos window hand-overs (scratch), zeroed before the batch
+    int max_nwin = 0, max_dbp_nwin = 0;
     size_t out_bytes = 0;                  // values / offsets / levels arena extent of the last decode
     size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
     size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0, off_bajobs = 0, off_batiles = 0;
@@ -252,7 +252,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     (void)d_dictbin;
     launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st);
     EVREC(ctx, ctx->ev[4], st);
-    launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), d_res, st);
+    launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), ctx->max_dbp_nwin, d_res, st);
     launch_runs(d_chunks, d_pages, d_runs, int(ctx->l_runs.size()), d_res, st);
     launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st);
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
@@ -922,11 +922,14 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->d_bytes = d_bytes;
 
     // ---- plan: sizes of scratch / outputs ----
-    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; uint64_t lt_off; uint64_t seg_off; int32_t nseg, seg_len, nwin; uint64_t pub_off; };
+    struct PagePlan { uint64_t scratch_off; uint64_t aux_off; int is_dict; uint64_t rt_off; uint64_t dx_off; uint64_t lt_off; uint64_t seg_off; int32_t nseg, seg_len, nwin; uint64_t pub_off; uint64_t dbp_off, dbp_pub_off; int32_t dbp_nwin; uint32_t dbp_bcap; };
     std::vector<PagePlan> pplan;
     size_t scratch = 0, out = 0, bits = 0;
     uint64_t nest_pub = 0;
     ctx->max_nwin = 0;
+    ctx->max_dbp_nwin = 0;
+    // PF_DBP_PAR=0: every DELTA_BINARY_PACKED page on the one-workgroup k_delta (tests)
+    const bool dbp_par = [] { const char* e = std::getenv("PF_DBP_PAR"); return !(e && e[0] == '0'); }();
     uint64_t chars_hint = 0;
     struct OutPlan { size_t values, validity, offsets, list_offsets, list_validity, def, rep; };
     std::vector<OutPlan> oplan(n_chunks);
@@ -972,7 +975,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     hs = PF_ERR_CORRUPT_PAGE; break;
                 }
                 bool compressed = cd.codec == PF_CODEC_SNAPPY && (!v2 || pd.is_compressed);
-                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull, ~0ull, ~0ull, 0, 0, 0, 0};
+                PagePlan pp{0, ~0ull, is_dict, ~0ull, ~0ull, ~0ull, ~0ull, 0, 0, 0, 0, ~0ull, 0, 0, 0};
                 if (v2) { pg.lvl = src; pg.rep_len = uint32_t(pd.rep_bytes); pg.def_len = uint32_t(pd.def_bytes); }
                 if (compressed) {
                     pp.scratch_off = take(scratch, pd.uncompressed_size - lvl, 16);
@@ -1002,8 +1005,16 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                     ck.n_pages++;
                     if (cd.physical_type == PF_BYTE_ARRAY)   // value positions / ids + per-block chars (k_flat)
                         pp.aux_off = take(scratch, 4ull * pd.num_values + 16 + 8ull * (uint64_t(pd.num_values) / FLAT_BLK + 2), 256);
-                    else if (pd.encoding == PF_ENC_DELTA_BINARY_PACKED && (cd.physical_type == PF_INT32 || cd.physical_type == PF_INT64))
+                    else if (pd.encoding == PF_ENC_DELTA_BINARY_PACKED && (cd.physical_type == PF_INT32 || cd.physical_type == PF_INT64)) {
                         pp.aux_off = take(scratch, 8ull * pd.num_values + 8, 256);
+                        if (pd.num_values >= DBP_PAR_MIN && dbp_par) {   // block-parallel decode (k_dbp_*)
+                            pp.dbp_bcap = uint32_t(pd.num_values / 8 + 2);
+                            pp.dbp_off = take(scratch, 12ull * pp.dbp_bcap + 16, 256);
+                            pp.dbp_nwin = int32_t((uint64_t(std::max(pd.uncompressed_size, pd.compressed_size)) + DBP_WIN - 1) / DBP_WIN + 1);
+                            pp.dbp_pub_off = nest_pub;
+                            nest_pub += uint64_t(pp.dbp_nwin) * sizeof(WinPub);
+                        }
+                    }
                     if (cd.physical_type == PF_BYTE_ARRAY) chars_hint += pd.uncompressed_size;
                     if (cd.physical_type == PF_BYTE_ARRAY &&
                         (pd.encoding == PF_ENC_DELTA_LENGTH_BYTE_ARRAY || pd.encoding == PF_ENC_DELTA_BYTE_ARRAY))
@@ -1127,6 +1138,13 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                 pg.lvltab = reinterpret_cast<uint32_t*>(S + pp.lt_off);
                 pg.lvl_cap = lvl_table_cap(pg.num_values);
                 ctx->l_lvl.push_back(int(i));
+            }
+            if (pp.dbp_off != ~0ull) {
+                pg.dbp = S + pp.dbp_off;
+                pg.dbp_pub = reinterpret_cast<WinPub*>(S + ctx->off_npub + pp.dbp_pub_off);
+                pg.dbp_nwin = pp.dbp_nwin;
+                pg.dbp_bcap = pp.dbp_bcap;
+                ctx->max_dbp_nwin = std::max(ctx->max_dbp_nwin, pp.dbp_nwin);
             }
             if (pp.seg_off != ~0ull) {
                 pg.seg = S + pp.seg_off;

@@ -30,7 +30,7 @@ def _zz(v):
     return (v << 1) ^ (v >> 63)
 
 
-def _dbp(values, block, nmini):
+def _dbp(values, block, nmini, junk_tail=False, bad_block=None):
     vpm = block // nmini
     out = bytearray(_uvarint(block) + _uvarint(nmini) + _uvarint(len(values)) + _uvarint(_zz(int(values[0])) & (2**64 - 1)))
     deltas = [(int(values[i]) - int(values[i - 1])) for i in range(1, len(values))]
@@ -43,8 +43,14 @@ def _dbp(values, block, nmini):
         for m in range(nmini):
             chunk = rel[m * vpm:(m + 1) * vpm]
             w = max((x.bit_length() for x in chunk), default=0)
-            widths.append(w)
             if not chunk:
+                widths.append(200 if junk_tail else 0)   # unconsumed miniblock: its width is never checked
+                continue
+            if bad_block is not None and b0 // block == bad_block and m == 0:
+                w = 65                                      # a width no INT64 reader accepts
+            widths.append(w)
+            if w > 64:
+                data += bytes((vpm * 64 + 7) // 8)
                 continue
             chunk = chunk + [0] * (vpm - len(chunk))
             acc = 0
@@ -65,11 +71,11 @@ def _page(body, num_values):
     return hdr + body
 
 
-def _write(path, values, block, nmini):
+def _write(path, values, block, nmini, **kw):
     from pfloor import _native
     from pfloor.writer import EncodedChunk, WriteField
     L = _native.lib()
-    page = _page(_dbp(values, block, nmini), len(values))
+    page = _page(_dbp(values, block, nmini, **kw), len(values))
     buf = C.create_string_buffer(page, len(page))
     ch = EncodedChunk()
     ch.bytes = C.cast(buf, C.c_void_p)
@@ -125,3 +131,34 @@ def test_gpu_dbp_configs(tmp_path, block, nmini):
     else:
         assert got["_status"] == 0, got["_error"]
         assert np.array_equal(np.frombuffer(got[(0, 0)]["values"].tobytes(), np.int64), v)
+
+
+# Pages of >= DBP_PAR_MIN (16384) entries take the block-parallel path (k_dbp_pos / k_dbp_blk /
+# k_dbp_scan, pf_delta.hip); PF_DBP_PAR=0 sends them to the one-workgroup k_delta. Both must give
+# the same values, accept junk widths of unconsumed trailing miniblocks and reject a bad width in a
+# middle block (which the parallel path hands back to k_delta).
+@pytest.mark.gpu
+@pytest.mark.parametrize("block,nmini", CONFIGS_OK)
+@pytest.mark.parametrize("par", ["1", "0"])
+def test_gpu_dbp_large_pages(tmp_path, monkeypatch, block, nmini, par):
+    from pfloor.decoder import decode_file
+    monkeypatch.setenv("PF_DBP_PAR", par)
+    v = _values(n=60001, seed=block + nmini)
+    path = str(tmp_path / f"dbp_big_{block}_{nmini}.parquet")
+    _write(path, v, block, nmini, junk_tail=True)
+    got = decode_file(path, device=0)
+    assert got["_status"] == 0, got["_error"]
+    assert np.array_equal(np.frombuffer(got[(0, 0)]["values"].tobytes(), np.int64), v)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("par", ["1", "0"])
+def test_gpu_dbp_large_page_bad_width(oracle, tmp_path, monkeypatch, par):
+    from pfloor.decoder import decode_file
+    monkeypatch.setenv("PF_DBP_PAR", par)
+    v = _values(n=40000, seed=9)
+    path = str(tmp_path / "dbp_big_bad.parquet")
+    _write(path, v, 128, 4, bad_block=100)
+    with oracle.open(path) as of:
+        assert of.decode(0, 0)["status"] != 0
+    assert decode_file(path, device=0)["_status"] != 0
