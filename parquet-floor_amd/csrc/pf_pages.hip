@@ -2842,8 +2842,9 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
 // ONE workgroup tile after tile: a 520K-entry page (one per chunk in config 5) runs ~1000 tiles in
 // series on one CU. Here the page is cut into segments of seg_len entries, each decoded by its own
 // workgroup from checkpoints of the three hybrid streams (rep, def, dictionary ids):
-//   k_nest_lvl   (page x {rep, def}, one wave): the stream's run headers, walked from LDS windows,
-//                give the state at every segment start;
+//   k_nest_lvl   (page x {rep, def} x 8 KiB window): every window position decoded as a run header,
+//                pointer jumping to the window exits, a single-pass hand-over between windows, and
+//                the state at every segment start;
 //   k_count_seg  (page x segment): slots / values / rows of the segment's levels;
 //   k_nest_scan  (page, one wave): their prefixes over the page, the page totals (k_scan), and the
 //                dictionary-id stream's state at each segment's first value;
@@ -2852,7 +2853,7 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
 //   k_decode_seg (page x segment): decode_page over the segment.
 // Checkpoint states are exactly rle_walk's state after the segment's first t values (mid-run when t
 // falls inside a run), so each segment's decode is the serial walk's, from t on.
-constexpr uint32_t NW_BYTES = 8192;   // k_nest_* LDS window over a stream
+constexpr uint32_t NW_BYTES = 8192;   // nest_walk's LDS window over a stream (k_nest_scan)
 static_assert(sizeof(RleState) == NEST_CK_BYTES, "checkpoint size (host plans the segment tables)");
 
 __device__ __forceinline__ RleState* nest_ck(const DevPage& pg, int k) {

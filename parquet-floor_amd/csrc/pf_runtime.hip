@@ -912,7 +912,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->timing_valid = false;
 
     // ---- input bytes on device ----
-    EVREC(ctx, ctx->ev[0], st);
+    // stage "h2d" (ev[0] -> ev[1]): the input copy when there is one, the metadata upload and the
+    // memsets; for device-resident input it starts at the metadata upload (not before the host plan)
+    const bool input_h2d = !bytes_on_device && n_bytes;
+    if (input_h2d) EVREC(ctx, ctx->ev[0], st);
     const uint8_t* d_bytes = bytes;
     if (!bytes_on_device && n_bytes) {
         HIPCHK(ctx, ctx->d_in.ensure(n_bytes));
@@ -1302,6 +1305,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         for (size_t j = 0; j < ctx->jobs.size(); j++) ctx->pages[size_t(ctx->jobs[j].page)].jfb = d_fb + j;
     }
     HIPCHK(ctx, ctx->h_res.ensure(align_up(sizeof(DevChunkResult) * n_chunks, 256) + sizeof(DevChunk) * n_chunks + 256));
+    if (!input_h2d) EVREC(ctx, ctx->ev[0], st);
     int rc = upload_meta(ctx);
     if (rc) return rc;
     mark();
