@@ -131,3 +131,59 @@ def test_damaged_nested_pages_same_status(decoder, monkeypatch, tmp_path):
     monkeypatch.delenv("PF_NEST_SEG")
     got = decode_file(os.path.join(GOLDEN, "ref_roundtrip.parquet"), decoder=decoder)
     assert got["_status"] == 0
+
+
+def _nested_types_file(tmp_path, rows=30000, seed=33):
+    """More leaf types under repetition: FIXED_LEN_BYTE_ARRAY(5), INT96 timestamps, FLOAT, BOOLEAN
+    (BOOLEAN pages stay on k_count / k_decode), INT32 dictionary three lists deep, an optional struct
+    field two levels down."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    rng = np.random.default_rng(seed)
+
+    def offsets(n, hi, null_p):
+        lens = rng.integers(0, hi, n)
+        nulls = rng.random(n) < null_p
+        lens = np.where(nulls, 0, lens)
+        o = np.zeros(n + 1, dtype=np.int32)
+        o[1:] = np.cumsum(lens)
+        return o, nulls, int(o[-1])
+
+    o, nl, m = offsets(rows, 5, 0.1)
+    flba = pa.array([bytes(rng.integers(0, 256, 5, dtype=np.uint8)) for _ in range(m)], type=pa.binary(5),
+                    mask=rng.random(m) < 0.1)
+    ts = pa.array((rng.integers(0, 2**40, m) * 1000).astype("datetime64[ns]"), mask=rng.random(m) < 0.1)
+    fl = pa.array(rng.random(m).astype(np.float32), mask=rng.random(m) < 0.2)
+    bo = pa.array(rng.random(m) < 0.5, mask=rng.random(m) < 0.1)
+    o2, nl2, m2 = offsets(m, 3, 0.05)
+    o3, nl3, m3 = offsets(m2, 3, 0.05)
+    deep_vals = pa.array(rng.integers(0, 20, m3).astype(np.int32), mask=rng.random(m3) < 0.1)
+    deep = pa.ListArray.from_arrays(pa.array(o3), deep_vals, mask=pa.array(nl3))
+    deep = pa.ListArray.from_arrays(pa.array(o2), deep, mask=pa.array(nl2))
+    st = pa.StructArray.from_arrays([pa.array(rng.integers(-5, 5, m).astype(np.int64), mask=rng.random(m) < 0.3),
+                                     pa.array(rng.random(m), mask=rng.random(m) < 0.3)], names=["x", "y"],
+                                    mask=pa.array(rng.random(m) < 0.1))
+
+    def lst(child):
+        return pa.ListArray.from_arrays(pa.array(o), child, mask=pa.array(nl))
+
+    t = pa.table({"f": lst(flba), "t": lst(ts), "fl": lst(fl), "b": lst(bo), "d": lst(deep), "s": lst(st)})
+    path = str(tmp_path / "nest_types.parquet")
+    pq.write_table(t, path, compression="snappy", row_group_size=rows, use_deprecated_int96_timestamps=True,
+                   use_dictionary=["d.list.element.list.element.list.element"], data_page_size=32 << 10)
+    return path
+
+
+@pytest.mark.parametrize("seg", [None, "100", "777"])
+def test_nested_leaf_types_in_segments(decoder, oracle, monkeypatch, tmp_path, seg):
+    from pfloor.decoder import decode_file
+    path = _nested_types_file(tmp_path)
+    if seg is not None:
+        monkeypatch.setenv("PF_NEST_SEG", seg)
+    got = decode_file(path, decoder=decoder)
+    with oracle.open(path) as of:
+        for rg in range(of.num_row_groups):
+            for c in range(of.num_columns):
+                g = got[(rg, c)]
+                assert g["status"] == 0, (rg, c, got["_error"])
+                assert_chunk_equal(g, of.decode(rg, c), f"types rg{rg} c{c} seg={seg}")
