@@ -884,9 +884,9 @@ __device__ void repair_window(const SnappyJob* __restrict__ jobs, const int2 jw,
     lo[lane] = acc;
 }
 
-// Grid-stride over the windows with a bounded grid: only windows the chain pass could not resolve
-// (WM_MERGE / WM_FULL) do work, and a launch of one staged block per 8 KiB window would wait for
-// CUs held by other streams' kernels.
+// Grid-stride over the windows (PF_REPAIR_GRID bounds the grid; by default one block per window):
+// only windows the chain pass could not resolve (WM_MERGE / WM_FULL) and windows inside a literal
+// (WM_SKIP: bitmap cleared) do work.
 __global__ __launch_bounds__(64) void k_snappy_repair(const SnappyJob* __restrict__ jobs, const int2* __restrict__ wins,
                                                       int n_wins, const SnapWin* __restrict__ win,
                                                       uint32_t* __restrict__ lane_out, int* __restrict__ fb) {
@@ -1420,7 +1420,10 @@ void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins
     if (n_jobs <= 0) return;
     hipLaunchKernelGGL(k_snappy_index, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, d_win, d_ent, d_lane_out, d_fb);
     hipLaunchKernelGGL(k_snappy_chain, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_win, (const SnapEnt*)d_ent, d_lane_out, d_fb);
-    hipLaunchKernelGGL(k_snappy_repair, dim3(std::min(n_wins, 1024)), dim3(64), 0, s, d_jobs, d_wins, n_wins,
+#ifndef PF_REPAIR_GRID   // (1024: SF1 3.30 ms mean of 6 interleaved runs; 4096: 3.28; one per window: 3.26 of 3)
+#define PF_REPAIR_GRID (1 << 24)
+#endif
+    hipLaunchKernelGGL(k_snappy_repair, dim3(std::min(n_wins, PF_REPAIR_GRID)), dim3(64), 0, s, d_jobs, d_wins, n_wins,
                        (const SnapWin*)d_win, d_lane_out, d_fb);
     hipLaunchKernelGGL(k_snappy_splits, dim3(n_jobs), dim3(64), 0, s, d_jobs, (const SnapWin*)d_win,
                        (const uint32_t*)d_lane_out, d_splits, d_fb);
