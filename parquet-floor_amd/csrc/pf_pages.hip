@@ -2412,8 +2412,6 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     __shared__ uint32_t s_runs[4 * LVL_RUNS_LDS];
     __shared__ uint32_t s_T[4 + 2 * RUN_CAP];
     __shared__ uint16_t s_nxt[LVL_NXT];   // position of the next run header, per byte position
-    __shared__ uint16_t s_jmp[2][LVL_NXT];   // pointer doubling (chain positions)
-    __shared__ uint32_t s_mark[LVL_NXT / 32];
     const int pi = list[blockIdx.x];
     DevPage& pg = pages[pi];
     uint32_t* LT = pg.lvltab;
@@ -2438,13 +2436,6 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
         if (tid == 0) LT[1] = 0;
         return;
     }
-#ifdef PF_STAMPS
-    unsigned long long t_ph = __builtin_amdgcn_s_memtime();
-    if (tid == 0) PSTAMP(11, 1);
-#define LVL_PH(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) PSTAMP(i, t_ - t_ph); t_ph = t_; } while (0)
-#else
-#define LVL_PH(i) ((void)0)
-#endif
     {
         const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(sa - woff);
         const uint32_t nchunk = (woff + dn + 15u) / 16u;
@@ -2475,58 +2466,18 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
             s_nxt[p] = uint16_t(nx);
         }
         __syncthreads();
-        LVL_PH(12);
-        // the chain's positions: reachability from 0 by pointer doubling (round r marks the positions
-        // 2^r steps after a marked one; the jump table doubles, double-buffered), then compaction in
-        // position order (= chain order). A position with no run (s_nxt == 0xffff) is marked when
-        // reached and ends its chain, as the one-lane chase (one LDS load per run, ~270 cycles each:
-        // 70 % of the kernel at ~1,000 runs per page) recorded it.
-        {
-            for (uint32_t w = tid; w < LVL_NXT / 32; w += LT_NT) s_mark[w] = w == 0 && dn > 0 ? 1u : 0u;
-            for (uint32_t q = tid; q < dn; q += LT_NT) s_jmp[0][q] = s_nxt[q];
-            __syncthreads();
-            uint32_t cur = 0;
-            for (uint32_t span = 1; span < dn; span <<= 1) {
-                const uint16_t* J = s_jmp[cur];
-                uint16_t* J2 = s_jmp[cur ^ 1];
-                bool added = false;
-                for (uint32_t q = tid; q < dn; q += LT_NT) {
-                    const uint32_t j = J[q];
-                    if (j < dn) {
-                        if ((s_mark[q >> 5] >> (q & 31u)) & 1u) {
-                            const uint32_t bit = 1u << (j & 31u);
-                            added |= !(atomicOr(&s_mark[j >> 5], bit) & bit);
-                        }
-                        J2[q] = J[j];
-                    } else {
-                        J2[q] = uint16_t(0xffffu);
-                    }
-                }
-                // nothing new 2^r .. 2^(r+1) steps out: the chain has ended
-                if (!__any(added)) break;
-                __syncthreads();
-                cur ^= 1;
-            }
-        }
         uint32_t nh = 0;
-        for (uint32_t w0 = 0; w0 < (dn + 31) / 32; w0 += LT_NT) {
-            const uint32_t w = w0 + uint32_t(tid);
-            const uint32_t mw = w < (dn + 31) / 32 ? s_mark[w] : 0u;
-            const uint32_t c = __popc(mw);
-            uint32_t x = c;
-            #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(x, d, 64);
-                if (tid >= d) x += y;
+        {
+            uint32_t p = 0;
+            while (p < dn && nh < cap) {
+                if (tid == 0) runs[4 * nh + 1] = p;   // header positions, decoded below
+                nh++;
+                const uint32_t q = s_nxt[p];
+                if (q == 0xffffu) break;
+                p = q;
             }
-            uint32_t k = nh + x - c;
-            for (uint32_t m = mw; m; m &= m - 1u, k++)
-                if (k < cap) runs[4 * k + 1] = w * 32u + uint32_t(__ffs(m) - 1);   // header positions, decoded below
-            nh += __shfl(x, 63, 64);
         }
-        nh = min(nh, cap);
-        __syncthreads();   // the header positions are visible to the wave
-        LVL_PH(13);
+        __syncthreads();   // lane 0's header positions are visible to the wave
         uint64_t carry = 0;
         uint32_t nr = 0, ok = 1;
         for (uint32_t c0 = 0; c0 < nh && carry < ne; c0 += LT_NT) {
@@ -2622,7 +2573,6 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     // end entries, the level bytes its packed runs read and the dictionary-id bytes of its values
     __threadfence_block();
     __syncthreads();
-    LVL_PH(14);
     uint32_t* BT = runs + 4 * cap;
     const uint32_t nblk = (ne + FBLK - 1) / FBLK;
     // dictionary id runs (k_runs, same stream): value index -> bit offset in the id stream
@@ -2689,8 +2639,6 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     }
     fit = __all(fit) ? 1u : 0u;   // one wave
     if (tid == 0) { LT[0] = nr; LT[2] = carry; LT[1] = fit; }
-    LVL_PH(15);
-#undef LVL_PH
 }
 
 // k_flat_null: one 512-thread workgroup per 4096-entry block, 8 consecutive entries per thread. The
