@@ -53,13 +53,36 @@ RG_ROWS = 1 << 20
 SEED = 42
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PCIE_GBS = 63.0         # MI355X_MICROARCH.md: PCIe Gen5 x16 per direction
-# kernels of each stage (rocprof names), for the PMC traffic and the label of the roofline object
-STAGE_KERNELS = {"snappy_exec": r"k_snappy_exec", "snappy_parse": r"k_snappy_(index|chain)$",
-                 "flat": r"k_flat(_fixed|_null)?$", "decode": r"k_decode$", "delta": r"k_delta$",
-                 "count": r"k_count(_flat)?$"}
-STAGE_LABEL = {"snappy_exec": "k_snappy_exec2 (Snappy executor stage)", "snappy_parse": "k_snappy_index + k_snappy_chain",
-               "flat": "flat stage: k_flat_fixed + k_flat_null + k_flat", "decode": "k_decode",
-               "delta": "k_delta (DELTA_BINARY_PACKED)", "count": "count stage: k_count_flat + k_count"}
+# kernels of each stage (rocprof names, pf_runtime.hip's launch order between the stage events), for
+# the PMC traffic and the label of the roofline object
+STAGE_KERNELS = {
+    "snappy_parse": r"k_snappy_(head|litcopy|index|chain|repair|splits)$",
+    "snappy_exec": r"k_snappy_(exec2|serial)$",
+    "delta": r"k_(dbp_pos|dbp_blk|dbp_scan|delta)$",
+    "levels": r"k_(runs|lvl|dlen)$",
+    "count": r"k_(nest_lvl|count|count_flat|count_seg|nest_scan|nest_ids|nest_chars|ba_[a-z]+)$",
+    "scan": r"k_scan$",
+    "flat": r"k_flat(_all|_fixed|_null)?$",
+    "decode": r"k_(decode|decode_seg|dba_chars)$",
+}
+STAGE_LABEL = {"snappy_exec": "Snappy executor stage: k_snappy_exec2 (+ redo, serial fallback)",
+               "snappy_parse": "Snappy parse stage: k_snappy_head + index + chain + repair + splits",
+               "delta": "DELTA_BINARY_PACKED stage: k_dbp_pos / k_dbp_blk / k_dbp_scan + k_delta",
+               "levels": "level / id run stage: k_runs + k_lvl + k_dlen",
+               "count": "count stage: k_nest_lvl, k_count[_flat|_seg], k_nest_scan / ids / chars, PLAIN BYTE_ARRAY k_ba_*",
+               "scan": "k_scan", "flat": "flat stage: k_flat_all (k_flat_fixed + k_flat_null + k_flat)",
+               "decode": "decode stage: k_decode + k_decode_seg + k_dba_chars"}
+# the algorithmic bytes each stage is priced with (bench.stage_bytes)
+STAGE_BYTES_DEF = {
+    "snappy_parse": "compressed Snappy stream bytes read",
+    "snappy_exec": "compressed Snappy stream bytes read + decompressed bytes written",
+    "delta": "DELTA_BINARY_PACKED sections read + values written (4 or 8 B)",
+    "levels": "page bodies (decompressed) of nullable / dictionary-encoded pages, read once",
+    "count": "page bodies (decompressed) of BYTE_ARRAY and nested pages, read once",
+    "scan": "none (prefix sums over page counts)",
+    "flat": "page bodies (decompressed) read once + decoded column bytes written",
+    "decode": "page bodies (decompressed) read once + decoded column bytes written",
+}
 ROOF_PASSES = 3         # isolated decodes of context 0's first batch for the roofline kernel time
 E2E_PASSES = 2
 METRIC = "decoded GB/s + rows/s (node), lineitem-shape Snappy+dict, 1/2/4/8 GPUs"
@@ -250,11 +273,14 @@ class BatchInput:
         self.host.free()
 
 
-def page_stats(descs):
-    """Algorithmic byte counts from the page headers."""
-    comp = uncomp = snappy_in = snappy_out = dbp_body = dbp_values = 0
+def page_stats(descs, cols=None):
+    """Algorithmic byte counts from the page headers. cols: the chunks' column
+    descriptors (same order), for the per-stage counts."""
+    comp = uncomp = snappy_in = snappy_out = dbp_body = dbp_out = 0
+    lvl_body = count_body = 0
     pages = 0
-    for d in descs:
+    for ci, d in enumerate(descs):
+        col = cols[ci] if cols is not None else None
         for i in range(d.n_pages):
             p = d.pages[i]
             pages += 1
@@ -266,9 +292,21 @@ def page_stats(descs):
                 snappy_out += p.uncompressed_size - lvl
             if p.encoding == 5 and p.page_type in (0, 3):   # DELTA_BINARY_PACKED data page
                 dbp_body += p.uncompressed_size - lvl
-                dbp_values += p.num_values
+                dbp_out += p.num_values * (4 if d.physical_type == 1 else 8)
+            if col is not None and p.page_type in (0, 3):
+                if col.max_def > 0 or p.encoding in (2, 8):
+                    lvl_body += p.uncompressed_size
+                if col.physical_type == 6 or col.max_rep > 0:
+                    count_body += p.uncompressed_size
     return dict(pages=pages, compressed=comp, uncompressed=uncomp, snappy_in=snappy_in, snappy_out=snappy_out,
-                dbp_body=dbp_body, dbp_values=dbp_values)
+                dbp_body=dbp_body, dbp_out=dbp_out, lvl_body=lvl_body, count_body=count_body)
+
+
+def stage_bytes(st, dbytes):
+    """Algorithmic bytes per stage (STAGE_BYTES_DEF) of one batch."""
+    return {"snappy_exec": st["snappy_in"] + st["snappy_out"], "snappy_parse": st["snappy_in"],
+            "delta": st["dbp_body"] + st["dbp_out"], "levels": st["lvl_body"], "count": st["count_body"],
+            "flat": st["uncompressed"] + dbytes, "decode": st["uncompressed"] + dbytes}
 
 
 def chunk_decoded_bytes(col, ci):
@@ -503,8 +541,9 @@ def spawn_ranks(args, argv):
 
 class ContextPool:
     """One persistent host thread per decode stream (ctypes releases the GIL, so the host-side
-    planning of one stream overlaps the GPU work of the others). run(k) makes every stream decode
-    its batches k times in order and returns when all are done.
+    planning of one stream overlaps the GPU work of the others). The threads are started once and
+    parked on a condition between runs, so run(k) costs no thread start / join: it hands every
+    stream "decode your batches k times in order" and returns when all are done.
 
     pipelined=True (the timed steps): each stream has two contexts sharing its HIP stream
     (pf_ctx_create_shared); batch i+1 is planned and enqueued on one while batch i still decodes on
@@ -519,6 +558,11 @@ class ContextPool:
         self.last = list(decs)           # per stream: the context holding its last decoded batch
         self.stage_acc, self.host_s, self.host_calls = {}, 0.0, 0
         self._lock = threading.Lock()
+        self._cv = threading.Condition()
+        self._gen, self._job, self._done, self._errs, self._stop = 0, None, 0, [], False
+        self._threads = [threading.Thread(target=self._loop, args=(i,), daemon=True) for i in range(len(decs))]
+        for t in self._threads:
+            t.start()
 
     def _decode(self, d, bi):
         t0 = time.perf_counter()
@@ -533,46 +577,81 @@ class ContextPool:
         if d.wait() != 0:
             raise RuntimeError(d.error())
 
-    def _worker(self, i, passes, pipelined, errs):
+    def _work(self, i, passes, pipelined):
         d, bl = self.decs[i], self.batches[i]
-        try:
-            if pipelined:
-                pair = (d, self.twins[i])
-                seq = [bi for _ in range(passes) for bi in bl]
-                for k, bi in enumerate(seq):
-                    self._decode(pair[k % 2], bi)
-                    if k > 0:
-                        self._wait(pair[(k - 1) % 2])
-                if seq:
-                    self._wait(pair[(len(seq) - 1) % 2])
-                    self.last[i] = pair[(len(seq) - 1) % 2]
-                return
-            for _ in range(passes):
-                for bi in bl:
-                    self._decode(d, bi)
-                    self._wait(d)
-                    if i == 0:
-                        for k, v in d.timing().items():
-                            self.stage_acc[k] = self.stage_acc.get(k, 0.0) + v
-            self.last[i] = d
-        except Exception as e:
-            errs.append(e)
+        if pipelined:
+            pair = (d, self.twins[i])
+            seq = [bi for _ in range(passes) for bi in bl]
+            for k, bi in enumerate(seq):
+                self._decode(pair[k % 2], bi)
+                if k > 0:
+                    self._wait(pair[(k - 1) % 2])
+            if seq:
+                self._wait(pair[(len(seq) - 1) % 2])
+                self.last[i] = pair[(len(seq) - 1) % 2]
+            return
+        for _ in range(passes):
+            for bi in bl:
+                self._decode(d, bi)
+                self._wait(d)
+                if i == 0:
+                    for k, v in d.timing().items():
+                        self.stage_acc[k] = self.stage_acc.get(k, 0.0) + v
+        self.last[i] = d
+
+    def _loop(self, i):
+        seen = 0
+        while True:
+            with self._cv:
+                self._cv.wait_for(lambda: self._stop or self._gen != seen)
+                if self._stop:
+                    return
+                seen, job = self._gen, self._job
+            try:
+                self._work(i, *job)
+            except Exception as e:
+                self._errs.append(e)
+            with self._cv:
+                self._done += 1
+                self._cv.notify_all()
 
     def set_timing(self, on):
         for d in self.decs + (self.twins or []):
             d.set_timing(on)
 
     def run(self, passes, pipelined=False):
-        errs = []
         self.set_timing(not pipelined)
-        ts = [threading.Thread(target=self._worker, args=(i, passes, pipelined, errs)) for i in range(len(self.decs))]
-        [t.start() for t in ts]
-        [t.join() for t in ts]
-        if errs:
-            raise errs[0]
+        with self._cv:
+            self._errs, self._done, self._job = [], 0, (passes, pipelined)
+            self._gen += 1
+            self._cv.notify_all()
+            self._cv.wait_for(lambda: self._done == len(self._threads))
+        if self._errs:
+            raise self._errs[0]
+
+    def warm(self, passes, min_s, pipelined=True):
+        """Untimed warmup: `passes` passes, then more until at least min_s seconds of identical work
+        have run (clocks and caches settle; a 5-pass warmup is ~16 ms). Returns the passes run."""
+        t0 = time.perf_counter()
+        n = 0
+        if passes > 0:
+            self.run(passes, pipelined)
+            n = passes
+        while time.perf_counter() - t0 < min_s:
+            k = max(1, n)   # doubling chunks: few run() calls
+            self.run(k, pipelined)
+            n += k
+        return n
 
     def reset(self):
         self.stage_acc, self.host_s, self.host_calls = {}, 0.0, 0
+
+    def close(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        for t in self._threads:
+            t.join()
 
 
 def main():
@@ -580,6 +659,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)   # ~1.2 s timed: long enough for an SMI sampler to see the GPU busy
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup-s", type=float, default=0.3,
+                    help="untimed warmup runs at least --warmup passes and at least this many seconds of them")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="sf1")
     ap.add_argument("--data-dir", default=os.environ.get("PF_BENCH_DIR", "/tmp/pfloor_bench"))
     ap.add_argument("--streams", type=int, default=4,
@@ -631,7 +712,7 @@ def main():
         pmc = {"error": "skipped: bench.py is running under a profiler"}
     elif world == 1 and not args.no_pmc:
         try:
-            pmc = measure_pmc(args, "k_snappy_exec|k_snappy_index|k_snappy_chain|k_flat|k_decode|k_delta|k_count")
+            pmc = measure_pmc(args, "k_snappy|k_flat|k_decode|k_delta|k_dbp|k_count|k_runs|k_lvl|k_dlen|k_nest|k_ba_|k_scan|k_dba")
         except Exception as e:
             pmc = {"error": repr(e)}
 
@@ -662,7 +743,9 @@ def main():
     _native.check(_native.lib().pf_sync(decs[0].h), decs[0].h, "pf_sync")   # uploads done before any context reads them
 
     pool = ContextPool(decs, batches, True, twins)
-    pool.run(args.warmup, pipelined=not args.no_pipeline)
+    t_w = time.perf_counter()
+    warm_passes = pool.warm(args.warmup, args.warmup_s, pipelined=not args.no_pipeline)
+    warm_s = time.perf_counter() - t_w
     # decoded bytes of one step (every batch's result is identical each step)
     dbytes = 0
     for d, bl in zip(decs, batches):
@@ -717,7 +800,7 @@ def main():
 
     # ---- roofline of the dominant stage: context 0's first batch decoded alone ----
     b0 = batches[0][0]
-    st0 = page_stats(b0.descs)
+    st0 = page_stats(b0.descs, [pf.columns[c] for (_p, c, *_r) in b0.items])
     dbytes0 = 0
     iso = {}
     dec = decs[0]
@@ -729,24 +812,18 @@ def main():
             iso[k] = iso.get(k, 0.0) + v / ROOF_PASSES
     for i, (p, c, *_r) in enumerate(b0.items):
         dbytes0 += chunk_decoded_bytes(pf.columns[c], dec.info(i))
-    kern_bytes = {
-        "snappy_exec": st0["snappy_in"] + st0["snappy_out"],   # compressed read + decompressed written
-        "snappy_parse": st0["snappy_in"],                       # compressed read (token index)
-        "flat": st0["uncompressed"] + dbytes0,                  # page bodies read + decoded bytes written
-        "decode": st0["uncompressed"] + dbytes0,
-        "delta": st0["dbp_body"] + 8 * st0["dbp_values"],      # DBP values sections read + 8-B values written
-        "count": st0["uncompressed"],                            # page bodies read (levels / lengths / ids)
-    }
+    kern_bytes = stage_bytes(st0, dbytes0)
     dom = max((k for k in iso if k in kern_bytes), key=lambda k: iso.get(k, 0.0))
     dom_ms = iso.get(dom, 0.0)
     dom_bytes = kern_bytes[dom]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else None
-    traffic, traffic_detail = None, None
+    traffic, traffic_detail, traffic_names = None, None, None
     if pmc and "error" not in pmc:
         traffic_detail = pmc_traffic_per_kernel(pmc)
         names = [n for n in traffic_detail if STAGE_KERNELS.get(dom) and re.match(STAGE_KERNELS[dom], n.split("<")[0])]
         if names:
             traffic = sum(traffic_detail[n]["traffic_bytes"] for n in names)
+            traffic_names = sorted(names)
     b_alg_step = None
     descs_all = [d for bl in batches for bi in bl for d in bi.descs]
     st_all = page_stats(descs_all)
@@ -824,6 +901,8 @@ def main():
         "value": round(value, 3), "unit": "decoded GB/s",
         "rows_per_s": round(float(tot[1]) * args.steps / dt, 1),
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "warmup_policy": {"passes_run": warm_passes, "seconds": round(warm_s, 3),
+                          "rule": f"max(--warmup passes, passes filling {args.warmup_s} s), untimed, same work as a step"},
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
         "dtype": "u8", "data": f"synthetic (pyarrow-written {w['kind']}-shaped file, seed {w['seed']})",
@@ -845,7 +924,8 @@ def main():
                      "traffic_source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE per launch, measured in "
                                        "this run (child processes, same batch, 1 stream)" if traffic else
                                        (pmc or {}).get("error"),
-                     "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4),
+                     "algorithmic_bytes_per_launch": dom_bytes, "algorithmic_bytes_def": STAGE_BYTES_DEF.get(dom),
+                     "traffic_kernels": traffic_names, "launch_ms": round(dom_ms, 4),
                      "launch_ms_source": f"HIP events on context 0's stream, its first batch decoded alone x{ROOF_PASSES} "
                                          "after the timed region",
                      "stage_ms_overlapped": round(stage_ms.get(dom, 0.0), 4)},
@@ -866,6 +946,7 @@ def main():
             out["cpu_baseline"] = cpu_baselines(path, pf)
         except Exception as e:   # reported, never fatal
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    pool.close()
     for bi in cache.values():
         bi.free(decs[0])
     for d in twins + decs:

@@ -3022,7 +3022,8 @@ __global__ __launch_bounds__(NL_NT) void k_nest_lvl(const DevChunk* __restrict__
     const int nseg = pg.nseg;
     const uint64_t sl = uint64_t(uint32_t(pg.seg_len));
     RleState* out = nest_ck(pg, which);
-    if (which == 0 && w == 0 && tid == 0) pg.seg_ok = 1;
+    // (max: a window that timed out waiting for its hand-over may already have set 2 = failed)
+    if (which == 0 && w == 0 && tid == 0) __hip_atomic_fetch_max(&pg.seg_ok, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (which == 1 && ck.max_def == 0) {
         if (w == 0) for (int k = tid; k < nseg; k += NL_NT) { RleState r; rle_init(r); out[k] = r; }
         return;
@@ -3102,7 +3103,9 @@ __global__ __launch_bounds__(NL_NT) void k_nest_lvl(const DevChunk* __restrict__
             }
         }
         WinPub& me = pub[w];
-        if (!ok) set_status(res, pg.chunk, ST_CORRUPT, pi);
+        // a hand-over that never came (a scheduling stall, not the data): the page leaves the segment
+        // path and k_count / k_decode decode it whole, as k_dbp_pos does with dbp_ok = 2
+        if (!ok) __hip_atomic_fetch_max(&pg.seg_ok, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&me.p, xp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&me.e, xe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&me.st, xst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

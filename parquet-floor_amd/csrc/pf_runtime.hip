@@ -85,7 +85,7 @@ struct HostBuf {
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-constexpr int N_EVENTS = 10;  // h2d, snappy parse, snappy exec, dict, delta, count, scan, flat, decode
+constexpr int N_EVENTS = 11;  // h2d, snappy parse, snappy exec, dict, delta, levels, count, scan, flat, decode
 constexpr uint32_t BA_TILE_BYTES = 8192;   // pf_pages.hip BA_TILE
 constexpr int64_t FLAT_BLK = 4096;         // pf_pages.hip FBLK   // h2d, snappy, dict, delta, count, scan, flat, decode
 
@@ -253,25 +253,26 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st);
     EVREC(ctx, ctx->ev[4], st);
     launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), ctx->max_dbp_nwin, d_res, st);
+    EVREC(ctx, ctx->ev[5], st);
     launch_runs(d_chunks, d_pages, d_runs, int(ctx->l_runs.size()), d_res, st);
     launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st);
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
-    EVREC(ctx, ctx->ev[5], st);
+    EVREC(ctx, ctx->ev[6], st);
     launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, ctx->max_nwin, d_res, st);
     launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st);
     launch_nest_count(d_chunks, d_pages, d_nest, n_nest, d_nseg, n_nseg, d_res, st);
     launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
               d_res, st);
-    EVREC(ctx, ctx->ev[6], st);
+    EVREC(ctx, ctx->ev[7], st);
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
-    EVREC(ctx, ctx->ev[7], st);
-    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty());
     EVREC(ctx, ctx->ev[8], st);
+    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty());
+    EVREC(ctx, ctx->ev[9], st);
     launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), ctx->n_decode_first, d_res, st);
     launch_nest_decode(d_chunks, d_pages, d_nseg, n_nseg, d_res, st);
     launch_dba_chars(d_chunks, d_pages, d_dba, int(ctx->l_dba.size()), d_res, st);
-    EVREC(ctx, ctx->ev[9], st);
+    EVREC(ctx, ctx->ev[10], st);
     HIPCHK(ctx, hipGetLastError());
     // results + device-written chunk fields (chars base) back to pinned host memory
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_res.p, meta + ctx->off_res, sizeof(DevChunkResult) * ctx->n_chunks,
@@ -1751,6 +1752,29 @@ int pf_debug_page_direct(pf_ctx* ctx, int* out, int n_pages) {
         HIPCHK(ctx, hipMemcpy(pg.data(), static_cast<uint8_t*>(ctx->d_meta.p) + ctx->off_pages, sizeof(DevPage) * size_t(m),
                               hipMemcpyDeviceToHost));
         for (int i = 0; i < m; i++) out[i] = pg[size_t(i)].direct;
+    }
+    return np;
+}
+
+// Diagnostics (not part of pfloor.h): per page of the last finished pf_decode_row_group, which
+// parallel paths took it: {direct (DIRECT_*), dbp_ok (1 = k_dbp_* decoded it, 2 = handed back to
+// k_delta), seg_ok (1 = nested segment kernels, 2 = hand-over failed, decoded whole)}. Returns the
+// page count; out holds 3 ints per page.
+int pf_debug_page_paths(pf_ctx* ctx, int* out, int n_pages) {
+    if (!ctx || !ctx->d_meta.p || !ctx->tables_from_decode) return fail(ctx, PF_ERR_STATE, "no finished decode");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int np = int(ctx->pages.size());
+    const int m = n_pages < np ? n_pages : np;
+    if (out && m > 0) {
+        std::vector<DevPage> pg(static_cast<size_t>(m));
+        HIPCHK(ctx, hipMemcpy(pg.data(), static_cast<uint8_t*>(ctx->d_meta.p) + ctx->off_pages, sizeof(DevPage) * size_t(m),
+                              hipMemcpyDeviceToHost));
+        for (int i = 0; i < m; i++) {
+            out[3 * i] = pg[size_t(i)].direct;
+            out[3 * i + 1] = pg[size_t(i)].dbp_ok;
+            out[3 * i + 2] = pg[size_t(i)].seg_ok;
+        }
     }
     return np;
 }

@@ -230,7 +230,7 @@ class GpuDecoder:
         buf = (C.c_float * 16)()
         n = C.c_int()
         check(lib().pf_last_timing(self.h, buf, 16, C.byref(n)), self.h, "pf_last_timing")
-        names = ["h2d", "snappy_parse", "snappy_exec", "dict", "delta", "count", "scan", "flat", "decode"]
+        names = ["h2d", "snappy_parse", "snappy_exec", "dict", "delta", "levels", "count", "scan", "flat", "decode"]
         return dict(zip(names, list(buf)[:n.value]))
 
     def fetch_batch(self, chunk_types):

@@ -232,18 +232,18 @@ class RowGroupPipeline:
         self.row_groups = list(row_groups)
         self.depth = max(1, int(depth))
         self.decs = []   # [device slot][k]
-        try:
-            for d in devices:
-                first = GpuDecoder(d)
-                slot = [first]
-                for _ in range(self.depth - 1):
-                    slot.append(GpuDecoder(share=first))
-                self.decs.append(slot)
-        except Exception:
-            self.close()
-            raise
         self.inflight = collections.OrderedDict()   # position in row_groups -> decoder, or the enqueue error
         self.next_enqueue = 0
+        try:
+            for d in devices:
+                slot = []
+                self.decs.append(slot)   # registered before its contexts exist: close() frees a partial slot
+                slot.append(GpuDecoder(d))
+                for _ in range(self.depth - 1):
+                    slot.append(GpuDecoder(share=slot[0]))
+        except Exception:
+            self.close()   # the contexts created so far; the device error propagates
+            raise
 
     def _decoder(self, i):
         g = len(self.decs)
