@@ -148,6 +148,16 @@ def logical_row_groups(args, n_phys, world):
     return w.get("logical", n_phys)
 
 
+def chunk_cost(pf, p, c, kind):
+    """LPT cost of one column chunk: its compressed bytes, or the decompressed bytes of its pages
+    (what the Snappy executor and the value kernels walk: dense integer columns cost more per
+    compressed byte than text)."""
+    if kind == "compressed":
+        return pf.chunk_range(p, c)[1]
+    d = pf.chunk_desc(p, c, 0)
+    return sum(d.pages[i].uncompressed_size for i in range(d.n_pages))
+
+
 def units_for_rank(args, pf, world, rank, S, batch=None):
     """This rank's work units (logical rg, physical rg, columns), dealt to S contexts, then grouped
     into decode batches: [[batch, ...] per context], batch = list of units."""
@@ -204,7 +214,7 @@ def units_for_rank(args, pf, world, rank, S, batch=None):
         # of adding up. A column heavier than a context's fair share is cut into that many slices of
         # its row groups; slices go longest-processing-time first (compressed bytes) to the least
         # loaded context.
-        size = {(p, c): pf.chunk_range(p, c)[1] for _, p, _ in units for c in cols}
+        size = {(p, c): chunk_cost(pf, p, c, getattr(args, "lpt_cost", "compressed")) for _, p, _ in units for c in cols}
         cost = {c: sum(size[(p, c)] for _, p, _ in units) for c in cols}
         share = sum(cost.values()) / S
         slices = []
@@ -355,7 +365,7 @@ def measure_pmc(args, kernel_re):
         cmd = [prof, "--pmc", cnt, "--kernel-include-regex", kernel_re, "--output-format", "csv", "-d", d, "-o", "run",
                "--", sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
                "--data-dir", args.data_dir, "--streams", str(args.streams), "--split", args.split, "--pool", str(args.pool),
-               "--string-ctx", str(args.string_ctx)]
+               "--string-ctx", str(args.string_ctx), "--lpt-cost", args.lpt_cost]
         t0 = time.time()
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
         log(f"[bench] rocprofv3 --pmc {cnt}: rc {r.returncode} in {time.time() - t0:.1f}s")
@@ -669,6 +679,8 @@ def main():
                     help="sf1: give each context all row groups of a column subset (default), the same with "
                          "BYTE_ARRAY and fixed-width columns on separate contexts (kinds), or whole row groups")
     ap.add_argument("--string-ctx", type=int, default=2, help="--split kinds: contexts for the BYTE_ARRAY columns")
+    ap.add_argument("--lpt-cost", choices=("decompressed", "compressed"), default="compressed",
+                    help="sf1 --split columns: the per-chunk cost the column slices are dealt by")
     ap.add_argument("--columns", default=None, help=argparse.SUPPRESS)   # analysis only: comma-separated column subset
     ap.add_argument("--pool", type=int, default=100000,
                     help="wide: distinct values per column (SURVEY 8(d) sweep: 1K, 16K, 32K, 64K, 100K)")

@@ -40,8 +40,9 @@ struct SnappyJob {
     uint8_t* ddst;
     uint32_t dlo;
     uint32_t dgran;
-    uint32_t dflags;      // diagnostics: bit 0 = the block-parallel executor rejects the job (PF_DEBUG_FORCE_REDO)
-    uint32_t lit;         // FB_LITCOPY: where the page's one literal starts in src
+    uint32_t dflags;      // bit 0 (diagnostics) = the block-parallel executor rejects the job (PF_DEBUG_FORCE_REDO);
+                          // bit 1 = k_snappy_litcopy candidate (dictionary page, or a data page that did not compress)
+    uint32_t lit;         // FB_LITCOPY: the page's literal count (their table is in tokmap)
 };
 
 enum : int32_t { DONE_FIXED = 1, DONE_FLAT = 2, DONE_NULL = 4 };
@@ -155,6 +156,7 @@ constexpr uint32_t RT_BYTES = 16 + 8 * RT_CAP;
 constexpr uint32_t LT_BLOCK_RUNS = 512;    // most runs one k_flat_null block may overlap (its LDS table)
 constexpr uint32_t LT_BT_WORDS = 8;
 constexpr uint32_t NL_DST = 4096;          // level bytes one k_flat_null block stages in LDS
+constexpr uint32_t NULL_DICT_LDS = 16384;   // k_flat_null stages dictionaries up to this many bytes in LDS
 constexpr uint32_t NL_IST = 12288;         // dictionary-id bytes one k_flat_null block stages in LDS
 __host__ __device__ inline uint32_t lvl_table_cap(int32_t num_values) {
     // RLE runs are >= 8 repeats and bit-packed groups 8 values for the writers we know (parquet-mr,

@@ -1721,16 +1721,35 @@ __global__ __launch_bounds__(64) void k_snappy_head(SnappyJob* __restrict__ jobs
     if (t.kind != 0) return;
     const uint64_t data = pos + t.arg;   // the first literal's bytes: in[data, data + t.ol)
     if (data + t.ol > n) return;
-    if (pg.flags & PG_DICT) {
-        // dictionary pointers (dict_data, BaJob.p) were set from the scratch body, and gathers want it
-        // aligned: a one-literal dictionary page is copied there by k_snappy_litcopy, without a parse
-        if (pos + t.tl == n && t.ol == J.dst_len) {
-            J.lit = uint32_t(data);
+    const bool one = pos + t.tl == n && t.ol == J.dst_len;   // one literal covers the page
+    if ((J.dflags & 2u) && !(one && !(pg.flags & PG_DICT))) {
+        // a stream of literals only (incompressible data: Snappy emits one literal per 64 KiB block,
+        // e.g. a 400 KB dictionary of random values is 7): copied to the scratch body by
+        // k_snappy_litcopy from a table {data offset, output offset} per literal, kept in the job's
+        // token bitmap (unused: no index pass runs on the job), without any parse. Dictionary pages
+        // always take this (their decoded pointers were set from the scratch body, and gathers want it
+        // aligned); data pages only when flagged by the host (compressed size >= uncompressed).
+        uint32_t* tab = J.tokmap;
+        uint64_t p = pos, o = 0;
+        uint32_t cnt = 0;
+        while (p < n && cnt < LC_MAX) {
+            const SnapTok u = snap_tok(glb_read8(in, n, p));
+            const uint64_t d = p + u.arg;
+            if (u.kind != 0 || d + u.ol > n) break;
+            tab[2 * cnt] = uint32_t(d);
+            tab[2 * cnt + 1] = uint32_t(o);
+            o += u.ol;
+            p = d + u.ol;
+            cnt++;
+        }
+        if (p == n && o == J.dst_len && cnt > 0) {
+            J.lit = cnt;
             fb[j] = FB_LITCOPY;
         }
         return;
     }
-    if (pos + t.tl == n && t.ol == J.dst_len) {   // one literal covers the page
+    if (pg.flags & PG_DICT) return;
+    if (one) {
         pg.body = in + data;
         pg.direct = DIRECT_INPLACE;
         fb[j] = FB_INPLACE;
@@ -2656,9 +2675,13 @@ struct NullLds {
     uint32_t scan_tmp[NTN / 64];
 };
 
+// Dictionaries of at most dlds bytes (dynamic LDS sized by the host to the batch's largest fitting
+// dictionary, <= NULL_DICT_LDS; 0 when the batch has none) are staged in LDS and gathered from there
+// (north_star K3: "dictionary staged in LDS when it fits"); larger ones are gathered from L2 / HBM.
 __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                                   const int2* __restrict__ blocks, DevChunkResult* res) {
+                                                   const int2* __restrict__ blocks, DevChunkResult* res, uint32_t dlds) {
     __shared__ __attribute__((aligned(16))) NullLds S;
+    extern __shared__ __attribute__((aligned(16))) uint64_t DL[];
     const int2 pbk = blocks[blockIdx.x];
     if (pbk.x < 0) return;   // padding of the XCD-grouped block list (runtime)
     const int pi = pbk.x;
@@ -2723,6 +2746,13 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     const uint32_t doff = stage_bytes(S.dst, s.def, s.def_n, d0, d1);
     const uint32_t ioff = dict ? stage_bytes(S.ist, ids, ids_n, i0, i1) : 0u;
     for (uint32_t i = tid; i < FBLK / 32 + 2; i += NTN) S.vbits[i] = 0;
+    const bool dl = dict && dlds != 0 && ck.dict_n > 0 && uint64_t(ck.dict_n) * uint64_t(w) <= dlds &&
+                    (reinterpret_cast<uintptr_t>(ck.dict_data) & 7u) == 0;
+    if (dl) {   // the dictionary into LDS (8-byte loads; the page body is 16-byte aligned scratch)
+        const uint64_t* g = reinterpret_cast<const uint64_t*>(ck.dict_data);
+        const uint32_t nw = uint32_t((uint64_t(ck.dict_n) * uint64_t(w) + 7u) / 8u);
+        for (uint32_t i = tid; i < nw; i += NTN) DL[i] = g[i];
+    }
     __syncthreads();
     const uint8_t* dst8 = reinterpret_cast<const uint8_t*>(S.dst);
     const uint8_t* ist8 = reinterpret_cast<const uint8_t*>(S.ist);
@@ -2770,22 +2800,44 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     if (fv && !bad) {
         if (dict) {
             int vr = run_find(S.vrun, int(vnr), gv0);
+            const Run V0 = S.vrun[vr];
+            // the thread's present values are gv0, gv0 + 1, ...: when one id run holds them all, their
+            // ids are consecutive fields of that run (no run search per value)
+            const bool one_run = gv0 + uint32_t(__popc(fv)) <= V0.first + V0.count;
+            const uint32_t b0 = V0.packed ? uint32_t(uint64_t(V0.data) + uint64_t(gv0 - V0.first) * id_bw - ibase) : 0u;
+            uint32_t r = 0;
             #pragma unroll
             for (int k = 0; k < NEPT; k++) {
                 if (!((fv >> k) & 1u)) continue;
-                const uint32_t gv = gv0 + __popc(fv & ((1u << k) - 1u));
-                while (vr + 1 < int(vnr) && gv >= S.vrun[vr].first + S.vrun[vr].count) vr++;
-                const Run& V = S.vrun[vr];
-                uint32_t id = V.data;
-                if (V.packed) {
-                    const uint32_t b = uint32_t(uint64_t(V.data) + uint64_t(gv - V.first) * id_bw - ibase);
-                    bad |= b + id_bw > ilim;
-                    id = b + id_bw <= ilim ? lds_bits(ist8, b, id_bw) : 0u;
+                uint32_t id;
+                if (one_run) {
+                    id = V0.data;
+                    if (V0.packed) {
+                        const uint32_t b = b0 + r * id_bw;
+                        bad |= b + id_bw > ilim;
+                        id = b + id_bw <= ilim ? lds_bits(ist8, b, id_bw) : 0u;
+                    }
+                } else {
+                    const uint32_t gv = gv0 + r;
+                    while (vr + 1 < int(vnr) && gv >= S.vrun[vr].first + S.vrun[vr].count) vr++;
+                    const Run& V = S.vrun[vr];
+                    id = V.data;
+                    if (V.packed) {
+                        const uint32_t b = uint32_t(uint64_t(V.data) + uint64_t(gv - V.first) * id_bw - ibase);
+                        bad |= b + id_bw > ilim;
+                        id = b + id_bw <= ilim ? lds_bits(ist8, b, id_bw) : 0u;
+                    }
                 }
+                r++;
                 bad |= int64_t(id) >= ck.dict_n;
-                const uint8_t* src = ck.dict_data + uint64_t(int64_t(id) < ck.dict_n ? id : 0u) * uint64_t(w);
-                if (w == 4) v[k] = ld_u32_any(src);
-                else v[k] = ld_u64_any(src);
+                const uint32_t idc = int64_t(id) < ck.dict_n ? id : 0u;
+                if (dl) {
+                    v[k] = w == 4 ? uint64_t(reinterpret_cast<const uint32_t*>(DL)[idc]) : DL[idc];
+                } else {
+                    const uint8_t* src = ck.dict_data + uint64_t(idc) * uint64_t(w);
+                    if (w == 4) v[k] = ld_u32_any(src);
+                    else v[k] = ld_u64_any(src);
+                }
             }
         } else {
             #pragma unroll
@@ -3423,32 +3475,47 @@ extern "C" int pf_debug_walk_runs(const uint8_t* stream, uint64_t n, int bw, uin
 
 // Dictionary pages that are one Snappy literal (k_snappy_head: FB_LITCOPY): the literal's bytes to
 // the page's 16-byte aligned scratch body, 16 bytes per thread per step (aligned dword loads +
-// v_alignbyte), LC_SPLIT workgroups per page.
+// v_alignbyte), LC_SPLIT workgroups per page. The job's literals (k_snappy_head's table in its token
+// bitmap: {data offset, output offset} per literal) are found by a binary search per 16-byte chunk;
+// a chunk spanning two literals is copied byte by byte.
 constexpr int LC_SPLIT = 16;
 __global__ __launch_bounds__(NT) void k_snappy_litcopy(const SnappyJob* __restrict__ jobs, const int* __restrict__ list,
                                                        const int* __restrict__ fb) {
+    __shared__ uint32_t tab[2 * LC_MAX];
     const int j = list[blockIdx.x];
     if (fb[j] != FB_LITCOPY) return;
     const SnappyJob& J = jobs[j];
-    const uintptr_t sa = reinterpret_cast<uintptr_t>(J.src) + J.lit;
-    const uint32_t sh = uint32_t(sa & 3u);
-    const PF_GLOBAL uint32_t* q = (const PF_GLOBAL uint32_t*)(sa & ~uintptr_t(3));
-    const uintptr_t send = reinterpret_cast<uintptr_t>(J.src) + J.src_len;   // aligned dwords below it are readable
+    const uint32_t cnt = J.lit;
+    if (threadIdx.x < 2 * cnt) tab[threadIdx.x] = J.tokmap[threadIdx.x];
+    __syncthreads();
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(J.src);
+    const uintptr_t send = s0 + J.src_len;   // aligned dwords below it are readable
     PF_GLOBAL uint8_t* d = gptr(J.dst);
     const uint32_t n = J.dst_len;
     for (uint32_t c = (blockIdx.y * NT + threadIdx.x) * 16u; c < n; c += LC_SPLIT * NT * 16u) {
-        uint32_t w[5];
-        #pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const uintptr_t a = (sa & ~uintptr_t(3)) + c + 4u * uint32_t(k);
-            w[k] = a < send ? q[c / 4u + uint32_t(k)] : 0u;
+        uint32_t lo = 0, hi = cnt;   // last literal whose output starts at or before c
+        while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (tab[2 * m + 1] <= c) lo = m; else hi = m;
         }
-        const u32x4 v = {__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
-                         __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh)};
-        if (c + 16u <= n) {
+        const uint32_t oend = lo + 1 < cnt ? tab[2 * lo + 3] : n;
+        if (c + 16u <= oend) {
+            const uintptr_t sa = s0 + tab[2 * lo] + (c - tab[2 * lo + 1]);
+            const uint32_t sh = uint32_t(sa & 3u);
+            const PF_GLOBAL uint32_t* q = (const PF_GLOBAL uint32_t*)(sa & ~uintptr_t(3));
+            uint32_t w[5];
+            #pragma unroll
+            for (int k = 0; k < 5; k++) w[k] = (sa & ~uintptr_t(3)) + 4u * uint32_t(k) < send ? q[k] : 0u;
+            const u32x4 v = {__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
+                             __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh)};
             *(PF_GLOBAL u32x4*)(d + c) = v;
-        } else {
-            for (uint32_t k = 0; c + k < n; k++) d[c + k] = uint8_t(v[k >> 2] >> (8 * (k & 3)));
+        } else {   // the chunk ends the page or spans literals
+            const PF_GLOBAL uint8_t* g = (const PF_GLOBAL uint8_t*)(J.src);
+            uint32_t k = lo;
+            for (uint32_t b = c; b < c + 16u && b < n; b++) {
+                while (k + 1 < cnt && tab[2 * k + 3] <= b) k++;
+                d[b] = g[tab[2 * k] + (b - tab[2 * k + 1])];
+            }
         }
     }
 }
@@ -3474,11 +3541,13 @@ void launch_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, i
     if (n > 0) hipLaunchKernelGGL(k_lvl, dim3(n), dim3(LT_NT), 0, st, d_chunks, d_pages, d_list, d_res);
 }
 void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
-                 hipStream_t st, bool nullable) {   // d_list: n (page, block) pairs
+                 hipStream_t st, bool nullable, uint32_t null_dict_lds) {   // d_list: n (page, block) pairs
     if (n <= 0) return;
     const int2* blocks = reinterpret_cast<const int2*>(d_list);
     // pages with nulls first (k_flat_null marks them DONE_NULL), then every other page in one launch
-    if (nullable) hipLaunchKernelGGL(k_flat_null, dim3(n), dim3(NTN), 0, st, d_chunks, d_pages, blocks, d_res);
+    static const bool no_dl = [] { const char* e = std::getenv("PF_NULL_DICT_LDS"); return e && e[0] == '0'; }();
+    const uint32_t dl = no_dl ? 0u : null_dict_lds;
+    if (nullable) hipLaunchKernelGGL(k_flat_null, dim3(n), dim3(NTN), dl, st, d_chunks, d_pages, blocks, d_res, dl);
     static const bool split = [] { const char* e = std::getenv("PF_FLAT_SPLIT"); return e && e[0] == '1'; }();
     if (split) {   // A/B: the two kernels in stream order
         hipLaunchKernelGGL(k_flat_fixed, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);

@@ -36,7 +36,7 @@ void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hi
 void launch_dba_chars(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, BaJob*, hipStream_t);
 void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
-void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool);
+void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool, uint32_t);
 void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
@@ -142,6 +142,7 @@ struct pf_ctx {
     std::vector<BaJob> bajobs;             // PLAIN BYTE_ARRAY walks: dictionary pages, then data pages
     std::vector<int2> ba_tiles;            // (job relative to its batch, tile)
     int n_ba_dict = 0, n_ba_dict_tiles = 0;
+    uint32_t null_dict_lds = 0;   // bytes of the largest nullable-page dictionary that fits k_flat_null's LDS stage
     uint32_t n_splits = 0;
     SnapWin* d_win = nullptr;              // in d_tokmap: bitmap | lane outs | windows | entry tables
     SnapEnt* d_ent = nullptr;
@@ -267,7 +268,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
     EVREC(ctx, ctx->ev[8], st);
-    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty());
+    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty(), ctx->null_dict_lds);
     EVREC(ctx, ctx->ev[9], st);
     launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), ctx->n_decode_first, d_res, st);
     launch_nest_decode(d_chunks, d_pages, d_nseg, n_nseg, d_res, st);
@@ -896,6 +897,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->pages.clear(); ctx->jobs.clear();
     ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_flat.clear(); ctx->l_decode.clear();
     ctx->l_runs.clear(); ctx->l_dlen.clear(); ctx->l_dba.clear(); ctx->l_lvl.clear(); ctx->l_djobs.clear();
+    ctx->null_dict_lds = 0;
     ctx->l_nest.clear(); ctx->l_nseg.clear();
     // nested pages: entries per segment (k_nest_*); PF_NEST_SEG=n (tests) sets it and sends every
     // eligible nested page, one segment or more, down the segment path (0: none)
@@ -1142,6 +1144,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                 pg.lvltab = reinterpret_cast<uint32_t*>(S + pp.lt_off);
                 pg.lvl_cap = lvl_table_cap(pg.num_values);
                 ctx->l_lvl.push_back(int(i));
+                const DevChunk& lc = ctx->chunks[size_t(pg.chunk)];
+                const uint64_t db = uint64_t(std::max<int64_t>(lc.dict_n, 0)) * uint64_t(std::max(lc.width, 0));
+                if (lc.dict_page >= 0 && db > 0 && db <= NULL_DICT_LDS)
+                    ctx->null_dict_lds = std::max(ctx->null_dict_lds, uint32_t(align_up(db, 256)));
             }
             if (pp.dbp_off != ~0ull) {
                 pg.dbp = S + pp.dbp_off;
@@ -1273,8 +1279,15 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         }
     }
     mark();
-    for (size_t j = 0; j < ctx->jobs.size(); j++)   // dictionary pages: k_snappy_litcopy candidates
-        if (ctx->pages[size_t(ctx->jobs[j].page)].flags & PG_DICT) ctx->l_djobs.push_back(int(j));
+    // k_snappy_litcopy candidates (k_snappy_head decides): dictionary pages, and data pages that did
+    // not compress (a stream of literals only; one literal is read in place instead)
+    for (size_t j = 0; j < ctx->jobs.size(); j++) {
+        SnappyJob& jb = ctx->jobs[j];
+        if ((ctx->pages[size_t(jb.page)].flags & PG_DICT) || jb.src_len >= jb.dst_len) {
+            jb.dflags |= 2u;
+            ctx->l_djobs.push_back(int(j));
+        }
+    }
     // ---- Snappy tables: 8 KiB index windows, 64 KiB pieces ----
     {
         int rc = plan_snappy(ctx);

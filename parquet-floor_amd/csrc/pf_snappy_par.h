@@ -19,9 +19,10 @@ constexpr uint32_t SNAP_INVALID = 0xffffffffu;
 constexpr uint32_t SNAP_BLOCK = 65536;            // Google Snappy block = executor piece
 
 // per-job decode path (SnappyJob fallback flags, ordered: atomicMax escalates)
-// FB_INPLACE: the page needs no decompression (one literal, k_snappy_head); FB_LITCOPY: a dictionary
-// page that is one literal, copied to its scratch body by k_snappy_litcopy. Every parse / executor
-// kernel skips both.
+// FB_INPLACE: the page needs no decompression (one literal, k_snappy_head); FB_LITCOPY: a page whose
+// stream is at most LC_MAX literals and nothing else, copied to its scratch body by k_snappy_litcopy.
+// Every parse / executor kernel skips both.
+constexpr uint32_t LC_MAX = 32;   // literals of a FB_LITCOPY job (its table lives in its token bitmap)
 enum : int { FB_OK = 0, FB_WHOLE = 1, FB_REDO = 2, FB_SERIAL = 3, FB_INPLACE = 4, FB_LITCOPY = 5 };
 // SnapWin.flags
 enum : uint32_t { WIN_BROKEN = 1, WIN_PASS = 2, WIN_NOCONV = 4 };

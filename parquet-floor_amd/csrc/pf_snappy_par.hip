@@ -1400,327 +1400,6 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
     for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) put1(od, a, ring[a & XRMASK]);
 }
 
-// ======================================================================== executor v3 (round 4)
-//
-// k_snappy_exec2's byte-lane resolution, but a piece is decoded by a 256-thread workgroup (4 waves)
-// instead of one wave: a batch is up to 256 tokens (one per thread; exec2 takes 64) and <= X3_B
-// output bytes, its bytes resolved by all 256 threads at once (8 per thread), and dependent copies
-// by pointer jumping over the whole batch (in place: a word is a value or the batch position of a
-// byte produced earlier in the batch; reading a word another thread has just advanced only jumps
-// further along the same chain). A dense 64 KiB piece (sorted / small-delta integers, ~12 k
-// tokens) is then ~50 batches of a few barriers each instead of ~190 single-wave steps: the
-// executor stage is set by the dense pieces' latency, which this divides by the
-// waves per piece. Far copies (source more than X3_RING - X3_B bytes back) read the flushed
-// output from HBM into per-wave LDS slots, after every wave's flush stores have landed.
-constexpr int X3_NT = 256;
-constexpr uint32_t X3_RING = 8192;                  // output ring (LDS)
-constexpr uint32_t X3_RMASK = X3_RING - 1;
-constexpr uint32_t X3_CH = 2048;                    // input bytes whose tokens are enumerated at once (8 per thread)
-constexpr uint32_t X3_STAGEB = X3_CH + 64 + 16;     // staged input: + lookahead (token tails, literal data) + alignment
-constexpr uint32_t X3_B = 2048;                     // output bytes of one batch (8 per thread)
-constexpr uint32_t X3_SLOT = 4096;                  // flush granule (16 bytes per thread)
-constexpr uint32_t X3_FARW = 8;                     // far copies per wave and batch
-constexpr uint32_t X3_LIT = 2048;                   // long literals are copied from HBM in pieces of this many bytes
-constexpr uint32_t X3_STAGE_OFF = X3_RING;
-constexpr uint32_t X3_FBUF_OFF = X3_RING + ((X3_STAGEB + 15u) & ~15u);
-constexpr uint32_t X3_LDS = X3_FBUF_OFF + 4u * X3_FARW * FBUF_W * 4u;
-static_assert(X3_B + X3_SLOT <= X3_RING, "ring: batch + unflushed bytes");
-static_assert(X3_LIT + X3_SLOT <= X3_RING, "ring: literal piece + unflushed bytes");
-static_assert(X3_B / 32 == 64, "one sbits word per lane of wave 0");
-static_assert(X3_STAGEB <= 16u * X3_NT, "one 16-byte stage load per thread");
-
-__global__ __launch_bounds__(X3_NT) void k_snappy_exec3(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
-                                                       const uint32_t* __restrict__ splits, int* __restrict__ fb) {
-    __shared__ __attribute__((aligned(16))) uint8_t L[X3_LDS];
-    __shared__ uint16_t tokpos[X3_CH / 2];      // a token is >= 2 input bytes
-    __shared__ uint2 desc[X3_NT];               // per batch token: {rel | flags | offset << 16, source}
-    __shared__ uint2 sw[X3_B / 32];             // per 32 output bytes: {token-start bits, tokens starting in earlier words}
-    __shared__ uint16_t jv[X3_B];               // pointer-jumping words of the batch
-    __shared__ uint32_t red[4][4];              // per wave: {ol total, last token end, first cut lane, flags | take count << 8}
-    __shared__ uint32_t bc[4];                  // broadcast: {btot | literal length, next ip, literal source, kind}
-    uint8_t* const ring = L;
-    uint8_t* const stage = L + X3_STAGE_OFF;
-    uint32_t* const fbuf = reinterpret_cast<uint32_t*>(L + X3_FBUF_OFF);
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int2 pc = pieces[blockIdx.x];
-    const int j = pc.x;
-    const uint32_t k = uint32_t(pc.y);
-    if (tid == 0) bc[0] = uint32_t(fb[j]);   // (another piece of the job may raise it meanwhile: read once)
-    if (tid < int(X3_B / 32)) sw[tid] = uint2{0u, 0u};
-    __syncthreads();
-    const int f = int(bc[0]);
-    if (f >= FB_REDO || (f == FB_WHOLE && k > 0)) return;
-    const bool whole = f == FB_WHOLE;
-    const SnappyJob job = jobs[j];
-    const uint8_t* in = job.src;
-    const uint64_t n = job.src_len;
-    const uint32_t* sp = splits + job.split_base;
-    uint64_t pos0 = 0, ulen = 0;
-    if (!uvarint(in, n, pos0, ulen) || ulen != job.dst_len) {
-        if (tid == 0) atomicMax(&fb[j], FB_SERIAL);
-        return;
-    }
-    if (job.dflags & 1u) {   // diagnostics: forced redo
-        if (tid == 0) atomicMax(&fb[j], FB_REDO);
-        return;
-    }
-    uint32_t ip, out_start, out_end = job.dst_len;
-    if (whole) {
-        ip = uint32_t(pos0);
-        out_start = 0;
-    } else {
-        if (k > 0 && sp[k] == SNAP_INVALID) return;   // no token at this boundary: an earlier piece covers it
-        ip = k == 0 ? uint32_t(pos0) : sp[k];
-        out_start = k * SNAP_BLOCK;
-        for (uint32_t k2 = k + 1; k2 < job.n_pieces; k2++)
-            if (sp[k2] != SNAP_INVALID) { out_end = k2 * SNAP_BLOCK; break; }
-    }
-    const PF_GLOBAL uint8_t* tm8 = (const PF_GLOBAL uint8_t*)(job.tokmap);
-    const PF_GLOBAL uint8_t* gin = gptr(in);
-    PF_GLOBAL uint8_t* gdst = gptr(job.dst);
-    const OutDst od{gdst, gptr(job.ddst), job.dlo, job.dgran};
-    uint32_t op = out_start, F = out_start;
-    bool bad = false;
-    while (op < out_end) {
-        if (ip >= n) { bad = true; break; }
-        const uint32_t I = ip & ~15u;
-        __syncthreads();   // the previous chunk's stage / token list readers are done
-        uint32_t woff;
-        {   // stage stream bytes [I - woff, I - woff + X3_STAGEB): one 16-byte load per thread
-            const uintptr_t ga = reinterpret_cast<uintptr_t>(in + I);
-            woff = uint32_t(ga & 15u);
-            if (tid < int(X3_STAGEB / 16)) {
-                const int64_t p = int64_t(I) - int64_t(woff) + 16 * int64_t(tid);
-                u32x4 v4 = {0u, 0u, 0u, 0u};
-                if (p < int64_t(n)) v4 = reinterpret_cast<const PF_GLOBAL u32x4*>(ga - woff)[tid];
-                reinterpret_cast<u32x4*>(stage)[tid] = v4;
-            }
-        }
-        // token starts in [ip, I + X3_CH): 8 input bytes per thread
-        const uint32_t p8 = I + 8u * uint32_t(tid);
-        uint32_t bits = uint64_t(p8) < n ? uint32_t(tm8[p8 >> 3]) : 0u;
-        if (p8 + 8u <= ip) bits = 0;
-        else if (p8 < ip) bits &= ~((1u << (ip - p8)) - 1u);
-        const uint32_t cnt = __popc(bits);
-        const uint32_t wi = dpp_incl_scan(cnt);
-        if (lane == 63) red[wv][0] = wi;
-        __syncthreads();
-        uint32_t q = wi - cnt, T = 0;
-        #pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const uint32_t c = red[w][0];
-            q += w < wv ? c : 0u;
-            T += c;
-        }
-        while (bits) {
-            const uint32_t b = uint32_t(__ffs(bits) - 1);
-            bits &= bits - 1;
-            tokpos[q++] = uint16_t(8u * uint32_t(tid) + b);
-        }
-        __syncthreads();   // token list and stage complete; red reusable
-        if (T == 0) { bad = true; break; }
-        uint32_t sb = 0;
-        while (sb < T && op < out_end) {
-            const uint32_t t = sb + uint32_t(tid);
-            const bool v = t < T;
-            const uint32_t pos = v ? uint32_t(tokpos[t]) : 0u;
-            const SnapTok tk = snap_tok(lds_read8(stage, woff + pos));
-            const uint32_t ol = v ? tk.ol : 0u;
-            const uint32_t olc = min(ol, 1u << 24);   // (a longer token fails the out_end test; keeps the sums in 32 bits)
-            const uint32_t start = I + pos;
-            const uint32_t endp = tk.tl > uint64_t(0xffffffffu - start) ? 0xffffffffu : start + uint32_t(tk.tl);
-            uint32_t prev = dpp_prev(endp);
-            const uint32_t winc = dpp_incl_scan(olc);
-            if (lane == 63) { red[wv][0] = winc; red[wv][1] = endp; }
-            __syncthreads();   // A
-            uint32_t pre = 0;
-            #pragma unroll
-            for (int w = 0; w < 4; w++) pre += w < wv ? red[w][0] : 0u;
-            if (lane == 0 && wv > 0) prev = red[wv - 1][1];
-            const uint32_t inc = pre + winc;
-            const uint32_t otok = op + inc - olc;
-            const bool take = v && otok < out_end;
-            const uint32_t kd = tk.kind, off = tk.arg;
-            const uint32_t srcv = start + tk.arg;   // literal data position
-            const bool wrong = take && ((t == sb ? start != ip : start != prev) || endp > n || inc > out_end - op ||
-                                        (kd != 0 && (off == 0 || off > otok - out_start)));
-            const bool lstaged = uint64_t(srcv) + ol <= uint64_t(I) + X3_CH + 64u;
-            const uint32_t a = otok - off;          // copy source start
-            const bool farc = take && kd != 0 && a + min(ol, off) <= op && int32_t(a - (op + X3_B - X3_RING)) < 0;
-            const unsigned long long farm = __ballot(farc);
-            const uint32_t frank = uint32_t(__popcll(farm & lane_mask_lt(uint32_t(lane))));
-            const unsigned long long cutm = __ballot(take && (inc > X3_B || (kd == 0 && !lstaged) || (farc && frank >= X3_FARW)));
-            const unsigned long long takem = __ballot(take);
-            const bool wwrong = __any(wrong);
-            if (lane == 0) {
-                red[wv][2] = cutm ? uint32_t(__ffsll(cutm) - 1) : 64u;
-                red[wv][3] = (wwrong ? 1u : 0u) | (farm ? 2u : 0u) | (uint32_t(__popcll(takem)) << 8);
-            }
-            __syncthreads();   // B
-            uint32_t cut = X3_NT, nt = 0;
-            bool bw = false, anyfar = false;
-            #pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const uint32_t c = red[w][2], fl = red[w][3];
-                if (c < 64u && cut == uint32_t(X3_NT)) cut = 64u * uint32_t(w) + c;
-                bw |= (fl & 1u) != 0;
-                anyfar |= (fl & 2u) != 0;
-                nt += fl >> 8;
-            }
-            if (bw) { bad = true; break; }
-            if (nt == 0) break;   // the previous batch ended exactly at out_end
-            cut = min(cut, nt);
-            if (cut == 0) {
-                // one long literal (or one not staged), from HBM; copies are <= 64 bytes, so only a literal gets here
-                if (tid == 0) { bc[0] = ol; bc[1] = endp; bc[2] = srcv; bc[3] = kd; }
-                __syncthreads();   // C
-                const uint32_t L0 = bc[0], s0 = bc[2];
-                if (bc[3] != 0u) { bad = true; break; }
-                for (uint32_t d0 = 0; d0 < L0; d0 += X3_LIT) {
-                    const uint32_t c = min(L0 - d0, X3_LIT);
-                    const uint32_t b0 = 8u * uint32_t(tid);
-                    if (b0 < c) {
-                        uint8_t by[8];
-                        #pragma unroll
-                        for (int u = 0; u < 8; u++) by[u] = b0 + u < c ? gin[s0 + d0 + b0 + u] : uint8_t(0);
-                        #pragma unroll
-                        for (int u = 0; u < 8; u++)
-                            if (b0 + u < c) ring[(op + d0 + b0 + u) & X3_RMASK] = by[u];
-                    }
-                    __syncthreads();   // ring bytes complete before the flush reads them
-                    while (op + d0 + c - F >= X3_SLOT) {
-                        const uint32_t a0 = F + 16u * uint32_t(tid);
-                        put16(od, a0, *reinterpret_cast<const u32x4*>(ring + (a0 & X3_RMASK)));
-                        F += X3_SLOT;
-                    }
-                    __syncthreads();   // flush reads done before the next piece overwrites ring slots
-                }
-                op += L0;
-                ip = bc[1];
-                sb += 1;
-                continue;
-            }
-            const bool inb = take && uint32_t(tid) < cut;
-            const bool cp = inb && kd != 0;
-            const bool far = cp && farc;
-            const uint32_t rel = otok - op;
-            if (uint32_t(tid) == cut - 1u) { bc[0] = inc; bc[1] = endp; }
-            // a far source straddling the direct split (level bytes | values) is not one window
-            const bool fbad = od.dd != nullptr && far && a < od.dlo && a + ol > od.dlo;
-            if (inb) {
-                const bool near = cp && !far;
-                const uint32_t d0 = rel | (near ? (1u << 12) : 0u) | ((near && off < ol) ? (1u << 13) : 0u) |
-                                    (min(off, 0xffffu) << 16);
-                const uint32_t fsh = od.dd != nullptr && a >= od.dlo ? uint32_t((reinterpret_cast<uintptr_t>(od.dd) + a) & 3u)
-                                                                      : (a & 3u);
-                const uint32_t slot = uint32_t(wv) * X3_FARW + frank;
-                const uint32_t d1 = kd == 0 ? X3_STAGE_OFF + woff + (srcv - I)
-                                            : (far ? X3_FBUF_OFF + slot * (FBUF_W * 4u) + fsh : a);
-                desc[tid] = uint2{d0, d1};
-                atomicOr(&sw[rel >> 5].x, 1u << (rel & 31u));
-            }
-            if (anyfar) wait_vmem();   // every thread's flush stores have landed before the barrier
-            if (__syncthreads_or(fbad)) { bad = true; break; }   // C
-            const uint32_t btot = bc[0];
-            const uint32_t ipn = bc[1];
-            if (far) {   // the copy's source (flushed output) into its LDS slot
-                const PF_GLOBAL uint8_t* fb0 = od.dd != nullptr && a >= od.dlo ? od.dd + a : gdst + a;
-                const uintptr_t fa = reinterpret_cast<uintptr_t>(fb0);
-                const PF_GLOBAL uint32_t* fsrc = (const PF_GLOBAL uint32_t*)(fa & ~uintptr_t(3));
-                const uint32_t nwd = (uint32_t(fa & 3u) + ol + 3u) >> 2;
-                uint32_t fw[FBUF_W];
-                #pragma unroll
-                for (int u = 0; u < int(FBUF_W); u++) fw[u] = uint32_t(u) < nwd ? fsrc[u] : 0u;
-                uint32_t* fl = fbuf + (uint32_t(wv) * X3_FARW + frank) * FBUF_W;
-                #pragma unroll
-                for (int u = 0; u < int(FBUF_W); u++)
-                    if (uint32_t(u) < nwd) fl[u] = fw[u];
-            }
-            if (wv == 0) {   // tokens starting in earlier words of the batch
-                const uint32_t c = __popc(sw[lane].x);
-                sw[lane].y = dpp_incl_scan(c) - c;
-            }
-            __syncthreads();   // D
-            // bytes x = 1024 u + 4 tid + kk of the batch: a value (< 0x100) or 0x8000 | batch position
-            uint32_t W[8];
-            #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const uint32_t x0 = 1024u * uint32_t(u) + 4u * uint32_t(tid);
-                const uint2 s = sw[(x0 >> 5) & 63u];
-                const uint32_t sh = x0 & 31u;
-                uint32_t addr[4];
-                bool pend[4];
-                #pragma unroll
-                for (int kk = 0; kk < 4; kk++) {
-                    const uint32_t x = x0 + uint32_t(kk);
-                    const bool act = x < btot;
-                    const uint32_t ti = min(s.y + __popc(s.x & ((2u << (sh + uint32_t(kk))) - 1u)), 256u) - 1u;
-                    const uint2 d = desc[act ? ti : 0u];
-                    const uint32_t jj = x - (d.x & 0x7ffu);
-                    const bool near = (d.x >> 12) & 1u;
-                    const uint32_t offv = max(d.x >> 16, 1u);
-                    const uint32_t r = ((d.x >> 13) & 1u) ? mod_small(jj & 63u, offv) : jj;
-                    const uint32_t y = d.y + r;   // near copy: absolute output position of the source byte
-                    pend[kk] = act && near && y >= op;
-                    addr[kk] = near ? (y & X3_RMASK) : (d.y + jj);
-                    W[4 * u + kk] = 0x8000u | ((y - op) & 0x7ffu);
-                    if (!act) { pend[kk] = false; addr[kk] = 0; }
-                }
-                #pragma unroll
-                for (int kk = 0; kk < 4; kk++) {
-                    const uint32_t val = uint32_t(L[addr[kk]]);
-                    W[4 * u + kk] = pend[kk] ? W[4 * u + kk] : val;
-                }
-            }
-            // pointer jumping over the batch (a source always precedes its reader)
-            while (true) {
-                bool mp = false;
-                #pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    #pragma unroll
-                    for (int kk = 0; kk < 4; kk++) {
-                        const uint32_t x = 1024u * uint32_t(u) + 4u * uint32_t(tid) + uint32_t(kk);
-                        if (x < btot) jv[x] = uint16_t(W[4 * u + kk]);
-                        mp |= (W[4 * u + kk] & 0x8000u) != 0u;
-                    }
-                }
-                if (!__syncthreads_or(mp)) break;
-                #pragma unroll
-                for (int i = 0; i < 8; i++)
-                    if (W[i] & 0x8000u) W[i] = jv[W[i] & 0x7ffu];
-            }
-            #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                #pragma unroll
-                for (int kk = 0; kk < 4; kk++) {
-                    const uint32_t x = 1024u * uint32_t(u) + 4u * uint32_t(tid) + uint32_t(kk);
-                    if (x < btot) ring[(op + x) & X3_RMASK] = uint8_t(W[4 * u + kk]);
-                }
-            }
-            __syncthreads();   // E: ring bytes complete
-            if (tid < int(X3_B / 32)) sw[tid].x = 0u;
-            while (op + btot - F >= X3_SLOT) {
-                const uint32_t a0 = F + 16u * uint32_t(tid);
-                put16(od, a0, *reinterpret_cast<const u32x4*>(ring + (a0 & X3_RMASK)));
-                F += X3_SLOT;
-            }
-            op += btot;
-            ip = ipn;
-            sb += cut;
-        }
-        if (bad) break;
-    }
-    if (bad) {
-        if (tid == 0) atomicMax(&fb[j], whole ? FB_SERIAL : FB_REDO);
-        return;
-    }
-    __syncthreads();
-    // tail: bytes [F, op)
-    for (uint32_t a = F + 16u * uint32_t(tid); a + 16u <= op; a += 16u * X3_NT)
-        put16(od, a, *reinterpret_cast<const u32x4*>(ring + (a & X3_RMASK)));
-    for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(tid); a < op; a += X3_NT) put1(od, a, ring[a & X3_RMASK]);
-}
-
 #ifdef PF_STAMPS
 extern "C" int pf_debug_stamps(unsigned long long* out, int n, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_stamps), sizeof(unsigned long long) * (n < 16 ? n : 16)) != hipSuccess) return -1;
@@ -1753,12 +1432,7 @@ void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins
 void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
                         int* d_fb, DevChunkResult* d_res, hipStream_t s) {
     if (n_jobs <= 0) return;
-    // PF_EXEC=3: the 4-wave executor (k_snappy_exec3); default: the one-wave executor
-    static const int exec_v = [] { const char* e = std::getenv("PF_EXEC"); return e && e[0] == '3' ? 3 : 2; }();
-    if (exec_v == 3)
-        hipLaunchKernelGGL(k_snappy_exec3, dim3(n_pieces), dim3(X3_NT), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb);
-    else
-        hipLaunchKernelGGL(k_snappy_exec2, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
+    hipLaunchKernelGGL(k_snappy_exec2, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
     // whole-page redo of pages whose pieces were not independent
     hipLaunchKernelGGL(k_snappy_exec2, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
     launch_snappy_serial(d_jobs, n_jobs, d_fb, d_res, s);

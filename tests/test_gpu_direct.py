@@ -111,3 +111,39 @@ def test_direct_pages_through_the_redo_path(decoder, oracle, tmp_path, monkeypat
     d = _direct(decoder)
     redone = [rec[5 * j + 4] for j in range(nj) if rec[5 * j] == 2]
     assert any(d[p] == DIRECT_VALUES for p in redone)   # accepted as direct, then decoded from scratch
+
+
+# Streams of literals only (k_snappy_head -> k_snappy_litcopy, no parse / executor): Snappy emits one
+# literal per 64 KiB block of incompressible input, so a 400 KB dictionary of random values is ~7
+# literals and a 160 KB data page of random doubles 3. Dictionary pages and data pages that did not
+# compress are copied from the literal table; the result must equal the oracle's decode.
+FB_LITCOPY = 5
+
+
+@pytest.mark.parametrize("version", ["1.0", "2.0"])
+def test_multi_literal_pages(decoder, oracle, tmp_path, version):
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from pfloor import _native
+    from pfloor.decoder import decode_file
+    rng = np.random.default_rng(23)
+    n = 120_000
+    pool = rng.integers(-2**31, 2**31, 100_000, dtype=np.int64).astype(np.int32)   # 400 KB dictionary
+    t = pa.table({
+        "dict_i32": pa.array(pool[rng.integers(0, len(pool), n)], mask=rng.random(n) < 0.3),
+        "rnd_f64": pa.array(rng.random(n)),                                          # PLAIN, incompressible
+        "rnd_nul": pa.array(rng.random(n), mask=rng.random(n) < 0.2),
+    })
+    path = str(tmp_path / f"lits_{version}.parquet")
+    pq.write_table(t, path, compression="snappy", data_page_version=version, row_group_size=n,
+                   use_dictionary=["dict_i32"], data_page_size=1 << 20)
+    got = decode_file(path, decoder=decoder)
+    assert got["_status"] == 0, got["_error"]
+    assert _check(got, oracle, path, f"literals v{version}") == 3
+    L = _native.lib()
+    L.pf_debug_snappy_fallback.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
+    nj = L.pf_debug_snappy_fallback(decoder.h, None, 0)
+    rec = (C.c_int * (5 * nj))()
+    L.pf_debug_snappy_fallback(decoder.h, rec, nj)
+    lit = [rec[5 * j + 2] for j in range(nj) if rec[5 * j] == FB_LITCOPY]
+    assert any(d > 65536 for d in lit), [rec[5 * j:5 * j + 5] for j in range(nj)]   # multi-literal pages copied
