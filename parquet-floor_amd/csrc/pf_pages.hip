@@ -187,7 +187,9 @@ __device__ inline int64_t plain_binary_walk(const uint8_t* p, uint64_t n, int64_
 // candidate's successor, and it must chain exactly (q_next == q + 4 + len) from the entry. Any
 // mismatch — a false candidate that got linked, overflow, too few values — falls back to the exact
 // serial walk, so the result is always the chain parquet-mr's BinaryPlainValuesReader reads.
-constexpr int BW_BPT = 16;                          // positions per thread per tile
+constexpr int BW_BPT = 4;                           // positions per thread per tile (4: 5.5 KiB of LDS, so the
+                                                    // normally idle k_ba_fallback launch does not wait for
+                                                    // CUs with 21 KiB free while other streams run)
 constexpr int BW_TILE = NT * BW_BPT;                // bytes per tile
 constexpr int BW_LOOK = 64;                         // staged lookahead for successor tests
 constexpr int BW_STAGE = BW_TILE + BW_LOOK + 16;    // + alignment shift
@@ -612,17 +614,26 @@ __device__ __forceinline__ uint64_t* flat_block_chars(const DevPage& pg) {
 __device__ __forceinline__ bool is_dict_enc(int e) { return e == 2 || e == 8; }
 
 // ---- k_count ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                              const int* page_list, DevChunkResult* res, BaJob* bajobs) {
-    __shared__ LevelLds L;
-    __shared__ Piece pval[TILE];
-    __shared__ uint32_t ids[TILE];
-    __shared__ uint32_t scan_tmp[NT / 64];
-    __shared__ RleState sval;
-    __shared__ int npval, verr;
-    __shared__ unsigned long long chars_acc;
+struct CountLds {
+    LevelLds L;
+    Piece pval[TILE];
+    uint32_t ids[TILE];
+    uint32_t scan_tmp[NT / 64];
+    RleState sval;
+    int npval, verr;
+    unsigned long long chars_acc;
+};
 
-    const int pi = page_list[blockIdx.x];
+__device__ void count_page(const DevChunk* __restrict__ chunks, DevPage* pages, int pi, DevChunkResult* res, BaJob* bajobs,
+                           CountLds& C) {
+    LevelLds& L = C.L;
+    Piece* pval = C.pval;
+    uint32_t* ids = C.ids;
+    uint32_t* scan_tmp = C.scan_tmp;
+    RleState& sval = C.sval;
+    int& npval = C.npval;
+    int& verr = C.verr;
+    unsigned long long& chars_acc = C.chars_acc;
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     if (res[pg.chunk].status != 0) return;   // an earlier stage failed this chunk
@@ -715,6 +726,18 @@ __global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunk
         pg.n_values = int64_t(vals);
         pg.n_rows = int64_t(rows);
         pg.n_chars = int64_t(chars_acc);
+    }
+}
+
+// Grid-stride over the BYTE_ARRAY / nested pages with a small grid: nearly every page is counted by
+// k_count_flat or k_count_seg and skipped here, and a block per page (22 KiB of LDS each) waited for
+// CUs held by the other streams' kernels (13-96 us per no-op launch in the r04 kernel trace).
+__global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                              const int* page_list, int n, DevChunkResult* res, BaJob* bajobs) {
+    __shared__ CountLds C;
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        count_page(chunks, pages, page_list[i], res, bajobs, C);
+        __syncthreads();
     }
 }
 
@@ -1552,8 +1575,85 @@ __global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ 
     }
 }
 
+// One 16-byte output chunk at arena address c (tile chars start at a0, total bytes): chunks inside
+// one value are one 16-byte source read (aligned dwords + v_alignbyte); a chunk spanning values is
+// blended from one aligned window per value piece. v: a value at or before the chunk's first byte.
+__device__ inline void copy_chunk16(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
+                                    const uint8_t* sbase, const uint8_t* send, uintptr_t a0, uintptr_t c, uint32_t v) {
+    const int64_t r0 = int64_t(c) - int64_t(a0);
+    uint32_t vb = coff[v];
+    uint32_t vend = v + 1 < nv ? coff[v + 1] : total;
+    while (r0 >= 0 && uint32_t(r0) >= vend && v + 1 < nv) {   // zero-length values share a start
+        v++;
+        vb = coff[v];
+        vend = v + 1 < nv ? coff[v + 1] : total;
+    }
+    uint8_t* dst = reinterpret_cast<uint8_t*>(c);
+    if (r0 >= 0 && uint32_t(r0) >= vb && uint64_t(r0) + 16 <= vend) {
+        const uint8_t* sp = sbase + csrc[v] + (uint32_t(r0) - vb);
+        if (sp + 20 <= send) {
+            const uintptr_t sa = reinterpret_cast<uintptr_t>(sp);
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(sa & ~uintptr_t(3));
+            const uint32_t sh = uint32_t(sa & 3u);
+            uint32_t d[5];
+            #pragma unroll
+            for (int k = 0; k < 5; k++) d[k] = q[k];
+            uint4 o;
+            if (sh) {
+                o.x = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+                o.y = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+                o.z = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
+                o.w = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+            } else {
+                o = make_uint4(d[0], d[1], d[2], d[3]);
+            }
+            *reinterpret_cast<uint4*>(dst) = o;
+            return;
+        }
+    }
+    // the chunk spans values: one aligned 16-byte window per value piece, blended under a byte mask
+    // (dword loads that overlap the piece's source bytes only, so every load stays in the source)
+    uint32_t word[4] = {0, 0, 0, 0};
+    for (;;) {
+        const int64_t lo = max(max(r0, int64_t(vb)), int64_t(0)), hi = min(min(r0 + 16, int64_t(vend)), int64_t(total));
+        if (lo < hi) {
+            const uintptr_t need0 = reinterpret_cast<uintptr_t>(sbase) + csrc[v] + uint32_t(lo - vb);
+            const uintptr_t need1 = need0 + uintptr_t(hi - lo);            // source bytes [need0, need1)
+            const uintptr_t ws = need0 - uintptr_t(lo - r0);               // source of chunk byte 0
+            const uintptr_t wa = ws & ~uintptr_t(3);
+            const uint32_t sh = uint32_t(ws & 3u);
+            uint32_t d[5];
+            #pragma unroll
+            for (int k = 0; k < 5; k++) {
+                const uintptr_t da = wa + 4u * k;
+                d[k] = (da + 4 > need0 && da < need1) ? *reinterpret_cast<const uint32_t*>(da) : 0u;
+            }
+            const uint32_t bm = (0xffffu >> (16 - uint32_t(hi - r0))) & ~((1u << uint32_t(lo - r0)) - 1u);
+            #pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t w = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+                const uint32_t m = (((bm >> (4 * k)) & 0xfu) * 0x00204081u & 0x01010101u) * 0xffu;
+                word[k] = (word[k] & ~m) | (w & m);
+            }
+        }
+        if (int64_t(vend) >= r0 + 16 || v + 1 >= nv) break;
+        v++;
+        vb = coff[v];
+        vend = v + 1 < nv ? coff[v + 1] : total;
+    }
+    if (r0 >= 0 && r0 + 16 <= int64_t(total)) {
+        *reinterpret_cast<uint4*>(dst) = make_uint4(word[0], word[1], word[2], word[3]);
+    } else {
+        #pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int64_t r = r0 + k;
+            if (r >= 0 && r < int64_t(total)) dst[k] = uint8_t(word[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+}
+
 // copy_chars with a chunk -> value table (no per-chunk binary search) and 16-byte source reads
-// (aligned dwords + v_alignbyte) for chunks inside one value; other chunks byte by byte.
+// (aligned dwords + v_alignbyte) for chunks inside one value; other chunks blended per value piece.
 // cv: LDS table of CV_CAP u16; send: end of the readable source buffer.
 constexpr uint32_t CV_CAP = 4096;
 __device__ inline void copy_chars_fast(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
@@ -1572,79 +1672,97 @@ __device__ inline void copy_chars_fast(const uint32_t* coff, const uint32_t* csr
         for (uintptr_t c = (ab + 15) & ~uintptr_t(15); c < ae; c += 16) cv[(c - c0) >> 4] = uint16_t(v);
     }
     __syncthreads();
-    for (uint32_t ci = threadIdx.x; ci < nch; ci += blockDim.x) {
-        const uintptr_t c = c0 + uintptr_t(ci) * 16u;
+    for (uint32_t ci = threadIdx.x; ci < nch; ci += blockDim.x)
+        copy_chunk16(coff, csrc, nv, total, sbase, send, a0, c0 + uintptr_t(ci) * 16u, cv[ci]);
+}
+
+// PLAIN BYTE_ARRAY chars (round 4): the tile's values are consecutive in the page body, each after its
+// 4-byte length, so output byte r of value v comes from csrc[0] + r + 4 v: the chars are the source
+// range with a 4-byte hole before every value. A thread copies one 64-byte output span with ONE round
+// of source loads (the span's bytes plus 4 per value starting inside it: <= 21 aligned dwords), then
+// assembles each output dword from the two shifted source dwords around a hole (v_perm). copy_chars_fast
+// issued one dependent round of loads per 16-byte chunk, and its chunks spanning values (most of them
+// for ~27-byte comments) blended one value piece at a time. Spans at the tile's ends, and spans where
+// more than SP_K values start (or two holes fall in one dword), take copy_chunk16 per chunk.
+constexpr uint32_t SP_K = 4;
+__device__ __forceinline__ uint32_t sp_pick(const uint32_t* Z, int d, uint32_t h) {   // Z[d + h], h <= SP_K
+    uint32_t r = Z[d];
+    #pragma unroll
+    for (uint32_t k = 1; k <= SP_K; k++) r = h >= k ? Z[d + int(k)] : r;
+    return r;
+}
+__device__ inline void copy_chars_plain(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
+                                        const uint8_t* sbase, const uint8_t* send, uint8_t* obase, uint16_t* cv) {
+    if (total == 0 || nv == 0) return;
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(obase);
+    const uintptr_t s0 = a0 & ~uintptr_t(63);
+    const uint32_t nsp = uint32_t(((a0 + total + 63) & ~uintptr_t(63)) - s0) / 64u;
+    if (nsp > CV_CAP) { copy_chars(coff, csrc, nv, total, sbase, obase); return; }
+    // value v owns the spans whose first byte lies inside it
+    if (threadIdx.x == 0) cv[0] = 0;
+    for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {
+        const uint32_t b = coff[v], e = v + 1 < nv ? coff[v + 1] : total;
+        if (e <= b) continue;
+        const uintptr_t ab = a0 + b, ae = a0 + e;
+        for (uintptr_t c = (ab + 63) & ~uintptr_t(63); c < ae; c += 64) cv[(c - s0) >> 6] = uint16_t(v);
+    }
+    __syncthreads();
+    const uint32_t base0 = csrc[0] - coff[0];   // (coff[0] == 0)
+    for (uint32_t si = threadIdx.x; si < nsp; si += blockDim.x) {
+        const uintptr_t c = s0 + uintptr_t(si) * 64u;
         const int64_t r0 = int64_t(c) - int64_t(a0);
-        uint32_t v = cv[ci];
-        uint32_t vb = coff[v];
-        uint32_t vend = v + 1 < nv ? coff[v + 1] : total;
-        while (r0 >= 0 && uint32_t(r0) >= vend && v + 1 < nv) {   // zero-length values share a start
-            v++;
-            vb = coff[v];
-            vend = v + 1 < nv ? coff[v + 1] : total;
-        }
-        uint8_t* dst = reinterpret_cast<uint8_t*>(c);
-        if (r0 >= 0 && uint32_t(r0) >= vb && uint64_t(r0) + 16 <= vend) {
-            const uint8_t* sp = sbase + csrc[v] + (uint32_t(r0) - vb);
-            if (sp + 20 <= send) {
-                const uintptr_t sa = reinterpret_cast<uintptr_t>(sp);
-                const uint32_t* q = reinterpret_cast<const uint32_t*>(sa & ~uintptr_t(3));
-                const uint32_t sh = uint32_t(sa & 3u);
-                uint32_t d[5];
-                #pragma unroll
-                for (int k = 0; k < 5; k++) d[k] = q[k];
-                uint4 o;
-                if (sh) {
-                    o.x = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
-                    o.y = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
-                    o.z = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
-                    o.w = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
-                } else {
-                    o = make_uint4(d[0], d[1], d[2], d[3]);
-                }
-                *reinterpret_cast<uint4*>(dst) = o;
-                continue;
-            }
-        }
-        // the chunk spans values: one aligned 16-byte window per value piece, blended under a byte mask
-        // (dword loads that overlap the piece's source bytes only, so every load stays in the source)
-        uint32_t word[4] = {0, 0, 0, 0};
-        for (;;) {
-            const int64_t lo = max(max(r0, int64_t(vb)), int64_t(0)), hi = min(min(r0 + 16, int64_t(vend)), int64_t(total));
-            if (lo < hi) {
-                const uintptr_t need0 = reinterpret_cast<uintptr_t>(sbase) + csrc[v] + uint32_t(lo - vb);
-                const uintptr_t need1 = need0 + uintptr_t(hi - lo);            // source bytes [need0, need1)
-                const uintptr_t ws = need0 - uintptr_t(lo - r0);               // source of chunk byte 0
-                const uintptr_t wa = ws & ~uintptr_t(3);
-                const uint32_t sh = uint32_t(ws & 3u);
-                uint32_t d[5];
-                #pragma unroll
-                for (int k = 0; k < 5; k++) {
-                    const uintptr_t da = wa + 4u * k;
-                    d[k] = (da + 4 > need0 && da < need1) ? *reinterpret_cast<const uint32_t*>(da) : 0u;
-                }
-                const uint32_t bm = (0xffffu >> (16 - uint32_t(hi - r0))) & ~((1u << uint32_t(lo - r0)) - 1u);
-                #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t w = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-                    const uint32_t m = (((bm >> (4 * k)) & 0xfu) * 0x00204081u & 0x01010101u) * 0xffu;
-                    word[k] = (word[k] & ~m) | (w & m);
-                }
-            }
-            if (int64_t(vend) >= r0 + 16 || v + 1 >= nv) break;
-            v++;
-            vb = coff[v];
-            vend = v + 1 < nv ? coff[v + 1] : total;
-        }
-        if (r0 >= 0 && r0 + 16 <= int64_t(total)) {
-            *reinterpret_cast<uint4*>(dst) = make_uint4(word[0], word[1], word[2], word[3]);
-        } else {
+        const uint32_t v = si == 0 ? 0u : uint32_t(cv[si]);
+        bool wide = r0 >= 0 && r0 + 64 <= int64_t(total);
+        uint64_t M = 0;   // bit b: a value starts at span byte b (0 < b < 64)
+        uint32_t K = 0;
+        if (wide) {
+            uint32_t u = v + 1, prev = 0;
             #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const int64_t r = r0 + k;
-                if (r >= 0 && r < int64_t(total)) dst[k] = uint8_t(word[k >> 2] >> (8 * (k & 3)));
+            for (uint32_t k = 0; k <= SP_K; k++) {
+                const uint32_t b = u < nv ? coff[u] - uint32_t(r0) : 64u;
+                if (b < 64u) {
+                    wide &= k < SP_K && b != prev;   // (a zero-length value: two holes at one byte)
+                    M |= 1ull << b;
+                    K++;
+                    prev = b;
+                    u++;
+                }
             }
         }
+        const uintptr_t src = reinterpret_cast<uintptr_t>(sbase) + base0 + uint32_t(r0) + 4u * v;
+        if (wide) wide = src + 64u + 4u * K + 4u <= reinterpret_cast<uintptr_t>(send);
+        if (wide) {   // a dword holding two holes (values of 1-3 bytes) is not one v_perm
+            #pragma unroll
+            for (int d = 0; d < 16; d++) wide &= __popcll((M >> (4 * d + 1)) & 7ull) <= 1;
+        }
+        if (!wide) {
+            #pragma unroll
+            for (int k = 0; k < 4; k++) copy_chunk16(coff, csrc, nv, total, sbase, send, a0, c + 16u * uint32_t(k), v);
+            continue;
+        }
+        const uint32_t sh = uint32_t(src & 3u);
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(src & ~uintptr_t(3));
+        const uint32_t nd = (sh + 64u + 4u * K + 3u) >> 2;   // <= 21 dwords hold the span's source bytes
+        uint32_t W[21];
+        #pragma unroll
+        for (int k = 0; k < 21; k++) W[k] = uint32_t(k) < nd ? q[k] : 0u;
+        uint32_t Z[20];   // Z[j]: the 4 source bytes at src + 4 j
+        #pragma unroll
+        for (int k = 0; k < 20; k++) Z[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
+        uint32_t o[16];
+        #pragma unroll
+        for (int d = 0; d < 16; d++) {
+            const uint32_t h0 = uint32_t(__popcll(M & ((2ull << (4 * d)) - 1ull)));   // holes before byte 4 d + 1
+            const uint32_t m3 = uint32_t(M >> (4 * d + 1)) & 7u;                          // a hole at byte 4 d + 1..3
+            const uint32_t A = sp_pick(Z, d, h0);
+            const uint32_t B = sp_pick(Z, d, min(h0 + 1u, SP_K));
+            const uint32_t t = uint32_t(__ffs(m3));                                         // 1..3, 0: none
+            const uint32_t sel = 0x03020100u | (t ? (0x04040404u & (0xffffffffu << (8u * t))) : 0u);
+            o[d] = __builtin_amdgcn_perm(B, A, sel);
+        }
+        uint4* d4 = reinterpret_cast<uint4*>(c);
+        #pragma unroll
+        for (int k = 0; k < 4; k++) d4[k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
     }
 }
 
@@ -2311,6 +2429,7 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
             const uint8_t* sb = dict ? ck.dict_data : s.val;
             const uint8_t* se = dict ? pages[ck.dict_page].body + pages[ck.dict_page].body_len : s.val + s.val_n;
             if (tchars <= SHORT_AVG * tv) copy_chars_short(S.coff, S.csrc, tv, tchars, sb, ck.chars + char_base);
+            else if (!dict) copy_chars_plain(S.coff, S.csrc, tv, tchars, sb, se, ck.chars + char_base, S.cv);
             else copy_chars_fast(S.coff, S.csrc, tv, tchars, sb, se, ck.chars + char_base, S.cv);
         }
         if (ck.max_def > 0 && ck.validity) flush_bits(S.vbits, slot_base + e0, want, ck.validity);
@@ -3409,7 +3528,7 @@ void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list,
                   BaJob* d_bajobs, hipStream_t st) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_count_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res, d_bajobs);
-    hipLaunchKernelGGL(k_count, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res, d_bajobs);
+    hipLaunchKernelGGL(k_count, dim3(std::min(n, 64)), dim3(NT), 0, st, d_chunks, d_pages, d_list, n, d_res, d_bajobs);
 }
 // PLAIN BYTE_ARRAY walks of jobs [0, n_jobs) over tiles [0, n_tiles).
 void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevChunkResult* d_res, hipStream_t st) {
@@ -3560,7 +3679,7 @@ void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list
                    DevChunkResult* d_res, hipStream_t st) {
     // n_first: pages at the head of the list that will need k_decode (host-known); the rest are
     // checked by the stride loop
-    const int g = std::min(n, std::max(256, n_first));
+    const int g = std::min(n, std::max(32, n_first));   // (32: the stride loop is nearly always idle)
     if (n > 0) hipLaunchKernelGGL(k_decode, dim3(g), dim3(NT), 0, st, d_chunks, d_pages, d_list, n, d_res);
 }
 

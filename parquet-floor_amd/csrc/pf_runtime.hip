@@ -25,8 +25,9 @@
 
 namespace pf {
 void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, const int2*, int, uint32_t*,
-                   int*, DevChunkResult*, hipStream_t);
-void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, int*, hipStream_t);
+                   int*, DevChunkResult*, int, hipStream_t);
+void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, int*, int,
+                         hipStream_t);
 void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*, DevChunkResult*, hipStream_t);
 void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_snappy_head(SnappyJob*, int, DevPage*, const DevChunk*, int*, const DevChunkResult*, hipStream_t);
@@ -97,8 +98,10 @@ struct Streams {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t exec_stream = nullptr;
+    hipStream_t upload = nullptr;   // metadata / input H2D copies (pf_ctx::upload)
     ~Streams() {
         (void)hipSetDevice(device);
+        if (upload) { (void)hipStreamSynchronize(upload); (void)hipStreamDestroy(upload); }
         if (exec_stream) { (void)hipStreamSynchronize(exec_stream); (void)hipStreamDestroy(exec_stream); }
         if (stream) { (void)hipStreamSynchronize(stream); (void)hipStreamDestroy(stream); }
     }
@@ -113,6 +116,15 @@ struct pf_ctx {
     // get CUs ahead of this context's executor waves as those retire.
     hipStream_t exec_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // The batch's H2D copies (metadata tables, host input bytes) go on a stream of their own and
+    // `stream` waits for them (ev_up): on `stream` they would start only after the batch ahead of
+    // this one (a peer's, sharing the stream) has finished, and the copy engine's latency (~0.2 ms
+    // for SF1's ~0.4 MB of tables, ~0.7 ms for config 4's 3 MB) would open a gap between the two
+    // batches. The context's buffers are free once pf_wait has returned, so the copies can run
+    // under the peer's kernels. Only copies go on it (no kernels: it may share a hardware queue).
+    // PF_UPLOAD_STREAM=0: everything on `stream` (A/B).
+    hipStream_t upload = nullptr;
+    hipEvent_t ev_up = nullptr;
     hipEvent_t ev[N_EVENTS] = {};
     // recorded after the last operation of this context's decode: pf_wait waits for it, not for the
     // stream, so a context sharing the stream can have the next batch enqueued behind this one
@@ -142,7 +154,8 @@ struct pf_ctx {
     std::vector<BaJob> bajobs;             // PLAIN BYTE_ARRAY walks: dictionary pages, then data pages
     std::vector<int2> ba_tiles;            // (job relative to its batch, tile)
     int n_ba_dict = 0, n_ba_dict_tiles = 0;
-    uint32_t null_dict_lds = 0;   // bytes of the largest nullable-page dictionary that fits k_flat_null's LDS stage
+    uint32_t null_dict_lds = 0;            // bytes of the largest nullable-page dictionary that fits k_flat_null's LDS stage
+    int max_snap_win = 1;                  // index windows of the batch's largest Snappy job (k_snappy_chain's tables)
     uint32_t n_splits = 0;
     SnapWin* d_win = nullptr;              // in d_tokmap: bitmap | lane outs | windows | entry tables
     SnapEnt* d_ent = nullptr;
@@ -226,6 +239,10 @@ int enqueue_kernels(pf_ctx* ctx) {
     int* d_fallback = reinterpret_cast<int*>(meta + ctx->off_fallback);
     const int2* d_wins = reinterpret_cast<const int2*>(meta + ctx->off_wins);
 
+    if (ctx->upload) {   // the batch's H2D copies (upload_meta, the input) before its first kernel
+        HIPCHK(ctx, hipEventRecord(ctx->ev_up, ctx->upload));
+        HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_up, 0));
+    }
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
     if (ctx->npub_bytes)
         HIPCHK(ctx, hipMemsetAsync(static_cast<uint8_t*>(ctx->d_scratch.p) + ctx->off_npub, 0, ctx->npub_bytes, st));
@@ -234,7 +251,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_snappy_head(d_jobs, int(ctx->jobs.size()), d_pages, d_chunks, d_fallback, d_res, st);
     launch_snappy_litcopy(d_jobs, d_djobs, int(ctx->l_djobs.size()), d_fallback, st);
     launch_snappy_parse(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent,
-                        ctx->d_lane_out, d_splits, d_fallback, st);
+                        ctx->d_lane_out, d_splits, d_fallback, ctx->max_snap_win, st);
     EVREC(ctx, ctx->ev[2], st);
     if (ctx->exec_stream) {
         HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
@@ -291,10 +308,12 @@ int plan_snappy(pf_ctx* ctx) {
     ctx->wins.clear();
     ctx->pieces.clear();
     ctx->n_splits = 0;
+    ctx->max_snap_win = 1;
     uint32_t n_win = 0;
     size_t tw = 0, tp = 0;
     for (SnappyJob& jb : ctx->jobs) {
         jb.n_win = std::max<uint32_t>(1u, uint32_t((uint64_t(jb.src_len) + SNAP_WIN - 1) / SNAP_WIN));
+        ctx->max_snap_win = std::max(ctx->max_snap_win, int(std::min<uint32_t>(jb.n_win, 1u << 20)));
         jb.n_pieces = std::max<uint32_t>(1u, uint32_t((uint64_t(jb.dst_len) + SNAP_BLOCK - 1) / SNAP_BLOCK));
         tw += jb.n_win;
         tp += jb.n_pieces;
@@ -340,6 +359,8 @@ int plan_snappy(pf_ctx* ctx) {
     for (SnappyJob& jb : ctx->jobs) jb.tokmap = reinterpret_cast<uint32_t*>(base) + size_t(jb.win_base) * SNAP_WWORDS;
     return PF_OK;
 }
+
+hipStream_t up_stream(const pf_ctx* ctx) { return ctx->upload ? ctx->upload : ctx->stream; }
 
 // Upload metadata tables (results zeroed, arena counter zeroed).
 int upload_meta(pf_ctx* ctx) {
@@ -393,7 +414,7 @@ int upload_meta(pf_ctx* ctx) {
             r[c].num_rows = ck.num_entries;
         }
     }
-    HIPCHK(ctx, hipMemcpyAsync(ctx->d_meta.p, h, ctx->meta_bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_meta.p, h, ctx->meta_bytes, hipMemcpyHostToDevice, up_stream(ctx)));
     return PF_OK;
 }
 
@@ -776,9 +797,13 @@ int ctx_init(pf_ctx* ctx, pf_ctx* peer) {
         } else {
             HIPCHK(nullptr, hipStreamCreateWithFlags(&ctx->streams->stream, hipStreamNonBlocking));
         }
+        const char* us = std::getenv("PF_UPLOAD_STREAM");
+        if (!(us && us[0] == '0')) HIPCHK(nullptr, hipStreamCreateWithFlags(&ctx->streams->upload, hipStreamNonBlocking));
     }
     ctx->stream = ctx->streams->stream;
     ctx->exec_stream = ctx->streams->exec_stream;
+    ctx->upload = ctx->streams->upload;
+    if (ctx->upload) HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_up, hipEventDisableTiming));
     if (ctx->exec_stream) {
         HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
@@ -832,6 +857,7 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);   // this context's work and any peer's ahead of it
     if (ctx->exec_stream) (void)hipStreamSynchronize(ctx->exec_stream);
+    if (ctx->upload) (void)hipStreamSynchronize(ctx->upload);
     for (DevBuf* b : {&ctx->d_in, &ctx->d_scratch, &ctx->d_out, &ctx->d_bits, &ctx->d_chars, &ctx->d_meta, &ctx->d_tokmap,
                       &ctx->d_scan_in, &ctx->d_scan, &ctx->d_enc, &ctx->d_enc_sec, &ctx->d_enc_out})
         b->release();
@@ -843,6 +869,7 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
     if (ctx->ev_copy) (void)hipEventDestroy(ctx->ev_copy);
+    if (ctx->ev_up) (void)hipEventDestroy(ctx->ev_up);
     ctx->streams.reset();   // destroys the stream(s) when no other context shares them
     delete ctx;
     return PF_OK;
@@ -916,13 +943,19 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
 
     // ---- input bytes on device ----
     // stage "h2d" (ev[0] -> ev[1]): the input copy when there is one, the metadata upload and the
-    // memsets; for device-resident input it starts at the metadata upload (not before the host plan)
+    // memsets; for device-resident input it starts at the metadata upload (not before the host plan).
+    // With the upload stream it is what `stream` waits for them (in a pipelined run ~0: the copies
+    // ran under the previous batch; in the stage passes the stream is idle, so the host's
+    // upload_meta and the copy latency show)
     const bool input_h2d = !bytes_on_device && n_bytes;
     if (input_h2d) EVREC(ctx, ctx->ev[0], st);
     const uint8_t* d_bytes = bytes;
+    // (output copies still queued on `stream` read this context's arenas, not d_in / d_meta; the
+    // upload stream waits for them anyway, so it never runs ahead of anything of this context)
+    if (ctx->upload && ctx->copies_pending) HIPCHK(ctx, hipStreamWaitEvent(ctx->upload, ctx->ev_copy, 0));
     if (!bytes_on_device && n_bytes) {
         HIPCHK(ctx, ctx->d_in.ensure(n_bytes));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, bytes, n_bytes, hipMemcpyHostToDevice, st));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, bytes, n_bytes, hipMemcpyHostToDevice, up_stream(ctx)));
         d_bytes = static_cast<const uint8_t*>(ctx->d_in.p);
     }
     ctx->d_bytes = d_bytes;
@@ -1616,7 +1649,7 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     launch_snappy(reinterpret_cast<const SnappyJob*>(d + o_job), 1, reinterpret_cast<const int2*>(d + o_wn),
                   int(ctx->wins.size()), ctx->d_win, ctx->d_ent, ctx->d_lane_out, reinterpret_cast<const int2*>(d + o_pc),
                   int(ctx->pieces.size()), reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb),
-                  reinterpret_cast<DevChunkResult*>(d + o_res), st);
+                  reinterpret_cast<DevChunkResult*>(d + o_res), int(ctx->jobs.empty() ? 1 : ctx->jobs[0].n_win), st);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, ctx->h_res.ensure(512));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_res.p, d + o_res, sizeof(DevChunkResult), hipMemcpyDeviceToHost, st));

@@ -694,18 +694,23 @@ __device__ SnapEnt deep_walk(const SnappyJob& job, uint32_t w, uint32_t e, uint6
 // the chain) stops the propagation; the first such window is parsed exactly by the whole wave
 // once its entry is final, and the rounds continue behind it. The result replaces each window's
 // SnapWin: {true entry, merge point / exit, true output bytes, WM_* mode}.
+// LDS: the DP stage of the exact window parse (25 KiB) plus five per-window words sized by the host
+// to the batch's largest page (dynamic LDS, cap windows; round 3 sized them for FIX_MAXW = 20 KiB).
+// (r04: a whole-wave sequential exact parse instead of win_parse needs 9.5 KiB in all, but took the
+// isolated chain launch 93 -> 433 us on SF1: dense windows are parsed exactly often.)
 __global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict__ jobs, SnapWin* __restrict__ win,
                                                      const SnapEnt* __restrict__ ent, uint32_t* __restrict__ lane_out,
-                                                     int* __restrict__ fb) {
+                                                     int* __restrict__ fb, uint32_t cap) {
     __shared__ __attribute__((aligned(16))) uint8_t sp[SNAP_PSTAGE];
     __shared__ __attribute__((aligned(16))) uint16_t xs[SNAP_RB * 64];
     __shared__ __attribute__((aligned(16))) uint32_t sbits[SNAP_WWORDS];
     __shared__ uint32_t slo[64];
-    __shared__ uint32_t s_e[FIX_MAXW];     // current entry of window w
-    __shared__ uint32_t s_x[FIX_MAXW];     // exit given that entry (unresolved: the window's own exit)
-    __shared__ uint32_t s_pos[FIX_MAXW];   // merge point / exit (SnapWin.exit)
-    __shared__ uint32_t s_out[FIX_MAXW];   // true output bytes
-    __shared__ uint32_t s_mode[FIX_MAXW];  // 0 entry changed, 1 unresolved, else WM_* (WM_DONE: final)
+    extern __shared__ uint32_t dyn_chain[];
+    uint32_t* const s_e = dyn_chain;              // current entry of window w
+    uint32_t* const s_x = dyn_chain + cap;        // exit given that entry (unresolved: the window's own exit)
+    uint32_t* const s_pos = dyn_chain + 2 * cap;  // merge point / exit (SnapWin.exit)
+    uint32_t* const s_out = dyn_chain + 3 * cap;  // true output bytes
+    uint32_t* const s_mode = dyn_chain + 4 * cap; // 0 entry changed, 1 unresolved, else WM_* (WM_DONE: final)
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
     const SnappyJob job = jobs[j];
@@ -715,7 +720,7 @@ __global__ __launch_bounds__(64) void k_snappy_chain(const SnappyJob* __restrict
     SnapWin* Wn = win + job.win_base;
     const SnapEnt* E = ent + size_t(job.win_base) * 64;
     uint32_t* LO = lane_out + size_t(job.win_base) * 64;
-    if (nw > uint32_t(FIX_MAXW) || (Wn[0].flags & WIN_BROKEN)) {
+    if (nw > cap || nw > uint32_t(FIX_MAXW) || (Wn[0].flags & WIN_BROKEN)) {
         if (lane == 0) fb[j] = FB_SERIAL;
         return;
     }
@@ -1416,10 +1421,13 @@ void launch_snappy_serial(const SnappyJob*, int, const int*, DevChunkResult*, hi
 // Parse stage (token-start bitmaps, chain, 64 KiB split points) and execute stage, separately so
 // the runtime can time them apart.
 void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
-                         SnapEnt* d_ent, uint32_t* d_lane_out, uint32_t* d_splits, int* d_fb, hipStream_t s) {
+                         SnapEnt* d_ent, uint32_t* d_lane_out, uint32_t* d_splits, int* d_fb, int max_nwin, hipStream_t s) {
     if (n_jobs <= 0) return;
     hipLaunchKernelGGL(k_snappy_index, dim3(n_wins), dim3(64), 0, s, d_jobs, d_wins, d_win, d_ent, d_lane_out, d_fb);
-    hipLaunchKernelGGL(k_snappy_chain, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_win, (const SnapEnt*)d_ent, d_lane_out, d_fb);
+    // per-window tables of the largest page (multiple of 16 windows; pages above FIX_MAXW go serial)
+    const uint32_t cap = uint32_t(std::min(FIX_MAXW, (std::max(max_nwin, 1) + 15) & ~15));
+    hipLaunchKernelGGL(k_snappy_chain, dim3(n_jobs), dim3(64), 5 * 4 * cap, s, d_jobs, d_win, (const SnapEnt*)d_ent,
+                       d_lane_out, d_fb, cap);
 #ifndef PF_REPAIR_GRID   // (1024: SF1 3.30 ms mean of 6 interleaved runs; 4096: 3.28; one per window: 3.26 of 3)
 #define PF_REPAIR_GRID (1 << 24)
 #endif
@@ -1441,8 +1449,8 @@ void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_piece
 // All Snappy work of one batch, in stream order. fb must be zero on entry.
 void launch_snappy(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
                    SnapEnt* d_ent, uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
-                   int* d_fb, DevChunkResult* d_res, hipStream_t s) {
-    launch_snappy_parse(d_jobs, n_jobs, d_wins, n_wins, d_win, d_ent, d_lane_out, d_splits, d_fb, s);
+                   int* d_fb, DevChunkResult* d_res, int max_nwin, hipStream_t s) {
+    launch_snappy_parse(d_jobs, n_jobs, d_wins, n_wins, d_win, d_ent, d_lane_out, d_splits, d_fb, max_nwin, s);
     launch_snappy_exec(d_jobs, n_jobs, d_pieces, n_pieces, d_splits, d_fb, d_res, s);
 }
 

@@ -1,0 +1,20 @@
+#!/bin/bash
+# r04: lane-per-dword PLAIN chars copy + exec2 far-copy load hoist: tests, flat stamps, SF1 lines.
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-/root/repo} || exit 1
+OUT=$PWD/gpurun_out/${1:-r04_k}; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > $OUT/pytest.log 2>&1
+rc=$?; tail -2 $OUT/pytest.log; [ $rc -eq 0 ] || { tail -40 $OUT/pytest.log; exit 1; }
+PFLOOR_LIB_PATH=$PWD/parquet-floor_amd/diag/libpfloor_stamps.so timeout -k 10 300 python -u tools/probe_flat_cols.py > $OUT/probe_flat.log 2>&1 || { tail -20 $OUT/probe_flat.log; exit 1; }
+cat $OUT/probe_flat.log
+PFLOOR_LIB_PATH=$PWD/parquet-floor_amd/diag/libpfloor_stamps.so timeout -k 10 200 python -u tools/probe_exec.py > $OUT/probe_exec.log 2>&1 || { tail -20 $OUT/probe_exec.log; exit 1; }
+cat $OUT/probe_exec.log
+B="--no-cpu-baseline --no-pmc --no-e2e --no-write --steps 50 --warmup 5"
+one() { local tag=$1; shift
+  timeout -k 10 400 python -u bench.py $B "$@" > $OUT/b_$tag.json 2>> $OUT/err.log || { tail -20 $OUT/err.log; exit 1; }
+  python3 -c "import json; d=json.load(open('$OUT/b_$tag.json')); print('$tag', d['ms_per_step'], d['roofline']['kernel'][:30], d['roofline']['launch_ms'], {k: round(v,3) for k,v in d['stage_ms'].items()}, d['parity']['bit_exact'])"; }
+one s4
+one s1 --streams 1
+one s4b
+one flat --workload flat --steps 30
+one nested --workload nested --steps 30
