@@ -1373,8 +1373,22 @@ __device__ __forceinline__ uint64_t ld64_bytes(const uint8_t* p) {
     return v;
 }
 // LSB-first bit field of width w <= 32 starting at bit `sh` (< 8) of p (12 bytes readable from p).
-__device__ __forceinline__ uint32_t bits_fast(const uint8_t* p, uint32_t sh, int w) {
-    const uint64_t v = ld_u64_any(p) >> sh;
+// Branch-free unaligned loads from global memory for callers that guarantee the extra readable
+// bytes: all dwords are loaded unconditionally (no per-lane branch on the alignment, so a thread's
+// loads of several values stay in flight together) and joined with v_alignbyte (shift 0 = dword).
+__device__ __forceinline__ uint32_t gld_u32_8(const uint8_t* p) {   // p + 8 readable
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const PF_GLOBAL uint32_t* q = (const PF_GLOBAL uint32_t*)(a & ~uintptr_t(3));
+    return __builtin_amdgcn_alignbyte(q[1], q[0], uint32_t(a & 3u));
+}
+__device__ __forceinline__ uint64_t gld_u64_12(const uint8_t* p) {   // p + 12 readable
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const PF_GLOBAL uint32_t* q = (const PF_GLOBAL uint32_t*)(a & ~uintptr_t(3));
+    const uint32_t sh = uint32_t(a & 3u), d0 = q[0], d1 = q[1], d2 = q[2];
+    return uint64_t(__builtin_amdgcn_alignbyte(d1, d0, sh)) | (uint64_t(__builtin_amdgcn_alignbyte(d2, d1, sh)) << 32);
+}
+__device__ __forceinline__ uint32_t bits_fast(const uint8_t* p, uint32_t sh, int w) {   // p + 12 readable
+    const uint64_t v = gld_u64_12(p) >> sh;
     return uint32_t(v & (w == 32 ? 0xffffffffull : ((1ull << w) - 1ull)));
 }
 
@@ -1741,11 +1755,11 @@ __device__ inline void copy_chars_plain(const uint32_t* coff, const uint32_t* cs
             continue;
         }
         const uint32_t sh = uint32_t(src & 3u);
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(src & ~uintptr_t(3));
+        const PF_GLOBAL uint32_t* q = (const PF_GLOBAL uint32_t*)(src & ~uintptr_t(3));
         const uint32_t nd = (sh + 64u + 4u * K + 3u) >> 2;   // <= 21 dwords hold the span's source bytes
-        uint32_t W[21];
+        uint32_t W[21];   // (all issued together: dwords past nd re-read the last one, never past send)
         #pragma unroll
-        for (int k = 0; k < 21; k++) W[k] = uint32_t(k) < nd ? q[k] : 0u;
+        for (int k = 0; k < 21; k++) W[k] = q[min(uint32_t(k), nd - 1u)];
         uint32_t Z[20];   // Z[j]: the 4 source bytes at src + 4 j
         #pragma unroll
         for (int k = 0; k < 20; k++) Z[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
@@ -1760,9 +1774,9 @@ __device__ inline void copy_chars_plain(const uint32_t* coff, const uint32_t* cs
             const uint32_t sel = 0x03020100u | (t ? (0x04040404u & (0xffffffffu << (8u * t))) : 0u);
             o[d] = __builtin_amdgcn_perm(B, A, sel);
         }
-        uint4* d4 = reinterpret_cast<uint4*>(c);
+        PF_GLOBAL u32x4* d4 = (PF_GLOBAL u32x4*)c;
         #pragma unroll
-        for (int k = 0; k < 4; k++) d4[k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+        for (int k = 0; k < 4; k++) d4[k] = u32x4{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
     }
 }
 
@@ -1988,24 +2002,32 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
                 } else if (enc == 0) {
                     if ((uint64_t(e) + 1) * uint64_t(w) > s.val_n) { bad = 1; continue; }
                     const uint8_t* src = s.val + uint64_t(e) * uint64_t(w);
-                    if (w == 8) v[k] = src + 12 <= vend ? ld_u64_any(src) : ld64_bytes(src);
-                    else v[k] = src + 8 <= vend ? ld_u32_any(src) : ld32le(src, 0, 4);
+                    if (w == 8) v[k] = src + 12 <= vend ? gld_u64_12(src) : ld64_bytes(src);
+                    else v[k] = src + 8 <= vend ? gld_u32_8(src) : ld32le(src, 0, 4);
                 } else {
                     v[k] = reinterpret_cast<const uint64_t*>(pg.aux)[e];
                 }
             }
-            if (dict) {
+            if (dict) {   // all FB gathers issued together (entries past the tile / bad ids load element 0)
+                const int64_t dn = ck.dict_n;
                 #pragma unroll
                 for (uint32_t k = 0; k < FB; k++) {
                     const uint32_t e = e0 + (kb + k) * NT + uint32_t(tid);
-                    if (e >= e0 + want) continue;
-                    if (int64_t(id[k]) >= ck.dict_n) { bad = 1; continue; }
-                    if (dlds) {
+                    if (e < e0 + want && int64_t(id[k]) >= dn) bad = 1;
+                    id[k] = int64_t(id[k]) < dn ? id[k] : 0u;
+                }
+                if (dlds) {
+                    #pragma unroll
+                    for (uint32_t k = 0; k < FB; k++)
                         v[k] = w == 8 ? S.dict[id[k]] : reinterpret_cast<const uint32_t*>(S.dict)[id[k]];
-                    } else {
-                        const uint8_t* src = ck.dict_data + uint64_t(id[k]) * uint64_t(w);
-                        v[k] = w == 8 ? *reinterpret_cast<const uint64_t*>(src) : *reinterpret_cast<const uint32_t*>(src);
-                    }
+                } else if (w == 8) {
+                    const PF_GLOBAL uint64_t* g = (const PF_GLOBAL uint64_t*)ck.dict_data;
+                    #pragma unroll
+                    for (uint32_t k = 0; k < FB; k++) v[k] = g[id[k]];
+                } else {
+                    const PF_GLOBAL uint32_t* g = (const PF_GLOBAL uint32_t*)ck.dict_data;
+                    #pragma unroll
+                    for (uint32_t k = 0; k < FB; k++) v[k] = g[id[k]];
                 }
             }
             #pragma unroll
@@ -2044,8 +2066,8 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
                 } else if (enc == 0) {
                     if ((uint64_t(e) + 1) * uint64_t(w) > s.val_n) { bad = 1; continue; }
                     const uint8_t* src = s.val + uint64_t(e) * uint64_t(w);
-                    if (w == 8 && src + 12 <= vend) *reinterpret_cast<uint64_t*>(dst) = ld_u64_any(src);
-                    else if (w == 4 && src + 8 <= vend) *reinterpret_cast<uint32_t*>(dst) = ld_u32_any(src);
+                    if (w == 8 && src + 12 <= vend) *reinterpret_cast<uint64_t*>(dst) = gld_u64_12(src);
+                    else if (w == 4 && src + 8 <= vend) *reinterpret_cast<uint32_t*>(dst) = gld_u32_8(src);
                     else copy_value(dst, src, w);
                 } else {   // DELTA_BINARY_PACKED, decoded by k_delta into aux
                     const uint64_t* dv = reinterpret_cast<const uint64_t*>(pg.aux);
@@ -2557,6 +2579,10 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
     Sections s;
+    if (pg.done & DONE_NULL) {   // k_page_null decoded the page
+        if (tid == 0) LT[1] = 0;
+        return;
+    }
     if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.max_def <= 0 || !page_sections(pg, ck, s) || !s.def_rle ||
         s.def_n > LVL_STAGE) {   // (longer level sections: k_flat / k_decode)
         if (tid == 0) LT[1] = 0;
@@ -2803,6 +2829,12 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     extern __shared__ __attribute__((aligned(16))) uint64_t DL[];
     const int2 pbk = blocks[blockIdx.x];
     if (pbk.x < 0) return;   // padding of the XCD-grouped block list (runtime)
+#ifdef PF_STAMPS   // phase cycles per block: 0 blocks, 1 tables, 2 LDS stage, 3 levels + scan, 4 gather + store
+    unsigned long long t_ph = __builtin_amdgcn_s_memtime(), t_beg = t_ph;
+#define NSTAMP(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (threadIdx.x == 0) PSTAMP(i, t_ - t_ph); t_ph = t_; }
+#else
+#define NSTAMP(i) ((void)0)
+#endif
     const int pi = pbk.x;
     const uint32_t blk = uint32_t(pbk.y);
     DevPage& pg = pages[pi];
@@ -2810,7 +2842,7 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     const int tid = threadIdx.x;
     const uint32_t* LT = pg.lvltab;
     if (!LT || res[pg.chunk].status != 0 || ck.max_rep != 0 || (ck.width != 4 && ck.width != 8) ||
-        (pg.done & DONE_FIXED) || LT[1] != 1u)   // (other widths: k_flat / k_decode)
+        (pg.done & (DONE_FIXED | DONE_NULL)) || LT[1] != 1u)   // (other widths: k_flat / k_decode; k_page_null took it)
         return;
     Sections s;
     if (!page_sections(pg, ck, s)) return;
@@ -2841,6 +2873,7 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
         if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi);
         return;
     }
+    NSTAMP(1);
     // one round of loads: level runs, id runs, level bytes, id bytes
     const uint32_t nrun = r1 - r0;
     for (uint32_t i = tid; i < nrun; i += NTN) {
@@ -2873,6 +2906,7 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
         for (uint32_t i = tid; i < nw; i += NTN) DL[i] = g[i];
     }
     __syncthreads();
+    NSTAMP(2);
     const uint8_t* dst8 = reinterpret_cast<const uint8_t*>(S.dst);
     const uint8_t* ist8 = reinterpret_cast<const uint8_t*>(S.ist);
     const uint32_t dbase = d0 * 8u - doff * 8u;   // stream bit of LDS bit 0
@@ -2912,18 +2946,27 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     uint32_t tv;
     const uint32_t vo = block_excl_scan<NTN>(__popc(fv), S.scan_tmp, tv);
     if (tv != ve - vb) bad = 1;   // the block table disagrees with the levels
+    NSTAMP(3);
     const uint32_t gv0 = vb + vo;   // value index of this thread's first present entry
     uint64_t v[NEPT];
     #pragma unroll
     for (int k = 0; k < NEPT; k++) v[k] = 0;
     if (fv && !bad) {
+        // Two phases: the ids of the present entries (LDS only), then ALL of the thread's gathers
+        // issued back to back through global-address-space loads (absent entries load element 0 and
+        // are zeroed after), so the wave waits on one round of L2 / HBM latency instead of one per
+        // entry (flat loads under per-entry branches each ended in a vmcnt(0) wait).
         if (dict) {
+            uint32_t idv[NEPT];
+            #pragma unroll
+            for (int k = 0; k < NEPT; k++) idv[k] = 0;
             int vr = run_find(S.vrun, int(vnr), gv0);
             const Run V0 = S.vrun[vr];
             // the thread's present values are gv0, gv0 + 1, ...: when one id run holds them all, their
             // ids are consecutive fields of that run (no run search per value)
             const bool one_run = gv0 + uint32_t(__popc(fv)) <= V0.first + V0.count;
             const uint32_t b0 = V0.packed ? uint32_t(uint64_t(V0.data) + uint64_t(gv0 - V0.first) * id_bw - ibase) : 0u;
+            const int64_t dn = ck.dict_n;
             uint32_t r = 0;
             #pragma unroll
             for (int k = 0; k < NEPT; k++) {
@@ -2948,25 +2991,59 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
                     }
                 }
                 r++;
-                bad |= int64_t(id) >= ck.dict_n;
-                const uint32_t idc = int64_t(id) < ck.dict_n ? id : 0u;
-                if (dl) {
-                    v[k] = w == 4 ? uint64_t(reinterpret_cast<const uint32_t*>(DL)[idc]) : DL[idc];
+                bad |= int64_t(id) >= dn;
+                idv[k] = int64_t(id) < dn ? id : 0u;
+            }
+            const uintptr_t da = reinterpret_cast<uintptr_t>(ck.dict_data);
+            if (dl) {
+                #pragma unroll
+                for (int k = 0; k < NEPT; k++)
+                    v[k] = w == 4 ? uint64_t(reinterpret_cast<const uint32_t*>(DL)[idv[k]]) : DL[idv[k]];
+            } else if ((da & uintptr_t(w - 1)) == 0) {   // (dictionary pages start 16-byte aligned in scratch)
+                if (w == 4) {
+                    const PF_GLOBAL uint32_t* g = (const PF_GLOBAL uint32_t*)ck.dict_data;
+                    #pragma unroll
+                    for (int k = 0; k < NEPT; k++) v[k] = g[idv[k]];
                 } else {
-                    const uint8_t* src = ck.dict_data + uint64_t(idc) * uint64_t(w);
-                    if (w == 4) v[k] = ld_u32_any(src);
-                    else v[k] = ld_u64_any(src);
+                    const PF_GLOBAL uint64_t* g = (const PF_GLOBAL uint64_t*)ck.dict_data;
+                    #pragma unroll
+                    for (int k = 0; k < NEPT; k++) v[k] = g[idv[k]];
+                }
+            } else {
+                #pragma unroll
+                for (int k = 0; k < NEPT; k++) {
+                    const uint8_t* src = ck.dict_data + uint64_t(idv[k]) * uint64_t(w);
+                    v[k] = w == 4 ? uint64_t(ld_u32_any(src)) : ld_u64_any(src);
                 }
             }
         } else {
+            // value of entry k: gv0 + present entries before k (absent entries load their successor's,
+            // clamped to the thread's last present value)
+            const uint32_t last = gv0 + uint32_t(__popc(fv)) - 1u;
+            uint32_t vi[NEPT];
             #pragma unroll
-            for (int k = 0; k < NEPT; k++) {
-                if (!((fv >> k) & 1u)) continue;
-                const uint8_t* src = s.val + uint64_t(gv0 + __popc(fv & ((1u << k) - 1u))) * uint64_t(w);
-                if (w == 4) v[k] = ld_u32_any(src);
-                else v[k] = ld_u64_any(src);
+            for (int k = 0; k < NEPT; k++) vi[k] = min(gv0 + uint32_t(__popc(fv & ((1u << k) - 1u))), last);
+            if ((reinterpret_cast<uintptr_t>(s.val) & uintptr_t(w - 1)) == 0) {
+                if (w == 4) {
+                    const PF_GLOBAL uint32_t* g = (const PF_GLOBAL uint32_t*)s.val;
+                    #pragma unroll
+                    for (int k = 0; k < NEPT; k++) v[k] = g[vi[k]];
+                } else {
+                    const PF_GLOBAL uint64_t* g = (const PF_GLOBAL uint64_t*)s.val;
+                    #pragma unroll
+                    for (int k = 0; k < NEPT; k++) v[k] = g[vi[k]];
+                }
+            } else {
+                #pragma unroll
+                for (int k = 0; k < NEPT; k++) {
+                    const uint8_t* src = s.val + uint64_t(vi[k]) * uint64_t(w);
+                    v[k] = w == 4 ? uint64_t(ld_u32_any(src)) : ld_u64_any(src);
+                }
             }
         }
+        #pragma unroll
+        for (int k = 0; k < NEPT; k++)
+            if (!((fv >> k) & 1u)) v[k] = 0;
     }
     const uint64_t slot_base = uint64_t(pg.entry_start);
     if (m && !bad) {
@@ -3004,6 +3081,273 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     if (ck.validity) flush_bits(S.vbits, slot_base + e_begin, e_end - e_begin, ck.validity);
     if (tid == 0) {
         if (ck.needs_count == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values), (unsigned long long)tv);
+        atomicOr(&pg.done, DONE_NULL);
+    }
+#ifdef PF_STAMPS
+    NSTAMP(4);
+    if (tid == 0) { PSTAMP(0, 1); PSTAMP(5, t_ph - t_beg); }
+#endif
+#undef NSTAMP
+}
+
+// k_page_null: one 512-thread workgroup per nullable flat page (fixed width 4 / 8, dictionary or
+// PLAIN), for pages whose level section (<= LVL_STAGE bytes), level runs (<= PN_RUNS) and
+// dictionary-id bytes (<= PN_IST) fit its LDS. It runs before k_lvl in the levels stage and does
+// k_lvl's and k_flat_null's work for the page in one launch: the level and id sections are staged
+// once, the level run headers are found by the all-positions chain (every byte decoded as a
+// header, the chain from 0 followed in LDS), decoded in parallel and prefix-summed, and the page's
+// 4096-entry blocks are then decoded in a loop (8 consecutive entries per thread, present bits ->
+// block scan -> value index -> id from LDS -> gathers issued together -> 16-byte stores). The
+// page's metadata chain, its section staging and the level parse are paid once per page instead of
+// once per block, and k_lvl's one-wave block-table pass is gone. Anything it cannot decode
+// exactly (a broken chain, an id past the dictionary, too many runs) leaves the page unmarked:
+// k_lvl / k_flat_null / k_decode then take it and report it as before.
+constexpr int PN_NT = 512;
+constexpr uint32_t PN_RUNS = 512;        // level runs held in LDS
+constexpr uint32_t PN_IST = 32768;       // dictionary-id bytes staged in LDS
+constexpr uint32_t PN_MAX_BLOCKS = 16;   // entries <= 16 * FBLK
+struct PageNullLds {
+    uint32_t lv[(LVL_STAGE + 64) / 4];
+    uint16_t nxt[LVL_STAGE];
+    Run drun[PN_RUNS];
+    Run vrun[RUN_CAP];
+    uint32_t ist[PN_IST / 4 + 8];
+    uint32_t vbits[FBLK / 32 + 2];
+    uint32_t scan_tmp[PN_NT / 64];
+    uint32_t nh, ok, take;
+};
+__global__ __launch_bounds__(PN_NT) void k_page_null(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                    const int* __restrict__ list, DevChunkResult* res) {
+    __shared__ __attribute__((aligned(16))) PageNullLds S;
+    const int pi = list[blockIdx.x];
+    DevPage& pg = pages[pi];
+    const DevChunk& ck = chunks[pg.chunk];
+    const int tid = threadIdx.x;
+    const uint32_t* T = pg.runtab;
+    Sections s;
+    const int w = ck.width;
+    const bool dict = is_dict_enc(pg.encoding);
+    const uint32_t ne = uint32_t(pg.num_values);
+    // (uniform: every thread evaluates the same loads)
+    bool take = pg.lvltab != nullptr && res[pg.chunk].status == 0 && ck.max_rep == 0 && ck.max_def > 0 &&
+                (w == 4 || w == 8) && ck.values != nullptr && !(pg.done & (DONE_FIXED | DONE_NULL)) &&
+                (dict || pg.encoding == 0) && ne > 0 && ne <= PN_MAX_BLOCKS * FBLK && page_sections(pg, ck, s) &&
+                s.def_rle && s.def_n > 0 && s.def_n <= LVL_STAGE;
+    uint32_t id_bw = 0, idn = 0, vnr = 0, idcov = 0;
+    if (take && dict) {
+        take = T != nullptr && T[2] == 1u && T[0] <= uint32_t(RUN_CAP) && T[0] > 0 && s.val_n > 1 && s.val[0] <= 32 &&
+               s.val_n - 1 <= PN_IST && ck.dict_data != nullptr && ck.dict_n > 0;
+        if (take) { id_bw = s.val[0]; idn = uint32_t(s.val_n - 1); vnr = T[0]; idcov = T[1]; }
+    }
+    if (!take) return;
+    const int bw = bit_width(uint32_t(ck.max_def));
+    const uint32_t maxd = uint32_t(ck.max_def);
+    const uint32_t dn = uint32_t(s.def_n);
+    // ---- stage: level bytes, id bytes, id runs (one round of loads)
+    const uint32_t doff = stage_bytes(S.lv, s.def, dn, 0, dn);
+    const uint32_t ioff = dict ? stage_bytes(S.ist, s.val + 1, idn, 0, idn) : 0u;
+    for (uint32_t i = tid; i < vnr; i += PN_NT) {
+        const uint32_t f = T[4 + 2 * i];
+        const uint32_t nf = i + 1 < vnr ? (T[4 + 2 * (i + 1)] & 0x7fffffffu) : idcov;
+        Run r;
+        r.first = f & 0x7fffffffu;
+        r.count = nf - r.first;
+        r.data = T[5 + 2 * i];
+        r.packed = f >> 31;
+        S.vrun[i] = r;
+    }
+    __syncthreads();
+    const uint8_t* lv8 = reinterpret_cast<const uint8_t*>(S.lv);
+    const uint8_t* stw = lv8 + doff;   // stw[i] = level section byte i (zero past the section)
+    // ---- level run headers: every byte position as a header (position of the next one)
+    for (uint32_t p = tid; p < dn; p += PN_NT) {
+        uint32_t h = 0, hl = 0, nx = 0xffffu;
+        #pragma unroll
+        for (uint32_t k = 0; k < 3; k++) {   // (a header of > 3 bytes counts > 2^20 entries: no run here)
+            const uint32_t c = p + k < dn ? uint32_t(stw[p + k]) : 0x80u;
+            h |= (c & 0x7fu) << (7 * k);
+            if (!(c & 0x80u)) { hl = k + 1; break; }
+        }
+        if (hl) {
+            const uint32_t pay = (h & 1u) ? (h >> 1) * uint32_t(bw) : (uint32_t(bw) + 7u) >> 3;
+            if (p + hl + pay <= dn) nx = p + hl + pay;
+        }
+        S.nxt[p] = uint16_t(nx);
+    }
+    __syncthreads();
+    if (tid == 0) {   // the chain from position 0 (one LDS load per run)
+        uint32_t p = 0, nh = 0;
+        bool ok = true;
+        while (p < dn) {
+            if (nh == PN_RUNS) { ok = false; break; }
+            S.drun[nh++].data = p;   // header position (decoded below)
+            const uint32_t q = S.nxt[p];
+            if (q == 0xffffu) { ok = false; break; }   // no valid run at p
+            p = q;
+        }
+        S.nh = nh;
+        S.ok = ok ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!S.ok) return;   // k_lvl / k_decode take the page (and report what is wrong with it)
+    const uint32_t nh = S.nh;
+    {   // decode the headers in parallel; first entries by a block scan of the counts
+        uint32_t cnt = 0, data = 0, packed = 0;
+        bool bad = false;
+        const uint32_t k = uint32_t(tid);
+        if (k < nh) {
+            const uint32_t P = S.drun[k].data;
+            uint32_t h = 0, hl = 0;
+            for (uint32_t b = 0; b < 3; b++) {
+                const uint32_t c = stw[P + b];
+                h |= (c & 0x7fu) << (7 * b);
+                if (!(c & 0x80u)) { hl = b + 1; break; }
+            }
+            packed = h & 1u;
+            cnt = packed ? (h >> 1) * 8u : (h >> 1);
+            if (packed) data = (doff + P + hl) * 8u;   // LDS bit offset of the run's first level
+            else {
+                for (uint32_t b = 0; b < ((uint32_t(bw) + 7u) >> 3); b++) data |= uint32_t(stw[P + hl + b]) << (8 * b);
+                bad = data > maxd;
+            }
+        }
+        uint32_t tot;
+        const uint32_t first = block_excl_scan<PN_NT>(cnt, S.scan_tmp, tot);
+        if (k < nh) {
+            Run r;
+            r.first = first;
+            r.count = cnt;
+            r.data = data;
+            r.packed = packed;
+            S.drun[k] = r;
+        }
+        if (__syncthreads_or(bad || (tid == 0 && tot < ne))) return;
+    }
+    // ---- the page's blocks
+    const uint64_t slot_base = uint64_t(pg.entry_start);
+    const uint8_t* ist8 = reinterpret_cast<const uint8_t*>(S.ist);
+    const uint32_t ilim = (ioff + idn) * 8u;   // staged id bits
+    const uint32_t nblk = (ne + FBLK - 1) / FBLK;
+    const uintptr_t da = reinterpret_cast<uintptr_t>(dict ? ck.dict_data : s.val);
+    const bool galign = (da & uintptr_t(w - 1)) == 0;
+    const int64_t dnn = dict ? ck.dict_n : 0;
+    uint32_t vbase = 0;   // page-relative index of the block's first present value
+    for (uint32_t b = 0; b < nblk; b++) {
+        const uint32_t e_begin = b * FBLK, e_end = min(ne, e_begin + FBLK);
+        for (uint32_t i = tid; i < FBLK / 32 + 2; i += PN_NT) S.vbits[i] = 0;
+        const uint32_t e = e_begin + uint32_t(tid) * NEPT;
+        const uint32_t m = e < e_end ? min(uint32_t(NEPT), e_end - e) : 0u;
+        uint32_t fv = 0;
+        int bad = 0;
+        if (m) {
+            int r = run_find(S.drun, int(nh), e);
+            const Run R = S.drun[r];
+            if (e + m <= R.first + R.count && (!R.packed || bw == 1)) {   // one run
+                if (!R.packed) fv = R.data == maxd ? ((1u << m) - 1u) : 0u;
+                else fv = lds_bits(lv8, R.data + (e - R.first), m);
+            } else {
+                for (uint32_t k = 0; k < m; k++) {
+                    while (r + 1 < int(nh) && e + k >= S.drun[r].first + S.drun[r].count) r++;
+                    const Run& Rk = S.drun[r];
+                    uint32_t dl = Rk.data;
+                    if (Rk.packed) dl = lds_bits(lv8, Rk.data + (e + k - Rk.first) * uint32_t(bw), uint32_t(bw));
+                    bad |= dl > maxd;
+                    fv |= uint32_t(dl == maxd) << k;
+                }
+            }
+        }
+        uint32_t tv;
+        const uint32_t vo = block_excl_scan<PN_NT>(__popc(fv), S.scan_tmp, tv);
+        const uint32_t gv0 = vbase + vo;
+        uint32_t idv[NEPT];
+        #pragma unroll
+        for (int k = 0; k < NEPT; k++) idv[k] = 0;
+        if (fv) {
+            if (dict) {
+                if (gv0 + uint32_t(__popc(fv)) > idcov) bad = 1;
+                int vr = run_find(S.vrun, int(vnr), gv0);
+                uint32_t j = 0;
+                #pragma unroll
+                for (int k = 0; k < NEPT; k++) {
+                    if (!((fv >> k) & 1u)) continue;
+                    const uint32_t gv = gv0 + j++;
+                    while (vr + 1 < int(vnr) && gv >= S.vrun[vr].first + S.vrun[vr].count) vr++;
+                    const Run& V = S.vrun[vr];
+                    uint32_t id = V.data;
+                    if (V.packed) {
+                        const uint64_t bb = uint64_t(V.data) + uint64_t(ioff) * 8u + uint64_t(gv - V.first) * id_bw;
+                        bad |= bb + id_bw > ilim;
+                        id = bb + id_bw <= ilim ? lds_bits(ist8, uint32_t(bb), id_bw) : 0u;
+                    }
+                    bad |= int64_t(id) >= dnn;
+                    idv[k] = int64_t(id) < dnn ? id : 0u;
+                }
+            } else {
+                const uint32_t last = gv0 + uint32_t(__popc(fv)) - 1u;
+                if (uint64_t(last + 1) * uint64_t(w) > s.val_n) bad = 1;
+                #pragma unroll
+                for (int k = 0; k < NEPT; k++) idv[k] = bad ? 0u : min(gv0 + uint32_t(__popc(fv & ((1u << k) - 1u))), last);
+            }
+        }
+        if (__syncthreads_or(bad)) return;   // (nothing counted or marked: the fallback redoes the page)
+        uint64_t v[NEPT];
+        #pragma unroll
+        for (int k = 0; k < NEPT; k++) v[k] = 0;
+        if (!fv) {
+        } else if (galign) {
+            if (w == 4) {
+                const PF_GLOBAL uint32_t* g = (const PF_GLOBAL uint32_t*)da;
+                #pragma unroll
+                for (int k = 0; k < NEPT; k++) v[k] = g[idv[k]];
+            } else {
+                const PF_GLOBAL uint64_t* g = (const PF_GLOBAL uint64_t*)da;
+                #pragma unroll
+                for (int k = 0; k < NEPT; k++) v[k] = g[idv[k]];
+            }
+        } else {
+            #pragma unroll
+            for (int k = 0; k < NEPT; k++) {
+                const uint8_t* src = reinterpret_cast<const uint8_t*>(da) + uint64_t(idv[k]) * uint64_t(w);
+                v[k] = w == 4 ? uint64_t(ld_u32_any(src)) : ld_u64_any(src);
+            }
+        }
+        #pragma unroll
+        for (int k = 0; k < NEPT; k++)
+            if (!((fv >> k) & 1u)) v[k] = 0;
+        if (m) {
+            uint8_t* dst0 = ck.values + (slot_base + e) * uint64_t(w);
+            if (m == NEPT && (reinterpret_cast<uintptr_t>(dst0) & 15u) == 0) {
+                u32x4* d4 = reinterpret_cast<u32x4*>(dst0);
+                if (w == 4) {
+                    d4[0] = u32x4{uint32_t(v[0]), uint32_t(v[1]), uint32_t(v[2]), uint32_t(v[3])};
+                    d4[1] = u32x4{uint32_t(v[4]), uint32_t(v[5]), uint32_t(v[6]), uint32_t(v[7])};
+                } else {
+                    #pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        d4[q] = u32x4{uint32_t(v[2 * q]), uint32_t(v[2 * q] >> 32), uint32_t(v[2 * q + 1]), uint32_t(v[2 * q + 1] >> 32)};
+                }
+            } else {
+                for (uint32_t k = 0; k < m; k++) {
+                    uint32_t* d = reinterpret_cast<uint32_t*>(dst0 + uint64_t(k) * uint64_t(w));   // 4-byte aligned
+                    d[0] = uint32_t(v[k]);
+                    if (w == 8) d[1] = uint32_t(v[k] >> 32);
+                }
+            }
+        }
+        if (ck.validity && fv) {
+            const uint64_t abase = (slot_base + e_begin) & ~uint64_t(31);
+            const uint64_t rb = slot_base + e - abase;
+            const uint32_t sh = uint32_t(rb & 31);
+            atomicOr(&S.vbits[rb >> 5], fv << sh);
+            if (sh + NEPT > 32 && sh) atomicOr(&S.vbits[(rb >> 5) + 1], fv >> (32 - sh));
+        }
+        __syncthreads();
+        if (ck.validity) flush_bits(S.vbits, slot_base + e_begin, e_end - e_begin, ck.validity);
+        vbase += tv;
+        __syncthreads();   // (vbits / scan_tmp reused by the next block)
+    }
+    if (tid == 0) {
+        if (ck.needs_count == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values), (unsigned long long)vbase);
         atomicOr(&pg.done, DONE_NULL);
     }
 }
@@ -3657,7 +4001,11 @@ void launch_runs(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
 }
 void launch_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                 hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_lvl, dim3(n), dim3(LT_NT), 0, st, d_chunks, d_pages, d_list, d_res);
+    if (n <= 0) return;
+    // PF_PAGE_NULL=0: every nullable page through k_lvl + k_flat_null (A/B, tests)
+    static const bool page_null = [] { const char* e = std::getenv("PF_PAGE_NULL"); return !(e && e[0] == '0'); }();
+    if (page_null) hipLaunchKernelGGL(k_page_null, dim3(n), dim3(PN_NT), 0, st, d_chunks, d_pages, d_list, d_res);
+    hipLaunchKernelGGL(k_lvl, dim3(n), dim3(LT_NT), 0, st, d_chunks, d_pages, d_list, d_res);
 }
 void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                  hipStream_t st, bool nullable, uint32_t null_dict_lds) {   // d_list: n (page, block) pairs

@@ -72,17 +72,41 @@ struct DevBuf {
 
 struct HostBuf {
     void* p = nullptr;
+    void* d = nullptr;   // the device's address of the pinned pages (kernels read / write them over PCIe)
     size_t cap = 0;
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
-        if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
+        if (p) { (void)hipHostFree(p); p = nullptr; d = nullptr; cap = 0; }
         size_t want = std::max<size_t>(n + n / 4, 1 << 16);
         hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
-        if (e == hipSuccess) cap = want;
+        if (e == hipSuccess) {
+            cap = want;
+            if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) d = nullptr;
+        }
         return e;
     }
-    void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
+    void release() { if (p) (void)hipHostFree(p); p = nullptr; d = nullptr; cap = 0; }
 };
+
+// Copies between pinned host pages and device memory by a kernel on the decode stream: two ranges
+// of 8-byte words, grid-stride. The batch's metadata upload and its results download were SDMA /
+// blit copies on the stream (PF_ZC=0): config 1 0.41 -> 0.39 ms, the others unchanged.
+// (An upload stream of its own, event-joined, made every config slower: SF1 3.13 -> 4.4 ms.)
+__global__ __launch_bounds__(256) void k_copy_words(uint64_t* __restrict__ d0, const uint64_t* __restrict__ s0, uint32_t n0,
+                                                    uint64_t* __restrict__ d1, const uint64_t* __restrict__ s1, uint32_t n1) {
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n0 + n1; i += stride) {
+        if (i < n0) d0[i] = s0[i];
+        else d1[i - n0] = s1[i - n0];
+    }
+}
+static_assert(sizeof(DevChunkResult) % 8 == 0 && sizeof(DevChunk) % 8 == 0, "k_copy_words moves 8-byte words");
+inline void copy_words(void* d0, const void* s0, size_t b0, void* d1, const void* s1, size_t b1, hipStream_t st) {
+    const uint32_t n0 = uint32_t(b0 / 8), n1 = uint32_t(b1 / 8);
+    const uint32_t grid = std::max(1u, std::min(1024u, (n0 + n1 + 255u) / 256u));
+    hipLaunchKernelGGL(k_copy_words, dim3(grid), dim3(256), 0, st, static_cast<uint64_t*>(d0), static_cast<const uint64_t*>(s0), n0,
+                       static_cast<uint64_t*>(d1), static_cast<const uint64_t*>(s1), n1);
+}
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -98,10 +122,8 @@ struct Streams {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t exec_stream = nullptr;
-    hipStream_t upload = nullptr;   // metadata / input H2D copies (pf_ctx::upload)
     ~Streams() {
         (void)hipSetDevice(device);
-        if (upload) { (void)hipStreamSynchronize(upload); (void)hipStreamDestroy(upload); }
         if (exec_stream) { (void)hipStreamSynchronize(exec_stream); (void)hipStreamDestroy(exec_stream); }
         if (stream) { (void)hipStreamSynchronize(stream); (void)hipStreamDestroy(stream); }
     }
@@ -116,15 +138,7 @@ struct pf_ctx {
     // get CUs ahead of this context's executor waves as those retire.
     hipStream_t exec_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // The batch's H2D copies (metadata tables, host input bytes) go on a stream of their own and
-    // `stream` waits for them (ev_up): on `stream` they would start only after the batch ahead of
-    // this one (a peer's, sharing the stream) has finished, and the copy engine's latency (~0.2 ms
-    // for SF1's ~0.4 MB of tables, ~0.7 ms for config 4's 3 MB) would open a gap between the two
-    // batches. The context's buffers are free once pf_wait has returned, so the copies can run
-    // under the peer's kernels. Only copies go on it (no kernels: it may share a hardware queue).
-    // PF_UPLOAD_STREAM=0: everything on `stream` (A/B).
-    hipStream_t upload = nullptr;
-    hipEvent_t ev_up = nullptr;
+    bool zc = true;                        // metadata / results copied by k_copy_words (PF_ZC=0: SDMA copies)
     hipEvent_t ev[N_EVENTS] = {};
     // recorded after the last operation of this context's decode: pf_wait waits for it, not for the
     // stream, so a context sharing the stream can have the next batch enqueued behind this one
@@ -239,10 +253,6 @@ int enqueue_kernels(pf_ctx* ctx) {
     int* d_fallback = reinterpret_cast<int*>(meta + ctx->off_fallback);
     const int2* d_wins = reinterpret_cast<const int2*>(meta + ctx->off_wins);
 
-    if (ctx->upload) {   // the batch's H2D copies (upload_meta, the input) before its first kernel
-        HIPCHK(ctx, hipEventRecord(ctx->ev_up, ctx->upload));
-        HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_up, 0));
-    }
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
     if (ctx->npub_bytes)
         HIPCHK(ctx, hipMemsetAsync(static_cast<uint8_t*>(ctx->d_scratch.p) + ctx->off_npub, 0, ctx->npub_bytes, st));
@@ -293,10 +303,16 @@ int enqueue_kernels(pf_ctx* ctx) {
     EVREC(ctx, ctx->ev[10], st);
     HIPCHK(ctx, hipGetLastError());
     // results + device-written chunk fields (chars base) back to pinned host memory
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_res.p, meta + ctx->off_res, sizeof(DevChunkResult) * ctx->n_chunks,
-                               hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(ctx->h_res.p) + align_up(sizeof(DevChunkResult) * ctx->n_chunks, 256),
-                               d_chunks, sizeof(DevChunk) * ctx->n_chunks, hipMemcpyDeviceToHost, st));
+    const size_t res_pad = align_up(sizeof(DevChunkResult) * ctx->n_chunks, 256);
+    if (ctx->zc && ctx->h_res.d) {
+        copy_words(ctx->h_res.d, meta + ctx->off_res, sizeof(DevChunkResult) * ctx->n_chunks,
+                   static_cast<uint8_t*>(ctx->h_res.d) + res_pad, d_chunks, sizeof(DevChunk) * ctx->n_chunks, st);
+    } else {
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_res.p, meta + ctx->off_res, sizeof(DevChunkResult) * ctx->n_chunks,
+                                   hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipMemcpyAsync(static_cast<uint8_t*>(ctx->h_res.p) + res_pad, d_chunks, sizeof(DevChunk) * ctx->n_chunks,
+                                   hipMemcpyDeviceToHost, st));
+    }
     HIPCHK(ctx, hipEventRecord(ctx->ev_done, st));
     return PF_OK;
 }
@@ -360,8 +376,6 @@ int plan_snappy(pf_ctx* ctx) {
     return PF_OK;
 }
 
-hipStream_t up_stream(const pf_ctx* ctx) { return ctx->upload ? ctx->upload : ctx->stream; }
-
 // Upload metadata tables (results zeroed, arena counter zeroed).
 int upload_meta(pf_ctx* ctx) {
     uint8_t* h = static_cast<uint8_t*>(ctx->h_meta.p);
@@ -414,7 +428,8 @@ int upload_meta(pf_ctx* ctx) {
             r[c].num_rows = ck.num_entries;
         }
     }
-    HIPCHK(ctx, hipMemcpyAsync(ctx->d_meta.p, h, ctx->meta_bytes, hipMemcpyHostToDevice, up_stream(ctx)));
+    if (ctx->zc && ctx->h_meta.d) copy_words(ctx->d_meta.p, ctx->h_meta.d, ctx->meta_bytes, nullptr, nullptr, 0, ctx->stream);
+    else HIPCHK(ctx, hipMemcpyAsync(ctx->d_meta.p, h, ctx->meta_bytes, hipMemcpyHostToDevice, ctx->stream));
     return PF_OK;
 }
 
@@ -797,13 +812,13 @@ int ctx_init(pf_ctx* ctx, pf_ctx* peer) {
         } else {
             HIPCHK(nullptr, hipStreamCreateWithFlags(&ctx->streams->stream, hipStreamNonBlocking));
         }
-        const char* us = std::getenv("PF_UPLOAD_STREAM");
-        if (!(us && us[0] == '0')) HIPCHK(nullptr, hipStreamCreateWithFlags(&ctx->streams->upload, hipStreamNonBlocking));
     }
     ctx->stream = ctx->streams->stream;
     ctx->exec_stream = ctx->streams->exec_stream;
-    ctx->upload = ctx->streams->upload;
-    if (ctx->upload) HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_up, hipEventDisableTiming));
+    {
+        const char* z = std::getenv("PF_ZC");
+        ctx->zc = !(z && z[0] == '0');
+    }
     if (ctx->exec_stream) {
         HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
@@ -857,7 +872,6 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);   // this context's work and any peer's ahead of it
     if (ctx->exec_stream) (void)hipStreamSynchronize(ctx->exec_stream);
-    if (ctx->upload) (void)hipStreamSynchronize(ctx->upload);
     for (DevBuf* b : {&ctx->d_in, &ctx->d_scratch, &ctx->d_out, &ctx->d_bits, &ctx->d_chars, &ctx->d_meta, &ctx->d_tokmap,
                       &ctx->d_scan_in, &ctx->d_scan, &ctx->d_enc, &ctx->d_enc_sec, &ctx->d_enc_out})
         b->release();
@@ -869,7 +883,6 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
     if (ctx->ev_copy) (void)hipEventDestroy(ctx->ev_copy);
-    if (ctx->ev_up) (void)hipEventDestroy(ctx->ev_up);
     ctx->streams.reset();   // destroys the stream(s) when no other context shares them
     delete ctx;
     return PF_OK;
@@ -943,19 +956,13 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
 
     // ---- input bytes on device ----
     // stage "h2d" (ev[0] -> ev[1]): the input copy when there is one, the metadata upload and the
-    // memsets; for device-resident input it starts at the metadata upload (not before the host plan).
-    // With the upload stream it is what `stream` waits for them (in a pipelined run ~0: the copies
-    // ran under the previous batch; in the stage passes the stream is idle, so the host's
-    // upload_meta and the copy latency show)
+    // memsets; for device-resident input it starts at the metadata upload (not before the host plan)
     const bool input_h2d = !bytes_on_device && n_bytes;
     if (input_h2d) EVREC(ctx, ctx->ev[0], st);
     const uint8_t* d_bytes = bytes;
-    // (output copies still queued on `stream` read this context's arenas, not d_in / d_meta; the
-    // upload stream waits for them anyway, so it never runs ahead of anything of this context)
-    if (ctx->upload && ctx->copies_pending) HIPCHK(ctx, hipStreamWaitEvent(ctx->upload, ctx->ev_copy, 0));
     if (!bytes_on_device && n_bytes) {
         HIPCHK(ctx, ctx->d_in.ensure(n_bytes));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, bytes, n_bytes, hipMemcpyHostToDevice, up_stream(ctx)));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, bytes, n_bytes, hipMemcpyHostToDevice, st));
         d_bytes = static_cast<const uint8_t*>(ctx->d_in.p);
     }
     ctx->d_bytes = d_bytes;
@@ -1820,6 +1827,29 @@ int pf_debug_page_paths(pf_ctx* ctx, int* out, int n_pages) {
             out[3 * i] = pg[size_t(i)].direct;
             out[3 * i + 1] = pg[size_t(i)].dbp_ok;
             out[3 * i + 2] = pg[size_t(i)].seg_ok;
+        }
+    }
+    return np;
+}
+
+// Diagnostics (tests): the done flags of the last decode's pages (DONE_FIXED 1 / DONE_FLAT 2 /
+// DONE_NULL 4: which kernel took the page; k_page_null and k_flat_null both set DONE_NULL, and only
+// k_page_null's pages keep no level table (lvl = 0 in out[2 * i + 1])).
+extern "C" int pf_debug_page_done(pf_ctx* ctx, int* out, int n_pages) {
+    if (!ctx || !ctx->d_meta.p || !ctx->tables_from_decode) return fail(ctx, PF_ERR_STATE, "no finished decode");
+    if (ctx->pending) return fail(ctx, PF_ERR_STATE, "call pf_wait first");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int np = int(ctx->pages.size());
+    const int m = n_pages < np ? n_pages : np;
+    if (out && m > 0) {
+        std::vector<DevPage> pg(static_cast<size_t>(m));
+        HIPCHK(ctx, hipMemcpy(pg.data(), static_cast<uint8_t*>(ctx->d_meta.p) + ctx->off_pages, sizeof(DevPage) * size_t(m),
+                              hipMemcpyDeviceToHost));
+        for (int i = 0; i < m; i++) {
+            out[2 * i] = pg[size_t(i)].done;
+            uint32_t lt1 = 0;   // k_lvl's "block table fits" word (k_flat_null ran on the page)
+            if (pg[size_t(i)].lvltab) HIPCHK(ctx, hipMemcpy(&lt1, pg[size_t(i)].lvltab + 1, 4, hipMemcpyDeviceToHost));
+            out[2 * i + 1] = int(lt1);
         }
     }
     return np;

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Kernel trace of a short bench of one workload; per-stream timeline of one decode.
 #   tools/gpu_trace_wl.sh TAG [bench args]
+set -o pipefail
 cd ${GRAFT_REPO_ROOT:-/root/repo} || exit 1
 OUT=$PWD/gpurun_out/${1:-trace}; shift; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp

@@ -10,7 +10,11 @@ t00 = min(int(r["Start_Timestamp"]) for r in rows)
 for s in sorted({r["Stream_Id"] for r in rows}):
     rs = sorted((r for r in rows if r["Stream_Id"] == s), key=lambda r: int(r["Start_Timestamp"]))
     # a decode starts at its k_snappy_head (first kernel after the metadata upload / memsets)
-    starts = [i for i, r in enumerate(rs) if "k_snappy_head" in r["Kernel_Name"]]
+    # decodes start at their metadata upload: k_copy_words launches alternate upload / results
+    # download (zero-copy default); older traces: the Snappy index / head kernel
+    cw = [i for i, r in enumerate(rs) if "k_copy_words" in r["Kernel_Name"]]
+    starts = cw[0::2] if cw else [i for i, r in enumerate(rs) if "k_snappy_index" in r["Kernel_Name"] or
+                                  "k_snappy_head" in r["Kernel_Name"]]
     if not starts:
         continue
     print(f"stream {s}: {len(starts)} decodes")

@@ -12,7 +12,11 @@ print("streams:", streams)
 for s in ([sid] if sid else streams):
     rs = sorted((r for r in rows if r["Stream_Id"] == s), key=lambda r: int(r["Start_Timestamp"]))
     # a decode starts at the fillBuffer (bits memset) or the first k_snappy_index after a gap
-    starts = [i for i, r in enumerate(rs) if "k_snappy_index" in r["Kernel_Name"]]
+    # decodes start at their metadata upload: k_copy_words launches alternate upload / results
+    # download (zero-copy default); older traces: the Snappy index / head kernel
+    cw = [i for i, r in enumerate(rs) if "k_copy_words" in r["Kernel_Name"]]
+    starts = cw[0::2] if cw else [i for i, r in enumerate(rs) if "k_snappy_index" in r["Kernel_Name"] or
+                                  "k_snappy_head" in r["Kernel_Name"]]
     if not starts:
         continue
     i0 = starts[which] if -len(starts) <= which < len(starts) else starts[-1]
