@@ -51,13 +51,15 @@ sys.path.insert(0, os.path.join(ROOT, "parquet-floor_amd"))
 SF1_ROWS = 6001215
 RG_ROWS = 1 << 20
 SEED = 42
+# PF_DEBUG_SKIP (stage ablation, pf_runtime.hip): skipped stages leave chunks failed by design
+_SKIP = bool(os.environ.get("PF_DEBUG_SKIP"))
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PCIE_GBS = 63.0         # MI355X_MICROARCH.md: PCIe Gen5 x16 per direction
 # kernels of each stage (rocprof names, pf_runtime.hip's launch order between the stage events), for
 # the PMC traffic and the label of the roofline object
 STAGE_KERNELS = {
     "snappy_parse": r"k_snappy_(head|litcopy|index|chain|repair|splits)$",
-    "snappy_exec": r"k_snappy_(exec2|serial)$",
+    "snappy_exec": r"k_snappy_(exec2|exec5|serial)$",
     "delta": r"k_(dbp_pos|dbp_blk|dbp_scan|delta)$",
     "levels": r"k_(runs|lvl|dlen)$",
     "count": r"k_(nest_lvl|count|count_flat|count_seg|nest_scan|nest_ids|nest_chars|ba_[a-z]+)$",
@@ -65,7 +67,8 @@ STAGE_KERNELS = {
     "flat": r"k_flat(_all|_fixed|_null)?$",
     "decode": r"k_(decode|decode_seg|dba_chars)$",
 }
-STAGE_LABEL = {"snappy_exec": "Snappy executor stage: k_snappy_exec2 (+ redo, serial fallback)",
+STAGE_LABEL = {"snappy_exec": "Snappy executor stage: %s (+ redo, serial fallback)"
+               % ("k_snappy_exec2" if os.environ.get("PF_EXEC", "")[:1] == "2" else "k_snappy_exec5"),
                "snappy_parse": "Snappy parse stage: k_snappy_head + index + chain + repair + splits",
                "delta": "DELTA_BINARY_PACKED stage: k_dbp_pos / k_dbp_blk / k_dbp_scan + k_delta",
                "levels": "level / id run stage: k_runs + k_lvl + k_dlen",
@@ -345,7 +348,7 @@ def pmc_child(args):
     bi.upload(dec)
     for _ in range(1 + ROOF_PASSES):
         dec.decode(bi.descs, bi.dev.value, bi.nbytes, on_device=True)
-        if dec.wait() != 0:
+        if dec.wait() != 0 and not _SKIP:
             raise RuntimeError(dec.error())
     bi.free(dec)
     dec.close()
@@ -584,7 +587,8 @@ class ContextPool:
 
     @staticmethod
     def _wait(d):
-        if d.wait() != 0:
+        # PF_DEBUG_SKIP (stage ablation, pf_runtime.hip): skipped stages leave chunks failed by design
+        if d.wait() != 0 and not _SKIP:
             raise RuntimeError(d.error())
 
     def _work(self, i, passes, pipelined):
@@ -763,7 +767,7 @@ def main():
     for d, bl in zip(decs, batches):
         for bi in bl:
             d.decode(bi.descs, bi.dev.value, bi.nbytes, on_device=True)
-            if d.wait() != 0:
+            if d.wait() != 0 and not _SKIP:
                 raise RuntimeError(d.error())
             for i, (p, c, *_r) in enumerate(bi.items):
                 dbytes += chunk_decoded_bytes(pf.columns[c], d.info(i))
@@ -818,7 +822,7 @@ def main():
     dec = decs[0]
     for r in range(ROOF_PASSES):
         dec.decode(b0.descs, b0.dev.value, b0.nbytes, on_device=True)
-        if dec.wait() != 0:
+        if dec.wait() != 0 and not _SKIP:
             raise RuntimeError(dec.error())
         for k, v in dec.timing().items():
             iso[k] = iso.get(k, 0.0) + v / ROOF_PASSES
@@ -1062,7 +1066,7 @@ def measure_e2e(decs, batches, pf, st_all, copy_mode="batch", barrier=None):
         row = []
         for bi in bl:
             d.decode(bi.descs, bi.host.ptr.value, bi.nbytes, on_device=False)
-            if d.wait() != 0:
+            if d.wait() != 0 and not _SKIP:
                 raise RuntimeError(d.error())
             infos = [d.info(i) for i in range(len(bi.items))]
             row.append(infos)
@@ -1122,7 +1126,7 @@ def measure_e2e(decs, batches, pf, st_all, copy_mode="batch", barrier=None):
         try:
             for bj, bi in enumerate(bl):
                 d.decode(bi.descs, bi.host.ptr.value, bi.nbytes, on_device=False)
-                if d.wait() != 0:
+                if d.wait() != 0 and not _SKIP:
                     raise RuntimeError(d.error())
                 arr, idx, n = outs[ci][1][bj]
                 _native.check(L.pf_copy_columns_async(d.h, n, idx, arr), d.h, "pf_copy_columns_async")
@@ -1193,7 +1197,7 @@ def _e2e_batch(decs, batches, layouts, pf, barrier=None):
         need = 0
         for bi in bl:   # batch sizes from one decode of each batch
             d.decode(bi.descs, bi.host.ptr.value, bi.nbytes, on_device=False)
-            if d.wait() != 0:
+            if d.wait() != 0 and not _SKIP:
                 raise RuntimeError(d.error())
             n = C.c_size_t()
             _native.check(L.pf_batch_bytes(d.h, C.byref(n)), d.h, "pf_batch_bytes")
@@ -1208,7 +1212,7 @@ def _e2e_batch(decs, batches, layouts, pf, barrier=None):
             buf = bufs[ci]
             for bi in bl:
                 d.decode(bi.descs, bi.host.ptr.value, bi.nbytes, on_device=False)
-                if d.wait() != 0:
+                if d.wait() != 0 and not _SKIP:
                     raise RuntimeError(d.error())
                 _native.check(L.pf_copy_batch_async(d.h, buf.ptr, buf.nbytes), d.h, "pf_copy_batch_async")
             _native.check(L.pf_sync(d.h), d.h, "pf_sync")

@@ -253,17 +253,30 @@ int enqueue_kernels(pf_ctx* ctx) {
     int* d_fallback = reinterpret_cast<int*>(meta + ctx->off_fallback);
     const int2* d_wins = reinterpret_cast<const int2*>(meta + ctx->off_wins);
 
+    // diagnostics (bench analysis only, results are wrong): PF_DEBUG_SKIP=parse,exec,ba,levels,count,flat,decode
+    // leaves those stages' kernels out, so a step's time without them shows what they cost under load
+    static const unsigned skip = [] {
+        const char* e = std::getenv("PF_DEBUG_SKIP");
+        unsigned m = 0;
+        if (e) {
+            const char* names[] = {"parse", "exec", "ba", "levels", "count", "flat", "decode"};
+            for (int i = 0; i < 7; i++)
+                if (std::strstr(e, names[i])) m |= 1u << i;
+        }
+        return m;
+    }();
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
     if (ctx->npub_bytes)
         HIPCHK(ctx, hipMemsetAsync(static_cast<uint8_t*>(ctx->d_scratch.p) + ctx->off_npub, 0, ctx->npub_bytes, st));
     EVREC(ctx, ctx->ev[1], st);
     // single-literal pages in place, PLAIN fixed-width pages straight into the column (pf_pages.hip)
-    launch_snappy_head(d_jobs, int(ctx->jobs.size()), d_pages, d_chunks, d_fallback, d_res, st);
-    launch_snappy_litcopy(d_jobs, d_djobs, int(ctx->l_djobs.size()), d_fallback, st);
-    launch_snappy_parse(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent,
+    if (!(skip & 1u)) launch_snappy_head(d_jobs, int(ctx->jobs.size()), d_pages, d_chunks, d_fallback, d_res, st);
+    if (!(skip & 1u)) launch_snappy_litcopy(d_jobs, d_djobs, int(ctx->l_djobs.size()), d_fallback, st);
+    if (!(skip & 1u)) launch_snappy_parse(d_jobs, int(ctx->jobs.size()), d_wins, int(ctx->wins.size()), ctx->d_win, ctx->d_ent,
                         ctx->d_lane_out, d_splits, d_fallback, ctx->max_snap_win, st);
     EVREC(ctx, ctx->ev[2], st);
-    if (ctx->exec_stream) {
+    if (skip & 2u) {
+    } else if (ctx->exec_stream) {
         HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->exec_stream, ctx->ev_fork, 0));
         launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res,
@@ -278,26 +291,27 @@ int enqueue_kernels(pf_ctx* ctx) {
     const int2* d_batiles = reinterpret_cast<const int2*>(meta + ctx->off_batiles);
     const int n_ba = int(ctx->bajobs.size()), n_bt = int(ctx->ba_tiles.size());
     (void)d_dictbin;
-    launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st);
+    if (!(skip & 4u)) launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st);
     EVREC(ctx, ctx->ev[4], st);
     launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), ctx->max_dbp_nwin, d_res, st);
     EVREC(ctx, ctx->ev[5], st);
-    launch_runs(d_chunks, d_pages, d_runs, int(ctx->l_runs.size()), d_res, st);
-    launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st);
+    if (!(skip & 8u)) launch_runs(d_chunks, d_pages, d_runs, int(ctx->l_runs.size()), d_res, st);
+    if (!(skip & 8u)) launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st);
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
     EVREC(ctx, ctx->ev[6], st);
     launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, ctx->max_nwin, d_res, st);
-    launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st);
+    if (!(skip & 16u)) launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st);
     launch_nest_count(d_chunks, d_pages, d_nest, n_nest, d_nseg, n_nseg, d_res, st);
-    launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
-              d_res, st);
+    if (!(skip & 4u))
+        launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
+                  d_res, st);
     EVREC(ctx, ctx->ev[7], st);
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
     EVREC(ctx, ctx->ev[8], st);
-    launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty(), ctx->null_dict_lds);
+    if (!(skip & 32u)) launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty(), ctx->null_dict_lds);
     EVREC(ctx, ctx->ev[9], st);
-    launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), ctx->n_decode_first, d_res, st);
+    if (!(skip & 64u)) launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), ctx->n_decode_first, d_res, st);
     launch_nest_decode(d_chunks, d_pages, d_nseg, n_nseg, d_res, st);
     launch_dba_chars(d_chunks, d_pages, d_dba, int(ctx->l_dba.size()), d_res, st);
     EVREC(ctx, ctx->ev[10], st);

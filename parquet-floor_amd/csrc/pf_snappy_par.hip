@@ -1405,6 +1405,349 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
     for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) put1(od, a, ring[a & XRMASK]);
 }
 
+// ======================================================================== executor v5
+//
+// k_snappy_exec2 runs each 64-token batch as one serial instruction stream, and a dense piece
+// (16 K tokens per 64 KiB: l_partkey, l_extendedprice; sorted l_orderkey) is issue-bound at one
+// wave's rate — a wave alone on its SIMD issues a VALU instruction every 4 cycles — at ~600-700 K
+// cycles; the slowest piece sets the executor launch. k_snappy_exec5 splits that stream over the
+// two waves of one workgroup (two SIMDs), pipelined by one batch:
+//   wave 0 (producer): stages input, enumerates token starts, decodes batch i's tokens (output
+//     offsets, chain checks, cuts), loads its far-copy sources from HBM into LDS and writes the
+//     packed descriptors and token-start words into LDS buffer i & 1;
+//   wave 1 (consumer): meanwhile resolves batch i-1's bytes (exec2's windows, descriptors read from
+//     LDS instead of permuted from the token lanes) into the ring and flushes whole ring slots.
+// One workgroup barrier per batch. A far copy's source was flushed by the consumer: before every
+// barrier the consumer waits until all but its newest store have landed (all of them after a long
+// literal or an empty batch), the producer derives from the batch history the frontier below which
+// that guarantees the bytes (and their cache line) are in HBM, and a far copy above it cuts the batch
+// (one empty batch when it is the first token, which only follows a long literal).
+constexpr uint32_t X5_BATCH = 768;                     // output bytes of one batch (ring: + XSLOT + far margin)
+constexpr uint32_t X5_STG = (XSTAGE + 15u) & ~15u;     // one staged input chunk
+constexpr uint32_t X5_FSL = XFAR * FBUF_W * 4u;        // far-copy source slots of one batch
+constexpr uint32_t X5_STAGE0 = XRING;                  // [ring | stage x2 | far slots x2]: one byte address
+constexpr uint32_t X5_FBUF0 = XRING + 2u * X5_STG;     // selects any byte source
+constexpr uint32_t X5_LDS = X5_FBUF0 + 2u * X5_FSL;
+constexpr uint32_t X5_W = X5_BATCH / 32u;              // token-start words of a batch
+constexpr uint32_t X5_LINE = 128u;                     // a far source's cache line must be wholly landed
+enum : uint32_t { R5_NORMAL = 0, R5_LONG = 1, R5_NOP = 2, R5_END = 3, R5_BAD = 4 };
+
+// Workgroup barrier for LDS hand-over only (no wait on outstanding global stores).
+__device__ __forceinline__ void x5_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// Compiler ordering point for one wave's LDS accesses (the hardware runs them in order).
+__device__ __forceinline__ void x5_order() { asm volatile("" ::: "memory"); }
+
+__global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
+                                                      const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
+    __shared__ __attribute__((aligned(16))) uint8_t L[X5_LDS];
+    __shared__ uint16_t tokpos[XCHUNK / 2];
+    __shared__ uint32_t D0[2][64], D1[2][64];     // packed token descriptors (exec2's d0 / d1)
+    __shared__ uint32_t SB[2][X5_W], WP[2][X5_W];   // token starts of the batch's output, tokens in earlier words
+    __shared__ uint32_t REC[2][4];                  // kind, output start, output bytes, long literal input position
+    __shared__ uint16_t jv[256];
+    uint8_t* const ring = L;
+    const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
+    const int lane = int(threadIdx.x) & 63;
+    int j, k;
+    if (mode == 0) {
+        const int2 pc = pieces[blockIdx.x];
+        j = pc.x;
+        k = pc.y;
+    } else {
+        j = blockIdx.x;
+        k = 0;
+    }
+    const int f = fb[j];
+    bool whole;
+    if (mode == 0) {
+        if (f >= FB_REDO || (f == FB_WHOLE && k > 0)) return;
+        whole = f == FB_WHOLE;
+    } else {
+        if (f != FB_REDO) return;
+        whole = true;
+    }
+    const SnappyJob job = jobs[j];
+    const uint8_t* in = job.src;
+    const uint64_t n = job.src_len;
+    const uint32_t* sp = splits + job.split_base;
+    uint64_t pos0 = 0, ulen = 0;
+    if (!uvarint(in, n, pos0, ulen) || ulen != job.dst_len) {
+        if (threadIdx.x == 0) atomicMax(&fb[j], FB_SERIAL);
+        return;
+    }
+    if (mode == 0 && (job.dflags & 1u)) {   // diagnostics: forced redo
+        if (threadIdx.x == 0) atomicMax(&fb[j], FB_REDO);
+        return;
+    }
+    uint32_t ip, out_start, out_end = job.dst_len;
+    if (whole) {
+        ip = uint32_t(pos0);
+        out_start = 0;
+    } else {
+        if (k > 0 && sp[k] == SNAP_INVALID) return;   // no token at this boundary: an earlier piece covers it
+        ip = k == 0 ? uint32_t(pos0) : sp[k];
+        out_start = uint32_t(k) * SNAP_BLOCK;
+        for (uint32_t k2 = k + 1; k2 < job.n_pieces; k2++)
+            if (sp[k2] != SNAP_INVALID) { out_end = k2 * SNAP_BLOCK; break; }
+    }
+    const PF_GLOBAL uint16_t* tm16 = (const PF_GLOBAL uint16_t*)(job.tokmap);
+    const PF_GLOBAL uint8_t* gin = gptr(in);
+    PF_GLOBAL uint8_t* gdst = gptr(job.dst);
+    const OutDst od{gdst, mode == 0 ? gptr(job.ddst) : nullptr, job.dlo, job.dgran};
+    // producer state
+    uint32_t op = out_start, sb = 0, T = 0, I = 0, woff = 0, cb = 1;
+    uint32_t ops_m1 = out_start, k_m1 = R5_NOP, k_m2 = R5_NOP, nops = 0;
+    // consumer state
+    uint32_t F = out_start, cop = out_start;
+    uint32_t last = R5_END;
+    for (uint32_t it = 0;; it++) {
+        const uint32_t b = it & 1u;
+        if (wv == 0) {
+            // ---------------- producer: batch it into buffer b
+            uint32_t kind = R5_BAD, b_op = op, b_tot = 0, b_s0 = 0;
+            // landed frontier: the consumer finished batch it-2 before the last barrier
+            const uint32_t sf = out_start + ((ops_m1 - out_start) & ~(XSLOT - 1u));
+            const uint32_t LF = k_m2 == R5_NORMAL ? (sf >= out_start + XSLOT ? sf - XSLOT : out_start) : sf;
+            bool ok = true;
+            if (op >= out_end) {
+                kind = R5_END;
+                ok = false;
+            } else if (sb >= T) {   // next input chunk (the other stage buffer: the consumer may read this one)
+                if (ip >= n) {
+                    ok = false;
+                } else {
+                    I = ip & ~15u;
+                    cb ^= 1u;
+                    woff = snap_stage(L + X5_STAGE0 + cb * X5_STG, in, n, I, XSTAGE, lane);
+                    const uint32_t p16 = I + 16u * uint32_t(lane);
+                    uint32_t bits = uint64_t(p16) < n ? uint32_t(tm16[p16 >> 4]) : 0u;
+                    if (p16 + 16u <= ip) bits = 0;
+                    else if (p16 < ip) bits &= ~((1u << (ip - p16)) - 1u);
+                    const uint32_t cnt = __popc(bits);
+                    const uint32_t ex = dpp_incl_scan(cnt);
+                    T = __builtin_amdgcn_readlane(ex, 63);
+                    uint32_t q = ex - cnt;
+                    while (bits) {
+                        const uint32_t bb = uint32_t(__ffs(bits) - 1);
+                        bits &= bits - 1;
+                        tokpos[q++] = uint16_t(16u * uint32_t(lane) + bb);
+                    }
+                    sb = 0;
+                    x5_order();
+                    if (T == 0) ok = false;
+                }
+            }
+            if (ok) {
+                const uint8_t* stg = L + X5_STAGE0 + cb * X5_STG;
+                const uint32_t t = sb + uint32_t(lane);
+                const bool v = t < T;
+                const uint32_t pos = v ? uint32_t(tokpos[t]) : 0u;
+                const SnapTok tk = snap_tok(lds_read8(stg, woff + pos));
+                const uint32_t ol = v ? tk.ol : 0u;
+                const uint32_t start = I + pos;
+                const uint32_t endp = tk.tl > uint64_t(0xffffffffu - start) ? 0xffffffffu : start + uint32_t(tk.tl);
+                const uint32_t prev = dpp_prev(endp);
+                const uint32_t inc = dpp_incl_scan(ol);
+                const uint32_t otok = op + inc - ol;
+                const bool take = v && otok < out_end;
+                const int nt = __popcll(__ballot(take));
+                const bool wrong = take && ((lane == 0 ? start != ip : start != prev) || endp > n || op + inc > out_end ||
+                                            inc < ol);
+                if (__any(wrong) || nt == 0) {
+                    ok = false;
+                } else {
+                    const uint32_t kd = tk.kind;
+                    const uint32_t off = tk.arg;
+                    const uint32_t srcv = start + tk.arg;   // literal data position
+                    const bool lstaged = srcv + ol <= I + XCHUNK + 64;
+                    const uint32_t a = otok - off;          // copy source start
+                    const bool farc = take && kd != 0 && a + min(ol, off) <= op &&
+                                      int32_t(a - (op + X5_BATCH - XRING)) < 0;
+                    const bool fnr = farc && a + ol + X5_LINE > LF;   // source not yet landed in HBM
+                    const unsigned long long farm = __ballot(farc);
+                    const uint32_t frank = uint32_t(__popcll(farm & lane_mask_lt(uint32_t(lane))));
+                    const unsigned long long cutm =
+                        __ballot(take && (ol > 64u || inc > X5_BATCH || (kd == 0 && !lstaged) || (farc && frank >= XFAR) || fnr));
+                    const uint32_t cut = cutm ? uint32_t(__ffsll(cutm) - 1) : uint32_t(nt);
+                    uint32_t used = 0;
+                    if (cut == 0) {
+                        if (__builtin_amdgcn_readfirstlane(kd) == 0) {   // one long literal: the consumer copies it
+                            kind = R5_LONG;
+                            b_tot = __builtin_amdgcn_readfirstlane(ol);
+                            b_s0 = __builtin_amdgcn_readfirstlane(srcv);
+                            used = 1;
+                            nops = 0;
+                        } else if (__builtin_amdgcn_readfirstlane(uint32_t(fnr)) && nops < 3) {
+                            kind = R5_NOP;   // wait one batch for the source's stores to land
+                            nops++;
+                        } else {
+                            ok = false;
+                        }
+                    } else {
+                        used = cut;
+                        const uint32_t btot = __builtin_amdgcn_readlane(inc, cut - 1);
+                        const bool inb = take && uint32_t(lane) < cut;
+                        const bool lit = inb && kd == 0;
+                        const bool cp = inb && kd != 0;
+                        const bool far = cp && farc;
+                        if (__any(cp && (off == 0 || off > otok - out_start))) ok = false;
+                        // a far source straddling the direct split (level bytes | values) is not one window
+                        if (od.dd != nullptr && __any(far && a < od.dlo && a + ol > od.dlo)) ok = false;
+                        if (ok) {
+                            uint32_t* fl = reinterpret_cast<uint32_t*>(L + X5_FBUF0 + b * X5_FSL) + frank * FBUF_W;
+                            if (far) {
+                                const PF_GLOBAL uint8_t* fb0 = od.dd != nullptr && a >= od.dlo ? od.dd + a : gdst + a;
+                                const uintptr_t fa = reinterpret_cast<uintptr_t>(fb0);
+                                const PF_GLOBAL uint32_t* fsrc = (const PF_GLOBAL uint32_t*)(fa & ~uintptr_t(3));
+                                const uint32_t nwd = (uint32_t(fa & 3u) + ol + 3u) >> 2;
+                                uint32_t fw[FBUF_W];
+                                #pragma unroll
+                                for (int u = 0; u < int(FBUF_W); u++) fw[u] = uint32_t(u) < nwd ? fsrc[u] : 0u;
+                                #pragma unroll
+                                for (int u = 0; u < int(FBUF_W); u++)
+                                    if (uint32_t(u) < nwd) fl[u] = fw[u];
+                            }
+                            const uint32_t rel = otok - op;
+                            uint32_t d0 = 0, d1 = 0;
+                            if (inb) {
+                                const bool near = cp && !far;
+                                d0 = rel | ((near ? X2_COPY : X2_LDSADDR) << 11) | ((near && off < ol) ? (1u << 12) : 0u) |
+                                     (min(off, 0xffffu) << 16);
+                                const uint32_t fsh = od.dd != nullptr && a >= od.dlo
+                                                         ? uint32_t((reinterpret_cast<uintptr_t>(od.dd) + a) & 3u) : (a & 3u);
+                                d1 = lit ? X5_STAGE0 + cb * X5_STG + woff + (srcv - I)
+                                         : (far ? X5_FBUF0 + b * X5_FSL + frank * (FBUF_W * 4) + fsh : a);
+                            }
+                            D0[b][lane] = d0;
+                            D1[b][lane] = d1;
+                            if (lane < int(X5_W)) SB[b][lane] = 0;
+                            x5_order();
+                            if (inb) atomicOr(&SB[b][rel >> 5], 1u << (rel & 31u));
+                            x5_order();
+                            const uint32_t c = lane < int(X5_W) ? __popc(SB[b][lane]) : 0u;
+                            const uint32_t e2 = dpp_incl_scan(c) - c;
+                            if (lane < int(X5_W)) WP[b][lane] = e2;
+                            kind = R5_NORMAL;
+                            b_tot = btot;
+                            nops = 0;
+                        }
+                    }
+                    if (ok && used) {
+                        op += b_tot;
+                        ip = __builtin_amdgcn_readlane(endp, int(used) - 1);
+                        sb += used;
+                    }
+                }
+            }
+            if (!ok && kind != R5_END) kind = R5_BAD;
+            if (lane == 0) {
+                REC[b][0] = kind;
+                REC[b][1] = b_op;
+                REC[b][2] = b_tot;
+                REC[b][3] = b_s0;
+            }
+            k_m2 = k_m1;
+            k_m1 = kind;
+            ops_m1 = b_op;
+        } else if (it > 0) {
+            // ---------------- consumer: batch it-1 from buffer b ^ 1
+            const uint32_t pb = b ^ 1u;
+            const uint32_t kind = __builtin_amdgcn_readfirstlane(REC[pb][0]);
+            const uint32_t s0 = __builtin_amdgcn_readfirstlane(REC[pb][1]);
+            const uint32_t btot = __builtin_amdgcn_readfirstlane(REC[pb][2]);
+            if (kind == R5_NORMAL) {
+                const uint32_t* sbw = SB[pb];
+                const uint32_t* wpw = WP[pb];
+                const uint32_t* d0w = D0[pb];
+                const uint32_t* d1w = D1[pb];
+                for (uint32_t w0 = 0; w0 < btot; w0 += 256) {
+                    const uint32_t s1 = s0 + w0;
+                    uint32_t W[4], xw[4], ti[4], i0[4], i1[4], addr[4];
+                    bool act[4], pend[4];
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t x = w0 + 64u * uint32_t(u) + uint32_t(lane);
+                        act[u] = x < btot;
+                        xw[u] = act[u] ? x : btot - 1u;
+                    }
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t wd = xw[u] >> 5;
+                        ti[u] = wpw[wd] + __popc(sbw[wd] & ((2u << (xw[u] & 31u)) - 1u)) - 1u;
+                    }
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        i0[u] = d0w[ti[u]];
+                        i1[u] = d1w[ti[u]];
+                    }
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t jj = xw[u] - (i0[u] & 0x7ffu);
+                        const bool copy = ((i0[u] >> 11) & 1u) == X2_COPY;
+                        const uint32_t offv = max(i0[u] >> 16, 1u);
+                        const uint32_t r = (i0[u] & (1u << 12)) ? mod_small(jj & 63u, offv) : jj;
+                        const uint32_t y = i1[u] + r;                 // copy: absolute output position of the source byte
+                        pend[u] = act[u] && copy && y >= s1;          // produced in this window
+                        addr[u] = copy ? (y & XRMASK) : (i1[u] + jj);
+                        W[u] = 0x100u | ((y - s1) & 0xffu);
+                    }
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t vv = uint32_t(L[addr[u]]);
+                        W[u] = pend[u] ? W[u] : (act[u] ? vv : 0u);
+                    }
+                    while (__any(((W[0] | W[1] | W[2] | W[3]) & 0x100u) != 0u)) {
+                        #pragma unroll
+                        for (int u = 0; u < 4; u++) jv[64u * uint32_t(u) + uint32_t(lane)] = uint16_t(W[u]);
+                        uint32_t G[4];
+                        #pragma unroll
+                        for (int u = 0; u < 4; u++) G[u] = jv[W[u] & 0xffu];
+                        #pragma unroll
+                        for (int u = 0; u < 4; u++) W[u] = (W[u] & 0x100u) ? G[u] : W[u];
+                    }
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (act[u]) ring[(s1 + 64u * uint32_t(u) + uint32_t(lane)) & XRMASK] = uint8_t(W[u]);
+                }
+                flush_slots(ring, od, F, s0 + btot, lane);
+                cop = s0 + btot;
+                asm volatile("s_waitcnt vmcnt(1)" ::: "memory");   // all but the newest store have landed
+            } else if (kind == R5_LONG) {
+                const uint32_t sl = __builtin_amdgcn_readfirstlane(REC[pb][3]);
+                for (uint32_t d0 = 0; d0 < btot; d0 += XLIT) {
+                    const uint32_t c = min(btot - d0, XLIT);
+                    const uint32_t b0 = uint32_t(lane) * 16u;
+                    if (b0 < c) {
+                        uint8_t by[16];
+                        #pragma unroll
+                        for (int u = 0; u < 16; u++) by[u] = b0 + u < c ? gin[sl + d0 + b0 + u] : uint8_t(0);
+                        #pragma unroll
+                        for (int u = 0; u < 16; u++)
+                            if (b0 + u < c) ring[(s0 + d0 + b0 + u) & XRMASK] = by[u];
+                    }
+                    flush_slots(ring, od, F, s0 + d0 + c, lane);
+                }
+                cop = s0 + btot;
+                wait_vmem();
+            } else {
+                wait_vmem();
+            }
+        }
+        x5_barrier();
+        last = __builtin_amdgcn_readfirstlane(REC[b][0]);
+        if (last >= R5_END) break;
+    }
+    if (last == R5_BAD) {
+        if (threadIdx.x == 0) atomicMax(&fb[j], whole ? FB_SERIAL : FB_REDO);
+        return;
+    }
+    if (wv == 1) {   // tail: bytes [F, cop)
+        for (uint32_t a = F + uint32_t(lane) * 16u; a + 16u <= cop; a += 1024u)
+            put16(od, a, *reinterpret_cast<const u32x4*>(ring + (a & XRMASK)));
+        for (uint32_t a = F + ((cop - F) & ~15u) + uint32_t(lane); a < cop; a += 64) put1(od, a, ring[a & XRMASK]);
+    }
+}
+
 #ifdef PF_STAMPS
 extern "C" int pf_debug_stamps(unsigned long long* out, int n, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_stamps), sizeof(unsigned long long) * (n < 16 ? n : 16)) != hipSuccess) return -1;
@@ -1440,9 +1783,16 @@ void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins
 void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
                         int* d_fb, DevChunkResult* d_res, hipStream_t s) {
     if (n_jobs <= 0) return;
-    hipLaunchKernelGGL(k_snappy_exec2, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
-    // whole-page redo of pages whose pieces were not independent
-    hipLaunchKernelGGL(k_snappy_exec2, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
+    // PF_EXEC=2: the one-wave executor (k_snappy_exec2); default: producer / consumer waves
+    static const bool one_wave = [] { const char* e = std::getenv("PF_EXEC"); return e && e[0] == '2'; }();
+    if (one_wave) {
+        hipLaunchKernelGGL(k_snappy_exec2, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
+        // whole-page redo of pages whose pieces were not independent
+        hipLaunchKernelGGL(k_snappy_exec2, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
+    } else {
+        hipLaunchKernelGGL(k_snappy_exec5, dim3(n_pieces), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
+        hipLaunchKernelGGL(k_snappy_exec5, dim3(n_jobs), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
+    }
     launch_snappy_serial(d_jobs, n_jobs, d_fb, d_res, s);
 }
 
