@@ -217,12 +217,14 @@ def units_for_rank(args, pf, world, rank, S, batch=None):
         # of adding up. A column heavier than a context's fair share is cut into that many slices of
         # its row groups; slices go longest-processing-time first (compressed bytes) to the least
         # loaded context.
-        size = {(p, c): chunk_cost(pf, p, c, getattr(args, "lpt_cost", "compressed")) for _, p, _ in units for c in cols}
+        sw = getattr(args, "string_weight", 1.0)
+        size = {(p, c): chunk_cost(pf, p, c, getattr(args, "lpt_cost", "compressed")) *
+                (sw if pf.columns[c].physical_type == 6 else 1.0) for _, p, _ in units for c in cols}
         cost = {c: sum(size[(p, c)] for _, p, _ in units) for c in cols}
         share = sum(cost.values()) / S
         slices = []
         for c in cols:
-            k = max(1, min(len(units), -(-cost[c] // max(1, int(share)))))
+            k = max(1, min(len(units), int(-(-cost[c] // max(1, int(share))))))
             for j in range(k):
                 us = units[j::k]
                 slices.append((sum(size[(p, c)] for _, p, _ in us), c, [(g, p) for g, p, _ in us]))
@@ -368,7 +370,7 @@ def measure_pmc(args, kernel_re):
         cmd = [prof, "--pmc", cnt, "--kernel-include-regex", kernel_re, "--output-format", "csv", "-d", d, "-o", "run",
                "--", sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
                "--data-dir", args.data_dir, "--streams", str(args.streams), "--split", args.split, "--pool", str(args.pool),
-               "--string-ctx", str(args.string_ctx), "--lpt-cost", args.lpt_cost]
+               "--string-ctx", str(args.string_ctx), "--lpt-cost", args.lpt_cost, "--string-weight", str(args.string_weight)]
         t0 = time.time()
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
         log(f"[bench] rocprofv3 --pmc {cnt}: rc {r.returncode} in {time.time() - t0:.1f}s")
@@ -683,6 +685,8 @@ def main():
                     help="sf1: give each context all row groups of a column subset (default), the same with "
                          "BYTE_ARRAY and fixed-width columns on separate contexts (kinds), or whole row groups")
     ap.add_argument("--string-ctx", type=int, default=2, help="--split kinds: contexts for the BYTE_ARRAY columns")
+    ap.add_argument("--string-weight", type=float, default=1.0,
+                    help="--split columns: LPT cost multiplier of BYTE_ARRAY chunks (their value walk, chars count and copy)")
     ap.add_argument("--lpt-cost", choices=("decompressed", "compressed"), default="compressed",
                     help="sf1 --split columns: the per-chunk cost the column slices are dealt by")
     ap.add_argument("--columns", default=None, help=argparse.SUPPRESS)   # analysis only: comma-separated column subset

@@ -1809,7 +1809,9 @@ __device__ inline void copy_chars_short(const uint32_t* coff, const uint32_t* cs
     }
 }
 
+constexpr uint32_t DSTR_CAP = 256;   // string dictionaries up to this many entries: {pos, len} staged in LDS
 struct FlatLds {
+    uint32_t dpos[DSTR_CAP], dlen[DSTR_CAP];
     Run drun[RUN_CAP];
     Run vrun[RUN_CAP];
     uint32_t coff[FT];
@@ -2275,6 +2277,13 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
         }
         if (tid == 0) { S.nvrun = int(nr); S.vcover = cov; S.vlo = 0; S.vres = cov >= ne ? 0 : 1; }
     }
+    // small string dictionaries: {pos, len} from LDS (visible after the tile loop's first barrier)
+    const bool dstage = binary && dict && ck.dict_pos != nullptr && ck.dict_n > 0 && ck.dict_n <= int64_t(DSTR_CAP);
+    if (dstage) {
+        const PF_GLOBAL uint32_t* gp = gptr(ck.dict_pos);
+        const PF_GLOBAL uint32_t* gl = gptr(ck.dict_len);
+        for (uint32_t i = uint32_t(tid); i < uint32_t(ck.dict_n); i += NT) { S.dpos[i] = gp[i]; S.dlen[i] = gl[i]; }
+    }
     __syncthreads();
 #ifdef PF_STAMPS
     unsigned long long ft1 = __builtin_amdgcn_s_memtime();
@@ -2396,24 +2405,53 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
                         else *reinterpret_cast<uint32_t*>(dst) = uint32_t(dv[gv]);
                     }
                 } else if (present) {
+                    // strings: ids / positions of all FEPT entries first (their loads in flight
+                    // together), the dictionary {pos, len} gathers in a second pass
                     const uint64_t gv = vidx + vo + j;
-                    uint32_t src = 0, l = 0;
                     if (dict) {
                         if (vr < 0) vr = run_find(S.vrun, S.nvrun, uint32_t(gv));
                         while (gv >= uint64_t(S.vrun[vr].first) + S.vrun[vr].count) vr++;
-                        const uint32_t id = run_value(S.vrun[vr], ids, ids_n, uint32_t(gv), id_bw);
-                        if (int64_t(id) >= ck.dict_n) bad = 1;
-                        else { src = ck.dict_pos[id]; l = ck.dict_len[id]; }
-                    } else {   // PLAIN: value positions from the k_ba walk
-                        const uint32_t p = pg.aux[gv];
-                        const uint32_t ln = (p >= 4 && p <= s.val_n) ? ld32le(s.val, p - 4, s.val_n) : 0xffffffffu;
-                        if (ln <= s.val_n - p) { src = p; l = ln; }
+                        const Run R = S.vrun[vr];
+                        uint32_t id = R.data;
+                        if (R.packed) {
+                            const uint64_t bit = uint64_t(R.data) + uint64_t(uint32_t(gv) - R.first) * uint64_t(id_bw);
+                            id = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
+                                                          : bits_le(ids, ids_n, bit, id_bw);
+                        }
+                        my_src[k] = id;
+                        my_len[k] = 1;   // present (the length comes from the dictionary)
+                    } else {   // PLAIN: value positions from the k_ba walk; a value's length is the
+                               // distance to the next position (the walk checked the chain), the
+                               // page's last value reads its length prefix
+                        const PF_GLOBAL uint32_t* ax = gptr(pg.aux);
+                        const uint32_t p = ax[gv];
+                        uint32_t ln;
+                        if (split && gv + 1 < uint64_t(ne)) {
+                            const uint32_t nx = ax[gv + 1];
+                            ln = nx >= p + 4 ? nx - p - 4 : 0xffffffffu;
+                        } else {
+                            ln = (p >= 4 && p <= s.val_n) ? ld32le(s.val, p - 4, s.val_n) : 0xffffffffu;
+                        }
+                        if (p >= 4 && p <= s.val_n && ln <= s.val_n - p) { my_src[k] = p; my_len[k] = ln; lsum += ln; }
                         else bad = 1;
                     }
+                    j++;
+                }
+            }
+            if (binary && dict) {
+                const PF_GLOBAL uint32_t* gp = gptr(ck.dict_pos);
+                const PF_GLOBAL uint32_t* gl = gptr(ck.dict_len);
+                #pragma unroll
+                for (uint32_t k = 0; k < FEPT; k++) {
+                    if (!my_len[k]) continue;
+                    const uint32_t id = my_src[k];
+                    uint32_t src = 0, l = 0;
+                    if (int64_t(id) >= ck.dict_n) bad = 1;
+                    else if (dstage) { src = S.dpos[id]; l = S.dlen[id]; }
+                    else { src = gp[id]; l = gl[id]; }
                     my_src[k] = src;
                     my_len[k] = l;
                     lsum += l;
-                    j++;
                 }
             }
         }
@@ -2488,7 +2526,10 @@ __global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks
 // with the fixed-width body when that applies, else with the general body. One stage instead of
 // two in stream order (the fixed-width columns' blocks no longer wait for the string blocks or the
 // other way round); the LDS of the two bodies is shared (they never run in one block together).
-__global__ __launch_bounds__(NT, 4) void k_flat_all(const DevChunk* __restrict__ chunks, DevPage* pages,
+#ifndef PF_FLAT_OCC
+#define PF_FLAT_OCC 4
+#endif
+__global__ __launch_bounds__(NT, PF_FLAT_OCC) void k_flat_all(const DevChunk* __restrict__ chunks, DevPage* pages,
                                                  const int2* __restrict__ blocks, DevChunkResult* res) {
     __shared__ union FlatAllLds {
         FixedLds f;
