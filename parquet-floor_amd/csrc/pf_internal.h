@@ -45,7 +45,9 @@ struct SnappyJob {
     uint32_t lit;         // FB_LITCOPY: the page's literal count (their table is in tokmap)
 };
 
-enum : int32_t { DONE_FIXED = 1, DONE_FLAT = 2, DONE_NULL = 4 };
+// DONE_PAGE: k_page_null decoded the whole page (with DONE_NULL); k_lvl and k_flat_null skip only
+// such pages -- never DONE_NULL itself, which k_flat_null's own finished blocks of the page set.
+enum : int32_t { DONE_FIXED = 1, DONE_FLAT = 2, DONE_NULL = 4, DONE_PAGE = 8 };
 
 // DevPage.direct (k_snappy_head): how the page's decompressed body reaches the decoders
 enum : int32_t { DIRECT_NONE = 0, DIRECT_VALUES = 1, DIRECT_INPLACE = 2 };

@@ -2620,7 +2620,7 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
     Sections s;
-    if (pg.done & DONE_NULL) {   // k_page_null decoded the page
+    if (pg.done & DONE_PAGE) {   // k_page_null decoded the page
         if (tid == 0) LT[1] = 0;
         return;
     }
@@ -2865,10 +2865,14 @@ struct NullLds {
 // dictionary, <= NULL_DICT_LDS; 0 when the batch has none) are staged in LDS and gathered from there
 // (north_star K3: "dictionary staged in LDS when it fits"); larger ones are gathered from L2 / HBM.
 __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                                   const int2* __restrict__ blocks, DevChunkResult* res, uint32_t dlds) {
+                                                   const int2* __restrict__ blocks, DevChunkResult* res, uint32_t dlds,
+                                                   int stagger) {
     __shared__ __attribute__((aligned(16))) NullLds S;
     extern __shared__ __attribute__((aligned(16))) uint64_t DL[];
     const int2 pbk = blocks[blockIdx.x];
+    // diagnostics (tests): blocks after a page's first start late, after it has finished
+    if (stagger && pbk.y > 0)
+        for (int i = 0; i < stagger; i++) __builtin_amdgcn_s_sleep(127);
     if (pbk.x < 0) return;   // padding of the XCD-grouped block list (runtime)
 #ifdef PF_STAMPS   // phase cycles per block: 0 blocks, 1 tables, 2 LDS stage, 3 levels + scan, 4 gather + store
     unsigned long long t_ph = __builtin_amdgcn_s_memtime(), t_beg = t_ph;
@@ -2883,7 +2887,8 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     const int tid = threadIdx.x;
     const uint32_t* LT = pg.lvltab;
     if (!LT || res[pg.chunk].status != 0 || ck.max_rep != 0 || (ck.width != 4 && ck.width != 8) ||
-        (pg.done & (DONE_FIXED | DONE_NULL)) || LT[1] != 1u)   // (other widths: k_flat / k_decode; k_page_null took it)
+        (pg.done & (DONE_FIXED | DONE_PAGE)) || LT[1] != 1u)   // (other widths: k_flat / k_decode; k_page_null took it)
+        // (not DONE_NULL: blocks of this page that finished first set it, and a block starting later must still run)
         return;
     Sections s;
     if (!page_sections(pg, ck, s)) return;
@@ -3389,7 +3394,7 @@ __global__ __launch_bounds__(PN_NT) void k_page_null(const DevChunk* __restrict_
     }
     if (tid == 0) {
         if (ck.needs_count == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&res[pg.chunk].num_values), (unsigned long long)vbase);
-        atomicOr(&pg.done, DONE_NULL);
+        atomicOr(&pg.done, DONE_NULL | DONE_PAGE);
     }
 }
 
@@ -4043,8 +4048,10 @@ void launch_runs(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
 void launch_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                 hipStream_t st) {
     if (n <= 0) return;
-    // PF_PAGE_NULL=0: every nullable page through k_lvl + k_flat_null (A/B, tests)
-    static const bool page_null = [] { const char* e = std::getenv("PF_PAGE_NULL"); return !(e && e[0] == '0'); }();
+    // PF_PAGE_NULL=1: k_page_null first (one 512-thread workgroup and ~57 KiB of LDS per page; under the
+    // bench's four streams its workgroups wait for whole CUs: config 4 5.57 ms with it, 4.47 without)
+    const char* pe = std::getenv("PF_PAGE_NULL");   // (read per launch: tests switch it in-process)
+    const bool page_null = pe && pe[0] == '1';
     if (page_null) hipLaunchKernelGGL(k_page_null, dim3(n), dim3(PN_NT), 0, st, d_chunks, d_pages, d_list, d_res);
     hipLaunchKernelGGL(k_lvl, dim3(n), dim3(LT_NT), 0, st, d_chunks, d_pages, d_list, d_res);
 }
@@ -4055,7 +4062,10 @@ void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
     // pages with nulls first (k_flat_null marks them DONE_NULL), then every other page in one launch
     static const bool no_dl = [] { const char* e = std::getenv("PF_NULL_DICT_LDS"); return e && e[0] == '0'; }();
     const uint32_t dl = no_dl ? 0u : null_dict_lds;
-    if (nullable) hipLaunchKernelGGL(k_flat_null, dim3(n), dim3(NTN), dl, st, d_chunks, d_pages, blocks, d_res, dl);
+    // PF_DEBUG_NULL_STAGGER=k (tests): k_flat_null's blocks > 0 of a page wait k sleep rounds (~3 us each)
+    const char* se = std::getenv("PF_DEBUG_NULL_STAGGER");   // (read per launch: tests set it in-process)
+    const int stagger = se ? std::atoi(se) : 0;
+    if (nullable) hipLaunchKernelGGL(k_flat_null, dim3(n), dim3(NTN), dl, st, d_chunks, d_pages, blocks, d_res, dl, stagger);
     static const bool split = [] { const char* e = std::getenv("PF_FLAT_SPLIT"); return e && e[0] == '1'; }();
     if (split) {   // A/B: the two kernels in stream order
         hipLaunchKernelGGL(k_flat_fixed, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);

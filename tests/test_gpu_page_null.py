@@ -16,6 +16,19 @@ from golden_util import assert_chunk_equal
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(scope="module", autouse=True)
+def page_null_on():
+    """k_page_null is opt-in (PF_PAGE_NULL=1, read per launch): this module tests it."""
+    import os
+    old = os.environ.get("PF_PAGE_NULL")
+    os.environ["PF_PAGE_NULL"] = "1"
+    yield
+    if old is None:
+        os.environ.pop("PF_PAGE_NULL", None)
+    else:
+        os.environ["PF_PAGE_NULL"] = old
+
+
 @pytest.fixture(scope="module")
 def decoder():
     from pfloor.decoder import GpuDecoder
@@ -88,3 +101,48 @@ def test_page_null_many_runs(decoder, oracle, tmp_path):
     assert got["_status"] == 0, got["_error"]
     with oracle.open(path) as of:
         assert_chunk_equal(got[(0, 0)], of.decode(0, 0), "many level runs")
+
+
+@pytest.mark.parametrize("page_null", ["0", "1"])
+def test_null_blocks_staggered(decoder, oracle, tmp_path, monkeypatch, page_null):
+    """Blocks after a page's first start only once it has finished (PF_DEBUG_NULL_STAGGER), with
+    k_page_null off (every page through k_lvl + k_flat_null) and on: bit-exact vs the oracle. r04
+    regression: a k_flat_null block skipped its page (values and count lost) once a sibling block
+    had finished and set DONE_NULL -- under the bench's four streams most config-4 runs hit it;
+    k_page_null now marks the pages it decodes DONE_PAGE and k_flat_null tests only that."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from pfloor.decoder import decode_file
+    monkeypatch.setenv("PF_PAGE_NULL", page_null)
+    monkeypatch.setenv("PF_DEBUG_NULL_STAGGER", "100")
+    rng = np.random.default_rng(5)
+    n = 60_000
+    cols = {}
+    for c, typ in enumerate((np.int32, np.int64, np.float64)):
+        pool = rng.integers(-2**31, 2**31 - 1, 3000).astype(typ)
+        cols[f"c{c}"] = pa.array(pool[rng.integers(0, len(pool), n)], mask=rng.random(n) < 0.3)
+    cols["p"] = pa.array(rng.integers(0, 1 << 40, n), mask=rng.random(n) < 0.3)   # PLAIN (no dictionary)
+    path = str(tmp_path / "stagger.parquet")
+    pq.write_table(pa.table(cols), path, compression="snappy", row_group_size=n,
+                   use_dictionary=["c0", "c1", "c2"])
+    got = decode_file(path, decoder=decoder)
+    assert got["_status"] == 0, got["_error"]
+    with oracle.open(path) as of:
+        for c in range(4):
+            assert_chunk_equal(got[(0, c)], of.decode(0, c), f"column {c} page_null={page_null}")
+
+
+@pytest.mark.parametrize("page_null", ["0", "1"])
+def test_null_blocks_concurrent(tmp_path, page_null):
+    """Two contexts decoding nullable multi-block pages at once, with k_page_null off (every page
+    through k_lvl + k_flat_null) and on: bit-exact vs the oracle every time. r04 regression: a
+    k_flat_null block skipped its page (values and count lost) when a sibling block of the same
+    page had already finished and set DONE_NULL; k_page_null now marks its pages DONE_PAGE."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, PF_PAGE_NULL=page_null)
+    w = os.path.join(os.path.dirname(os.path.abspath(__file__)), "null_race_worker.py")
+    r = subprocess.run([sys.executable, w, str(tmp_path / "race.parquet")], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
