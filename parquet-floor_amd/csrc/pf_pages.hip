@@ -2101,16 +2101,17 @@ __device__ __forceinline__ bool flat_fixed_block(FixedLds& S, const DevChunk* __
                                  DevChunkResult* res) {
     if (pbk.x < 0) return true;   // padding of the XCD-grouped block list (runtime)
     const int pi = pbk.x;
-    const uint32_t blk = uint32_t(pbk.y);
+    const uint32_t blk = uint32_t(pbk.y) & 0x0fffffffu;
+    const uint32_t bsz = FBLK << (uint32_t(pbk.y) >> 28);   // entries per block (runtime: wide blocks for no-null pages)
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
     if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.ptype == 6 || (pg.done & DONE_NULL)) return false;
     if (pg.direct == DIRECT_VALUES && pg.jfb != nullptr && *pg.jfb <= FB_WHOLE) {
         // the executor wrote the values (k_snappy_head checked the levels): this block's validity bits
-        const uint32_t ne = uint32_t(pg.num_values), e_begin = uint32_t(pbk.y) * FBLK;
-        if (e_begin >= ne && pbk.y > 0) return true;
-        const uint32_t e_end = min(ne, e_begin + FBLK);
+        const uint32_t ne = uint32_t(pg.num_values), e_begin = blk * bsz;
+        if (e_begin >= ne && blk > 0) return true;
+        const uint32_t e_end = min(ne, e_begin + bsz);
         if (ck.max_def > 0 && ck.validity && e_end > e_begin) {
             const uint64_t b0 = uint64_t(pg.entry_start) + e_begin, b1 = uint64_t(pg.entry_start) + e_end;
             uint32_t* vw = reinterpret_cast<uint32_t*>(ck.validity);
@@ -2140,7 +2141,7 @@ __device__ __forceinline__ bool flat_fixed_block(FixedLds& S, const DevChunk* __
     else take = false;
     if (!take) return false;
     const uint32_t ne = uint32_t(pg.num_values);
-    if (blk > 0 && blk * FBLK >= ne) return true;
+    if (blk > 0 && blk * bsz >= ne) return true;
     const int id_bw = (dict && s.val_n > 0) ? int(s.val[0]) : 0;
     const uint8_t* ids = dict && s.val_n > 0 ? s.val + 1 : s.val;
     const uint64_t ids_n = dict && s.val_n > 0 ? s.val_n - 1 : 0;
@@ -2150,8 +2151,8 @@ __device__ __forceinline__ bool flat_fixed_block(FixedLds& S, const DevChunk* __
         S.allp = tab ? 1 : (ck.max_def == 0 ? 1 : all_present(s.def, s.def_n, bit_width(ck.max_def), ne, uint32_t(ck.max_def)));
     __syncthreads();
     if (!S.allp) return false;
-    const uint32_t e_begin = blk * FBLK;
-    const uint32_t e_end = min(ne, e_begin + FBLK);
+    const uint32_t e_begin = blk * bsz;
+    const uint32_t e_end = min(ne, e_begin + bsz);
 #ifdef PF_STAMPS
     const unsigned long long ft0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2210,7 +2211,8 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
                            DevChunkResult* res) {
     if (pbk.x < 0) return;   // padding of the XCD-grouped block list (runtime)
     const int pi = pbk.x;
-    const uint32_t blk = uint32_t(pbk.y);
+    const uint32_t blk = uint32_t(pbk.y) & 0x0fffffffu;
+    const uint32_t bsz = FBLK << (uint32_t(pbk.y) >> 28);   // (wide blocks: fixed-width pages only)
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
@@ -2236,15 +2238,15 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
     const uint64_t ids_n = dict && s.val_n > 0 ? s.val_n - 1 : 0;
     const bool counted = ck.needs_count != 0;
     const uint64_t slot_base = uint64_t(pg.entry_start);   // flat: slot == entry
-    if (blk > 0 && blk * FBLK >= ne) return;
+    if (blk > 0 && blk * bsz >= ne) return;
     const uint32_t* T = pg.runtab;
     const bool tab = T != nullptr && T[3] == 1u && T[0] <= uint32_t(RUN_CAP);   // k_runs: levels all present
     if (tid == 0) S.allp = tab ? 1 : (ck.max_def == 0 ? 1 : all_present(s.def, s.def_n, bwd, ne, uint32_t(ck.max_def)));
     __syncthreads();
     const bool split = S.allp;
     if (!split && blk > 0) return;                          // block 0 decodes the whole page
-    const uint32_t e_begin = split ? blk * FBLK : 0u;
-    const uint32_t e_end = split ? min(ne, e_begin + FBLK) : ne;
+    const uint32_t e_begin = split ? blk * bsz : 0u;
+    const uint32_t e_end = split ? min(ne, e_begin + bsz) : ne;
 #ifdef PF_STAMPS
     const unsigned long long ft0 = __builtin_amdgcn_s_memtime();
     if (tid == 0) { PSTAMP(0, 1); if (dict) PSTAMP(6, 1); if (binary) PSTAMP(7, 1); }
@@ -2881,7 +2883,7 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
 #define NSTAMP(i) ((void)0)
 #endif
     const int pi = pbk.x;
-    const uint32_t blk = uint32_t(pbk.y);
+    const uint32_t blk = uint32_t(pbk.y) & 0x0fffffffu;   // (pages with a level table always have FBLK blocks)
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
