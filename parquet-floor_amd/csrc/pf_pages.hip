@@ -498,6 +498,154 @@ __global__ __launch_bounds__(NT) void k_ba_link(BaJob* __restrict__ jobs, const 
     }
 }
 
+// k_ba_cand + k_ba_link (both levels) + k_ba_count + k_ba_verify's chain check in one kernel per tile
+// (round 4). The links of a position come from candidates at most BA_HALO bytes before it, so a tile
+// computes candidates over [t0 - 2 BA_HALO, t1 + BA_HALO), first links over [t0 - BA_HALO, t1 +
+// BA_HALO) and second links over [t0, t1 + BA_HALO) from one staged window (LDS bitmaps, no global
+// atomics); positions both tiles see get the same bits. It writes the tile's accepted words and count,
+// and checks the chain locally: every accepted value of the tile must end exactly at the next accepted
+// position (and the job's first accepted position is 0); with the count check of k_ba_scan that is
+// k_ba_verify's test. A value longer than BA_HALO - 4 bytes is not linked here: its page fails the count
+// or the chain check and takes the exact fallback walk, like any page the filters cannot separate, so
+// the emitted positions are always the verified true chain.
+constexpr int BA_HALO = 128;
+constexpr uint32_t BA_XW = (2 * BA_HALO) / 32;                       // halo words before the tile
+constexpr uint32_t BA_NW = BA_XW + BA_TILE / 32 + BA_HALO / 32;        // words of the window
+constexpr uint32_t BA_FSTAGE = 3 * BA_HALO + BA_TILE + 48;           // staged bytes from t0 - 2 BA_HALO
+__global__ __launch_bounds__(NT) void k_ba_tile(BaJob* __restrict__ jobs, const int2* __restrict__ tiles) {
+    __shared__ __attribute__((aligned(16))) uint8_t stg[BA_FSTAGE + 16];
+    __shared__ uint32_t C[BA_NW], L1[BA_NW], L2[BA_NW];
+    __shared__ uint32_t tmp[NT / 64];
+    const int2 jt = tiles[blockIdx.x];
+    BaJob& J = jobs[jt.x];
+    if (J.state != BA_OK) return;
+    const uint32_t n = J.n;
+    const uint32_t t0 = uint32_t(jt.y) * BA_TILE;
+    if (t0 >= n) {
+        if (threadIdx.x == 0) J.tile_cnt[jt.y] = 0;
+        return;
+    }
+    const uint8_t* p = J.p;
+    const int64_t sb = int64_t(t0) - 2 * BA_HALO;   // stream position of word 0 / stage byte woff
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(p) + uintptr_t(sb);
+    const uint32_t woff = uint32_t(a0 & 15u);
+    {   // 16-byte loads; chunks wholly before the stream start or at / past its end are zero (the chunk
+        // holding byte 0 is read whole, as ba_stage does)
+        const int64_t first = sb - int64_t(woff);
+        const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(a0 - woff);
+        for (uint32_t c = threadIdx.x; c < (BA_FSTAGE + 16) / 16; c += NT) {
+            const int64_t q = first + int64_t(c) * 16;
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (q + 16 > 0 && q < int64_t(n)) v = src[c];
+            reinterpret_cast<u32x4*>(stg)[c] = v;
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < BA_NW; i += NT) { C[i] = 0; L1[i] = 0; L2[i] = 0; }
+    __syncthreads();
+    auto len_at = [&](int64_t q) { return lds_le32(stg, woff + uint32_t(q - sb)); };   // q in the window
+    // ---- candidates (k_ba_cand's rule)
+    for (uint32_t w = threadIdx.x; w < BA_NW; w += NT) {
+        const int64_t q0 = sb + int64_t(w) * 32;
+        if (q0 + 32 <= 0 || q0 >= int64_t(n)) continue;
+        const uint32_t a = woff + w * 32u;
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(stg + (a & ~3u));
+        const uint32_t s = a & 3u;
+        uint32_t D[10], E[9];
+        #pragma unroll
+        for (int i = 0; i < 10; i++) D[i] = d[i];
+        #pragma unroll
+        for (int i = 0; i < 9; i++) E[i] = __builtin_amdgcn_alignbyte(D[i + 1], D[i], s);
+        const int64_t room = int64_t(n) - q0 - 4;
+        uint64_t fit = 0;
+        #pragma unroll
+        for (int b = 0; b <= 32; b++) {
+            const uint32_t l = (b & 3) == 0 ? E[b >> 2] : __builtin_amdgcn_alignbyte(E[(b >> 2) + 1], E[b >> 2], b & 3);
+            fit |= uint64_t(int64_t(l) <= room - b && q0 + b >= 0) << b;
+        }
+        uint64_t m = 0;
+        for (uint64_t f = fit; f;) {
+            const int b = __ffsll((unsigned long long)f) - 1;
+            f &= f - 1;
+            const int64_t q = q0 + b;
+            const uint32_t sv = uint32_t(q) + 4 + len_at(q);
+            bool ok = sv == n;
+            if (!ok && uint64_t(sv) + 4 <= n) {
+                const int64_t r = int64_t(sv) - sb;
+                const uint32_t ls = r + 4 <= int64_t(BA_FSTAGE) ? lds_le32(stg, woff + uint32_t(r)) : ld32le(p, sv, n);
+                ok = ls <= n - sv - 4;
+            }
+            m |= uint64_t(ok) << b;
+        }
+        C[w] = uint32_t(m & ~(m >> 1));
+    }
+    __syncthreads();
+    const int64_t wend = sb + int64_t(BA_NW) * 32;   // end of the window
+    // ---- first links: successors (within the halo) of candidates, over [t0 - BA_HALO, wend)
+    for (uint32_t w = threadIdx.x; w < BA_NW; w += NT) {
+        uint32_t mm = C[w];
+        while (mm) {
+            const uint32_t b = uint32_t(__ffs(mm) - 1);
+            mm &= mm - 1;
+            const int64_t q = sb + int64_t(w) * 32 + b;
+            const int64_t sv = q + 4 + int64_t(len_at(q));
+            if (sv - q <= BA_HALO && sv >= int64_t(t0) - BA_HALO && sv < wend && sv < int64_t(n)) {
+                const uint32_t r = uint32_t(sv - sb);
+                atomicOr(&L1[r >> 5], 1u << (r & 31u));
+            }
+        }
+    }
+    if (threadIdx.x == 0 && t0 == 0) atomicOr(&L1[BA_XW], 1u);   // position 0 starts the chain
+    __syncthreads();
+    // ---- second links: successors of candidates that are first links, over [t0, wend)
+    for (uint32_t w = BA_XW / 2 + threadIdx.x; w < BA_NW; w += NT) {
+        uint32_t mm = C[w] & L1[w];
+        while (mm) {
+            const uint32_t b = uint32_t(__ffs(mm) - 1);
+            mm &= mm - 1;
+            const int64_t q = sb + int64_t(w) * 32 + b;
+            const int64_t sv = q + 4 + int64_t(len_at(q));
+            if (sv - q <= BA_HALO && sv >= int64_t(t0) && sv < wend && sv < int64_t(n)) {
+                const uint32_t r = uint32_t(sv - sb);
+                atomicOr(&L2[r >> 5], 1u << (r & 31u));
+            }
+        }
+    }
+    if (threadIdx.x == 0 && t0 == 0) atomicOr(&L2[BA_XW], 1u);
+    __syncthreads();
+    // ---- accepted = candidates & second links: the tile's words, its count, the local chain check
+    const uint32_t w = BA_XW + threadIdx.x;
+    const uint32_t acc = C[w] & L2[w];
+    const uint32_t wi = t0 / 32 + threadIdx.x;
+    J.cand[wi] = C[w];
+    J.link2[wi] = L2[w];
+    bool bad = t0 == 0 && threadIdx.x == 0 && !(acc & 1u);   // the chain starts at position 0
+    for (uint32_t mm = acc; mm && !bad;) {
+        const uint32_t b = uint32_t(__ffs(mm) - 1);
+        mm &= mm - 1;
+        const int64_t q = sb + int64_t(w) * 32 + b;
+        const int64_t sv = q + 4 + int64_t(len_at(q));
+        // a value ending past the halo cannot be checked here (the exact walk takes the page)
+        if (sv != int64_t(n) && sv - q > BA_HALO) { bad = true; break; }
+        // the next accepted position after q must be sv: no accepted bit in (q, min(sv, wend)), bit sv set
+        const int64_t stop = min(sv, wend);
+        for (int64_t x = q + 1; x < stop;) {
+            const uint32_t r = uint32_t(x - sb), ww = r >> 5;
+            const uint32_t word = (C[ww] & L2[ww]) >> (r & 31u);
+            const int64_t span = min(int64_t(32 - (r & 31u)), stop - x);
+            if (word & (span >= 32 ? 0xffffffffu : ((1u << span) - 1u))) { bad = true; break; }
+            x += span;
+        }
+        if (!bad && sv < wend && sv < int64_t(n)) {
+            const uint32_t r = uint32_t(sv - sb);
+            bad = !(((C[r >> 5] & L2[r >> 5]) >> (r & 31u)) & 1u);
+        }
+    }
+    uint32_t tot;
+    block_excl_scan<NT>(__popc(acc), tmp, tot);
+    if (threadIdx.x == 0) J.tile_cnt[jt.y] = tot;
+    if (__syncthreads_or(bad) && threadIdx.x == 0) atomicExch(&J.state, int32_t(BA_FALLBACK));
+}
+
 __global__ __launch_bounds__(NT) void k_ba_count(BaJob* __restrict__ jobs, const int2* __restrict__ tiles) {
     __shared__ uint32_t tmp[NT / 64];
     const int2 jt = tiles[blockIdx.x];
@@ -552,7 +700,11 @@ __global__ __launch_bounds__(NT) void k_ba_emit(BaJob* __restrict__ jobs, const 
         m &= m - 1;
         if (k < count) {
             J.pos[k] = q + 4;
-            if (J.len) J.len[k] = ld32le(J.p, q, n);
+            if (J.len || k + 1 == count) {
+                const uint32_t l = ld32le(J.p, q, n);
+                if (J.len) J.len[k] = l;
+                if (k + 1 == count && J.chars_out) *J.chars_out = int64_t(q) + 4 + int64_t(l) - 4 * int64_t(count);
+            }
         }
         k++;
     }
@@ -602,6 +754,7 @@ __global__ __launch_bounds__(NT) void k_ba_fallback(BaJob* __restrict__ jobs, in
 }
 
 // ---- values helpers ------------------------------------------------------------------------
+constexpr uint32_t DSTR_CAP = 256;   // string dictionaries up to this many entries: {pos, len} staged in LDS
 constexpr uint32_t FBLK = 4096;      // entries per k_flat workgroup: pages are split into blocks
 
 // BYTE_ARRAY data pages: chars of the entries before each FBLK block (k_count, dictionary pages),
@@ -1506,6 +1659,7 @@ __global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ 
                                                    const int* __restrict__ page_list, DevChunkResult* res,
                                                    BaJob* bajobs) {
     __shared__ Run R[RUN_CAP];
+    __shared__ uint32_t s_len[DSTR_CAP];   // lengths of small dictionaries
     __shared__ int s_ok;
     __shared__ unsigned long long s_acc;
     const int pi = page_list[blockIdx.x];
@@ -1538,14 +1692,24 @@ __global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ 
         const int id_bw = int(s.val[0]);
         uint64_t* bc = flat_block_chars(pg);
         int bad = 0;
+        const bool lstage = ck.dict_n > 0 && ck.dict_n <= int64_t(DSTR_CAP);
+        if (lstage)
+            for (uint32_t i = tid; i < uint32_t(ck.dict_n); i += NT) s_len[i] = gptr(ck.dict_len)[i];
         __syncthreads();
+        constexpr int EPB = int(FBLK) / NT;   // entries of a block per thread
         for (uint32_t b0 = 0; b0 < ne; b0 += FBLK) {
             const uint32_t b1 = min(ne, b0 + FBLK);
             if (tid == 0) s_acc = 0;
             __syncthreads();
             uint64_t acc = 0;
+            // ids of the thread's EPB entries first (their loads in flight together), then the lengths
+            uint32_t idk[EPB];
             int r = -1;
-            for (uint32_t e = b0 + uint32_t(tid); e < b1; e += NT) {
+            #pragma unroll
+            for (int k = 0; k < EPB; k++) {
+                const uint32_t e = b0 + uint32_t(k) * NT + uint32_t(tid);
+                idk[k] = 0xffffffffu;
+                if (e >= b1) continue;
                 if (r < 0) r = run_find(R, int(nr), e);
                 while (e >= R[r].first + R[r].count) r++;
                 const Run& Rr = R[r];
@@ -1556,8 +1720,11 @@ __global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ 
                                                   : bits_le(ids, ids_n, bit, id_bw);
                 }
                 if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
-                acc += ck.dict_len[id];
+                idk[k] = id;
             }
+            #pragma unroll
+            for (int k = 0; k < EPB; k++)
+                if (idk[k] != 0xffffffffu) acc += lstage ? s_len[idk[k]] : gptr(ck.dict_len)[idk[k]];
             atomicAdd(&s_acc, (unsigned long long)acc);
             __syncthreads();
             if (tid == 0 && bc) bc[b0 / FBLK] = total;
@@ -1809,7 +1976,6 @@ __device__ inline void copy_chars_short(const uint32_t* coff, const uint32_t* cs
     }
 }
 
-constexpr uint32_t DSTR_CAP = 256;   // string dictionaries up to this many entries: {pos, len} staged in LDS
 struct FlatLds {
     uint32_t dpos[DSTR_CAP], dlen[DSTR_CAP];
     Run drun[RUN_CAP];
@@ -3923,15 +4089,24 @@ void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list,
     hipLaunchKernelGGL(k_count, dim3(std::min(n, 64)), dim3(NT), 0, st, d_chunks, d_pages, d_list, n, d_res, d_bajobs);
 }
 // PLAIN BYTE_ARRAY walks of jobs [0, n_jobs) over tiles [0, n_tiles).
-void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevChunkResult* d_res, hipStream_t st) {
+void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevChunkResult* d_res, hipStream_t st,
+               bool short_values) {
     if (n_jobs <= 0 || n_tiles <= 0) return;
-    hipLaunchKernelGGL(k_ba_cand, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
-    hipLaunchKernelGGL(k_ba_link, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles, 1);
-    hipLaunchKernelGGL(k_ba_link, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles, 2);
-    hipLaunchKernelGGL(k_ba_count, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
+    // candidates, both link levels, the count and the chain check in one kernel (k_ba_tile) for batches
+    // of short values; otherwise (or PF_BA_FUSED=0) the round-3 kernels
+    const char* fe = std::getenv("PF_BA_FUSED");
+    const bool fused = short_values && !(fe && fe[0] == '0');
+    if (!fused) {
+        hipLaunchKernelGGL(k_ba_cand, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
+        hipLaunchKernelGGL(k_ba_link, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles, 1);
+        hipLaunchKernelGGL(k_ba_link, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles, 2);
+        hipLaunchKernelGGL(k_ba_count, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
+    } else {
+        hipLaunchKernelGGL(k_ba_tile, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
+    }
     hipLaunchKernelGGL(k_ba_scan, dim3(n_jobs), dim3(NT), 0, st, d_jobs);
     hipLaunchKernelGGL(k_ba_emit, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
-    hipLaunchKernelGGL(k_ba_verify, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
+    if (!fused) hipLaunchKernelGGL(k_ba_verify, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
     hipLaunchKernelGGL(k_ba_fallback, dim3(std::min(n_jobs, 64)), dim3(NT), 0, st, d_jobs, n_jobs, d_res);
 }
 // Diagnostics (tests/test_gpu_runs.py): walk_runs (one lane) and wave_walk_runs (one wave) over the

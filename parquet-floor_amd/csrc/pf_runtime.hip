@@ -29,7 +29,7 @@ void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, 
 void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, int*, int,
                          hipStream_t);
 void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*, DevChunkResult*, hipStream_t);
-void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t);
+void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t, bool);
 void launch_snappy_head(SnappyJob*, int, DevPage*, const DevChunk*, int*, const DevChunkResult*, hipStream_t);
 void launch_snappy_litcopy(const SnappyJob*, const int*, int, const int*, hipStream_t);
 void launch_delta(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
@@ -168,6 +168,7 @@ struct pf_ctx {
     std::vector<BaJob> bajobs;             // PLAIN BYTE_ARRAY walks: dictionary pages, then data pages
     std::vector<int2> ba_tiles;            // (job relative to its batch, tile)
     int n_ba_dict = 0, n_ba_dict_tiles = 0;
+    bool ba_short_dict = true, ba_short_data = true;   // every walk job's values average <= BA_SHORT bytes: k_ba_tile
     uint32_t null_dict_lds = 0;            // bytes of the largest nullable-page dictionary that fits k_flat_null's LDS stage
     int max_snap_win = 1;                  // index windows of the batch's largest Snappy job (k_snappy_chain's tables)
     uint32_t n_splits = 0;
@@ -291,7 +292,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     const int2* d_batiles = reinterpret_cast<const int2*>(meta + ctx->off_batiles);
     const int n_ba = int(ctx->bajobs.size()), n_bt = int(ctx->ba_tiles.size());
     (void)d_dictbin;
-    if (!(skip & 4u)) launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st);
+    if (!(skip & 4u)) launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st, ctx->ba_short_dict);
     EVREC(ctx, ctx->ev[4], st);
     launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), ctx->max_dbp_nwin, d_res, st);
     EVREC(ctx, ctx->ev[5], st);
@@ -304,7 +305,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_nest_count(d_chunks, d_pages, d_nest, n_nest, d_nseg, n_nseg, d_res, st);
     if (!(skip & 4u))
         launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
-                  d_res, st);
+                  d_res, st, ctx->ba_short_data);
     EVREC(ctx, ctx->ev[7], st);
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
@@ -1136,6 +1137,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     // ---- PLAIN BYTE_ARRAY walk jobs: dictionary pages first, then PLAIN data pages ----
     ctx->bajobs.clear();
     ctx->ba_tiles.clear();
+    ctx->ba_short_dict = ctx->ba_short_data = true;
+    // k_ba_tile links values of up to ~124 bytes within a tile; pages of longer values would all take
+    // the exact fallback walk there, so a batch with such pages keeps the multi-kernel walk
+    constexpr uint64_t BA_SHORT = 48;
     std::vector<size_t> ba_bm;
     for (int pass = 0; pass < 2; pass++) {
         for (size_t i = 0; i < ctx->pages.size(); i++) {
@@ -1155,6 +1160,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             const int rel = int(ctx->bajobs.size()) - (pass == 0 ? 0 : ctx->n_ba_dict);
             for (uint32_t t = 0; t < J.n_tiles; t++) ctx->ba_tiles.push_back(int2{rel, int(t)});
             if (pass == 1) pg.ba_job = int32_t(ctx->bajobs.size());
+            if (uint64_t(pg.body_len) > BA_SHORT * uint64_t(std::max<int64_t>(1, pg.num_values)))
+                (pass == 0 ? ctx->ba_short_dict : ctx->ba_short_data) = false;
             ctx->bajobs.push_back(J);
         }
         if (pass == 0) { ctx->n_ba_dict = int(ctx->bajobs.size()); ctx->n_ba_dict_tiles = int(ctx->ba_tiles.size()); }

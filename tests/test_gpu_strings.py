@@ -52,3 +52,36 @@ def test_plain_strings(decoder, oracle, tmp_path, mix, version, nulls):
     assert got["_status"] == 0, got["_error"]
     with oracle.open(path) as of:
         assert_chunk_equal(got[(0, 0)], of.decode(0, 0), f"plain {mix} v{version} nulls={nulls}")
+
+
+@pytest.mark.parametrize("version", ["1.0", "2.0"])
+def test_plain_strings_rare_long(decoder, oracle, tmp_path, version):
+    """Short values with a few long ones (page average under k_ba_tile's 48-byte limit, some values
+    past its 124-byte halo): the fused walk cannot link those values, the page takes the exact
+    fallback walk; a second, all-long column in the same batch sends the batch to the round-3 walk
+    kernels. Both columns bit-exact vs the oracle (k_ba_tile, round 4)."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from pfloor.decoder import decode_file
+    rng = np.random.default_rng(17)
+    n = 40_000
+    alphabet = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz ,.0123456789", np.uint8)
+
+    def strings(lens):
+        chars = alphabet[rng.integers(0, len(alphabet), int(lens.sum()))].tobytes()
+        offs = np.concatenate([[0], np.cumsum(lens)])
+        return [chars[offs[i]:offs[i + 1]].decode() for i in range(len(lens))]
+
+    short = rng.integers(8, 30, n)
+    short[rng.random(n) < 0.01] = rng.integers(200, 900)
+    t = pa.table({"a": pa.array(strings(short), type=pa.string()),
+                  "b": pa.array(strings(rng.integers(100, 300, n // 8)) * 8, type=pa.string())})
+    path = str(tmp_path / f"rare_long_{version}.parquet")
+    pq.write_table(t, path, compression="snappy", data_page_version=version, use_dictionary=False,
+                   row_group_size=n, data_page_size=256 << 10)
+    for cols in ([0], [0, 1]):
+        got = decode_file(path, columns=cols, decoder=decoder)
+        assert got["_status"] == 0, got["_error"]
+        with oracle.open(path) as of:
+            for c in cols:
+                assert_chunk_equal(got[(0, c)], of.decode(0, c), f"rare long v{version} col {c} of {cols}")
