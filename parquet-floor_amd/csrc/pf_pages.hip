@@ -1276,6 +1276,13 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
 constexpr int FT = PF_FT;            // entries per tile (fewer registers per thread, more blocks resident)
 constexpr int FEPT = FT / NT;        // consecutive entries per thread
 static_assert(FT <= int(FBLK) && FBLK % FT == 0 && FEPT <= 32, "tiles divide blocks; a thread's entries fit a 32-bit mask");
+#ifndef PF_FTX
+#define PF_FTX 2048   // SF1 2.936 / 2.936 ms vs 3.000-3.019 with 1024 (4096: 2.93, scratch for the arrays)
+#endif
+constexpr int FTX = PF_FTX;          // tile of the all-present fixed-width path (flat_present_fixed): its
+                                     // tiles' id loads and gathers per thread in flight together
+constexpr int FEPTX = FTX / NT;
+static_assert(FTX <= int(FBLK) && FBLK % FTX == 0, "fixed-width tiles divide blocks");
 #ifndef PF_RUN_CAP
 #define PF_RUN_CAP 256
 #endif
@@ -2092,7 +2099,7 @@ constexpr uint32_t DICT_LDS = PF_DICT_LDS;   // bytes of a fixed-width dictionar
 struct FixedLds {
     uint64_t dict[DICT_LDS / 8 + 1];
     Run vrun[RUN_CAP];
-    uint32_t coff[FT / 64];
+    uint32_t coff[FTX / 64];
     RunWalk vst;
     int nvrun, vres, allp;
     uint32_t vcover, vlo;
@@ -2120,7 +2127,7 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
         __syncthreads();
     }
     for (uint32_t e0 = e_begin, want = 0; e0 < e_end; e0 += want) {
-        want = min(uint32_t(FT), e_end - e0);
+        want = min(uint32_t(FTX), e_end - e0);
         int bad = 0;
         if (dict) {
             if ((S.vlo > e0 || e0 + want > S.vcover) && S.vres == 2) {
@@ -2131,7 +2138,7 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
                     if (tid == 0) S.vres = rr;
                 }
                 __syncthreads();
-                // a tile whose ids need more runs than the table holds (runs shorter than FT / RUN_CAP
+                // a tile whose ids need more runs than the table holds (runs shorter than FTX / RUN_CAP
                 // values): this tile is the part the table covers, the next window starts after it
                 if (S.vres == 2 && S.vcover > e0 && e0 + want > S.vcover) want = S.vcover - e0;
             }
@@ -2147,8 +2154,8 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
 #ifndef PF_FB_DIV
 #define PF_FB_DIV 2
 #endif
-            constexpr uint32_t FB = FEPT / PF_FB_DIV;   // entries per thread per load batch
-            for (uint32_t kb = 0; kb < FEPT; kb += FB) {
+            constexpr uint32_t FB = FEPTX / PF_FB_DIV;   // entries per thread per load batch
+            for (uint32_t kb = 0; kb < FEPTX; kb += FB) {
             uint64_t v[FB];
             uint32_t id[FB];
             #pragma unroll
@@ -2209,7 +2216,7 @@ __device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg,
             }
         } else if (!bad) {
             #pragma unroll 2
-            for (uint32_t k = 0; k < FEPT; k++) {
+            for (uint32_t k = 0; k < FEPTX; k++) {
                 const uint32_t e = e0 + k * NT + uint32_t(tid);
                 if (e >= e0 + want) break;
                 uint8_t* dst = ck.values + (slot_base + e) * uint64_t(w);
