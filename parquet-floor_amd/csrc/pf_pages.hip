@@ -1271,7 +1271,8 @@ __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chun
 // Pages it does not take (run tables full, BIT_PACKED levels, RLE booleans, BYTE_STREAM_SPLIT,
 // corrupt section layout) keep done == 0 and are decoded by k_decode.
 #ifndef PF_FT
-#define PF_FT 1024   // 1024: SF1 step 3.82-3.84 vs 3.94-3.97 ms with 2048, 4.04-4.06 with 512 (tools/gpu_ab_libs.sh)
+#define PF_FT 2048   // r04 (string path; the fixed-width path has FTX): SF1 2.896-2.899 vs 2.938-2.953 ms with
+                     // 1024 (profiles/r04_ab/tune.txt). r02, one tile size for both paths: 1024 beat 2048 (3.82 vs 3.94)
 #endif
 constexpr int FT = PF_FT;            // entries per tile (fewer registers per thread, more blocks resident)
 constexpr int FEPT = FT / NT;        // consecutive entries per thread
