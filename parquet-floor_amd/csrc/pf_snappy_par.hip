@@ -1422,7 +1422,10 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
 // literal or an empty batch), the producer derives from the batch history the frontier below which
 // that guarantees the bytes (and their cache line) are in HBM, and a far copy above it cuts the batch
 // (one empty batch when it is the first token, which only follows a long literal).
-constexpr uint32_t X5_BATCH = 768;                     // output bytes of one batch (ring: + XSLOT + far margin)
+#ifndef PF_X5_BATCH
+#define PF_X5_BATCH 768
+#endif
+constexpr uint32_t X5_BATCH = PF_X5_BATCH;                     // output bytes of one batch (ring: + XSLOT + far margin)
 constexpr uint32_t X5_STG = (XSTAGE + 15u) & ~15u;     // one staged input chunk
 constexpr uint32_t X5_FSL = XFAR * FBUF_W * 4u;        // far-copy source slots of one batch
 constexpr uint32_t X5_STAGE0 = XRING;                  // [ring | stage x2 | far slots x2]: one byte address
