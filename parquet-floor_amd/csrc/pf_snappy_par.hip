@@ -1694,11 +1694,14 @@ __global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restric
                         addr[u] = copy ? (y & XRMASK) : (i1[u] + jj);
                         W[u] = 0x100u | ((y - s1) & 0xffu);
                     }
+                    // the four source reads issued together (every addr is inside L): left to itself the
+                    // compiler sank each read into its lane's branch with a wait of its own
+                    uint32_t vv[4];
                     #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t vv = uint32_t(L[addr[u]]);
-                        W[u] = pend[u] ? W[u] : (act[u] ? vv : 0u);
-                    }
+                    for (int u = 0; u < 4; u++) vv[u] = uint32_t(L[addr[u]]);
+                    asm volatile("" : "+v"(vv[0]), "+v"(vv[1]), "+v"(vv[2]), "+v"(vv[3]));
+                    #pragma unroll
+                    for (int u = 0; u < 4; u++) W[u] = pend[u] ? W[u] : (act[u] ? vv[u] : 0u);
                     while (__any(((W[0] | W[1] | W[2] | W[3]) & 0x100u) != 0u)) {
                         #pragma unroll
                         for (int u = 0; u < 4; u++) jv[64u * uint32_t(u) + uint32_t(lane)] = uint16_t(W[u]);
