@@ -3026,8 +3026,12 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
 // block's level runs, the page's id runs and the level / id bytes the block reads (k_lvl's block
 // table) are all fetched at once into LDS, so the workgroup waits on one round of loads, then on the
 // dictionary gather; no spread step: entry k of a thread takes the value of rank popc(fv & (2^k - 1)).
-constexpr int NTN = 512;
-constexpr int NEPT = FBLK / NTN;   // 8
+#ifndef PF_NTN
+#define PF_NTN 512
+#endif
+constexpr int NTN = PF_NTN;
+constexpr int NEPT = FBLK / NTN;   // 8 (512 threads) or 16 (256)
+static_assert(NEPT % 4 == 0 && NEPT <= 16, "k_flat_null's stores and present masks");
 struct NullLds {
     Run drun[LT_BLOCK_RUNS];
     Run vrun[RUN_CAP];
@@ -3273,11 +3277,12 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
         if (m == NEPT && (reinterpret_cast<uintptr_t>(dst0) & 15u) == 0) {
             u32x4* d4 = reinterpret_cast<u32x4*>(dst0);
             if (w == 4) {
-                d4[0] = u32x4{uint32_t(v[0]), uint32_t(v[1]), uint32_t(v[2]), uint32_t(v[3])};
-                d4[1] = u32x4{uint32_t(v[4]), uint32_t(v[5]), uint32_t(v[6]), uint32_t(v[7])};
+                #pragma unroll
+                for (int q = 0; q < NEPT / 4; q++)
+                    d4[q] = u32x4{uint32_t(v[4 * q]), uint32_t(v[4 * q + 1]), uint32_t(v[4 * q + 2]), uint32_t(v[4 * q + 3])};
             } else {
                 #pragma unroll
-                for (int q = 0; q < 4; q++)
+                for (int q = 0; q < NEPT / 2; q++)
                     d4[q] = u32x4{uint32_t(v[2 * q]), uint32_t(v[2 * q] >> 32), uint32_t(v[2 * q + 1]), uint32_t(v[2 * q + 1] >> 32)};
             }
         } else {
@@ -3328,6 +3333,7 @@ constexpr int PN_NT = 512;
 constexpr uint32_t PN_RUNS = 512;        // level runs held in LDS
 constexpr uint32_t PN_IST = 32768;       // dictionary-id bytes staged in LDS
 constexpr uint32_t PN_MAX_BLOCKS = 16;   // entries <= 16 * FBLK
+constexpr int PN_NEPT = FBLK / PN_NT;    // 8 consecutive entries per thread
 struct PageNullLds {
     uint32_t lv[(LVL_STAGE + 64) / 4];
     uint16_t nxt[LVL_STAGE];
@@ -3457,8 +3463,8 @@ __global__ __launch_bounds__(PN_NT) void k_page_null(const DevChunk* __restrict_
     for (uint32_t b = 0; b < nblk; b++) {
         const uint32_t e_begin = b * FBLK, e_end = min(ne, e_begin + FBLK);
         for (uint32_t i = tid; i < FBLK / 32 + 2; i += PN_NT) S.vbits[i] = 0;
-        const uint32_t e = e_begin + uint32_t(tid) * NEPT;
-        const uint32_t m = e < e_end ? min(uint32_t(NEPT), e_end - e) : 0u;
+        const uint32_t e = e_begin + uint32_t(tid) * PN_NEPT;
+        const uint32_t m = e < e_end ? min(uint32_t(PN_NEPT), e_end - e) : 0u;
         uint32_t fv = 0;
         int bad = 0;
         if (m) {
@@ -3481,16 +3487,16 @@ __global__ __launch_bounds__(PN_NT) void k_page_null(const DevChunk* __restrict_
         uint32_t tv;
         const uint32_t vo = block_excl_scan<PN_NT>(__popc(fv), S.scan_tmp, tv);
         const uint32_t gv0 = vbase + vo;
-        uint32_t idv[NEPT];
+        uint32_t idv[PN_NEPT];
         #pragma unroll
-        for (int k = 0; k < NEPT; k++) idv[k] = 0;
+        for (int k = 0; k < PN_NEPT; k++) idv[k] = 0;
         if (fv) {
             if (dict) {
                 if (gv0 + uint32_t(__popc(fv)) > idcov) bad = 1;
                 int vr = run_find(S.vrun, int(vnr), gv0);
                 uint32_t j = 0;
                 #pragma unroll
-                for (int k = 0; k < NEPT; k++) {
+                for (int k = 0; k < PN_NEPT; k++) {
                     if (!((fv >> k) & 1u)) continue;
                     const uint32_t gv = gv0 + j++;
                     while (vr + 1 < int(vnr) && gv >= S.vrun[vr].first + S.vrun[vr].count) vr++;
@@ -3508,37 +3514,37 @@ __global__ __launch_bounds__(PN_NT) void k_page_null(const DevChunk* __restrict_
                 const uint32_t last = gv0 + uint32_t(__popc(fv)) - 1u;
                 if (uint64_t(last + 1) * uint64_t(w) > s.val_n) bad = 1;
                 #pragma unroll
-                for (int k = 0; k < NEPT; k++) idv[k] = bad ? 0u : min(gv0 + uint32_t(__popc(fv & ((1u << k) - 1u))), last);
+                for (int k = 0; k < PN_NEPT; k++) idv[k] = bad ? 0u : min(gv0 + uint32_t(__popc(fv & ((1u << k) - 1u))), last);
             }
         }
         if (__syncthreads_or(bad)) return;   // (nothing counted or marked: the fallback redoes the page)
-        uint64_t v[NEPT];
+        uint64_t v[PN_NEPT];
         #pragma unroll
-        for (int k = 0; k < NEPT; k++) v[k] = 0;
+        for (int k = 0; k < PN_NEPT; k++) v[k] = 0;
         if (!fv) {
         } else if (galign) {
             if (w == 4) {
                 const PF_GLOBAL uint32_t* g = (const PF_GLOBAL uint32_t*)da;
                 #pragma unroll
-                for (int k = 0; k < NEPT; k++) v[k] = g[idv[k]];
+                for (int k = 0; k < PN_NEPT; k++) v[k] = g[idv[k]];
             } else {
                 const PF_GLOBAL uint64_t* g = (const PF_GLOBAL uint64_t*)da;
                 #pragma unroll
-                for (int k = 0; k < NEPT; k++) v[k] = g[idv[k]];
+                for (int k = 0; k < PN_NEPT; k++) v[k] = g[idv[k]];
             }
         } else {
             #pragma unroll
-            for (int k = 0; k < NEPT; k++) {
+            for (int k = 0; k < PN_NEPT; k++) {
                 const uint8_t* src = reinterpret_cast<const uint8_t*>(da) + uint64_t(idv[k]) * uint64_t(w);
                 v[k] = w == 4 ? uint64_t(ld_u32_any(src)) : ld_u64_any(src);
             }
         }
         #pragma unroll
-        for (int k = 0; k < NEPT; k++)
+        for (int k = 0; k < PN_NEPT; k++)
             if (!((fv >> k) & 1u)) v[k] = 0;
         if (m) {
             uint8_t* dst0 = ck.values + (slot_base + e) * uint64_t(w);
-            if (m == NEPT && (reinterpret_cast<uintptr_t>(dst0) & 15u) == 0) {
+            if (m == PN_NEPT && (reinterpret_cast<uintptr_t>(dst0) & 15u) == 0) {
                 u32x4* d4 = reinterpret_cast<u32x4*>(dst0);
                 if (w == 4) {
                     d4[0] = u32x4{uint32_t(v[0]), uint32_t(v[1]), uint32_t(v[2]), uint32_t(v[3])};
@@ -3561,7 +3567,7 @@ __global__ __launch_bounds__(PN_NT) void k_page_null(const DevChunk* __restrict_
             const uint64_t rb = slot_base + e - abase;
             const uint32_t sh = uint32_t(rb & 31);
             atomicOr(&S.vbits[rb >> 5], fv << sh);
-            if (sh + NEPT > 32 && sh) atomicOr(&S.vbits[(rb >> 5) + 1], fv >> (32 - sh));
+            if (sh + PN_NEPT > 32 && sh) atomicOr(&S.vbits[(rb >> 5) + 1], fv >> (32 - sh));
         }
         __syncthreads();
         if (ck.validity) flush_bits(S.vbits, slot_base + e_begin, e_end - e_begin, ck.validity);
