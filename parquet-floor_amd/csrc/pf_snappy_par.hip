@@ -1790,7 +1790,8 @@ void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_piece
                         int* d_fb, DevChunkResult* d_res, hipStream_t s) {
     if (n_jobs <= 0) return;
     // PF_EXEC=2: the one-wave executor (k_snappy_exec2); default: producer / consumer waves
-    static const bool one_wave = [] { const char* e = std::getenv("PF_EXEC"); return e && e[0] == '2'; }();
+    const char* ee = std::getenv("PF_EXEC");   // (read per launch: tests switch it in-process)
+    const bool one_wave = ee && ee[0] == '2';
     if (one_wave) {
         hipLaunchKernelGGL(k_snappy_exec2, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
         // whole-page redo of pages whose pieces were not independent

@@ -96,3 +96,33 @@ def test_window_boundaries(dec, oracle, seed):
         got, fb = dec.snappy_decompress(oracle.snappy_compress(data, mode=0))
         assert got == data, (size, seed)
         assert fb == 0, (size, seed)
+
+
+def _far_after_literal(seed):
+    """Long literals (incompressible runs) each followed by copies of their own bytes 3.3-4.1 KiB
+    back: the first token after a long literal is a far copy whose source the executor is still
+    writing (exec5 waits one batch for those stores to land), then dense near copies."""
+    rng = np.random.default_rng(seed)
+    out = bytearray()
+    while len(out) < 300_000:
+        lit = rng.integers(0, 256, int(rng.integers(4200, 9000)), dtype=np.uint8).tobytes()
+        out += lit
+        for _ in range(int(rng.integers(1, 6))):
+            back = int(rng.integers(3300, 4100))
+            ln = int(rng.integers(4, 64))
+            out += out[len(out) - back:len(out) - back + ln]
+        out += (np.arange(int(rng.integers(100, 3000)), dtype=np.int32) // 3).tobytes()
+    return bytes(out)
+
+
+@pytest.mark.parametrize("executor", ["5", "2"])
+def test_executors_agree(dec, oracle, monkeypatch, executor):
+    """Both block-parallel executors (PF_EXEC=2: one wave per piece; default: producer / consumer
+    waves) on the seeded payloads and on far copies right after long literals."""
+    monkeypatch.setenv("PF_EXEC", executor)
+    rng = np.random.default_rng(11)
+    cases = dict(_payloads(rng), far1=_far_after_literal(1), far2=_far_after_literal(2))
+    for name, data in cases.items():
+        got, fb = dec.snappy_decompress(oracle.snappy_compress(data, mode=0))
+        assert got == data, (executor, name, len(data))
+        assert fb == 0, (executor, name)
