@@ -2280,8 +2280,13 @@ __device__ __forceinline__ bool flat_fixed_block(FixedLds& S, const DevChunk* __
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
-    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.ptype == 6 || (pg.done & DONE_NULL)) return false;
-    if (pg.direct == DIRECT_VALUES && pg.jfb != nullptr && *pg.jfb <= FB_WHOLE) {
+    // the page's, chunk's and result's words are read in one round (bitwise ors: a short-circuit
+    // chain puts a wait between each load)
+    const int* jfb = pg.jfb;
+    const bool dval = pg.direct == DIRECT_VALUES;
+    const int jf = jfb != nullptr ? *jfb : FB_WHOLE + 1;
+    if ((res[pg.chunk].status != 0) | (ck.max_rep != 0) | (ck.ptype == 6) | ((pg.done & DONE_NULL) != 0)) return false;
+    if (dval & (jf <= FB_WHOLE)) {
         // the executor wrote the values (k_snappy_head checked the levels): this block's validity bits
         const uint32_t ne = uint32_t(pg.num_values), e_begin = blk * bsz;
         if (e_begin >= ne && blk > 0) return true;
@@ -2320,7 +2325,9 @@ __device__ __forceinline__ bool flat_fixed_block(FixedLds& S, const DevChunk* __
     const uint8_t* ids = dict && s.val_n > 0 ? s.val + 1 : s.val;
     const uint64_t ids_n = dict && s.val_n > 0 ? s.val_n - 1 : 0;
     const uint32_t* T = pg.runtab;
-    const bool tab = T != nullptr && T[3] == 1u && T[0] <= uint32_t(RUN_CAP);   // k_runs: levels all present
+    uint32_t t0 = 0, t3 = 0;
+    if (T != nullptr) { t0 = T[0]; t3 = T[3]; }
+    const bool tab = (t3 == 1u) & (t0 <= uint32_t(RUN_CAP));   // k_runs: levels all present
     if (tid == 0)
         S.allp = tab ? 1 : (ck.max_def == 0 ? 1 : all_present(s.def, s.def_n, bit_width(ck.max_def), ne, uint32_t(ck.max_def)));
     __syncthreads();
@@ -2355,7 +2362,7 @@ __device__ __forceinline__ bool flat_fixed_block(FixedLds& S, const DevChunk* __
     }
     // values already in place: the executor decoded the page without falling back (a redo / serial
     // fallback writes the body to scratch instead, and the page is decoded from there)
-    const bool direct = pg.direct == DIRECT_VALUES && pg.jfb != nullptr && *pg.jfb <= FB_WHOLE;
+    const bool direct = dval & (jf <= FB_WHOLE);
     const int err = flat_present_fixed(S, ck, pg, s, dict, boolean, enc, w, ids, ids_n, id_bw,
                                        uint64_t(pg.entry_start), e_begin, e_end, direct);
 #ifdef PF_STAMPS
@@ -2392,7 +2399,7 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
     const int tid = threadIdx.x;
     // DONE_FIXED: k_flat_fixed took the page. Never test DONE_FLAT here: this kernel's own blocks of
     // the same page set it when they finish, and a block that starts later must still run.
-    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || (pg.done & (DONE_FIXED | DONE_NULL))) return;
+    if ((res[pg.chunk].status != 0) | (ck.max_rep != 0) | ((pg.done & (DONE_FIXED | DONE_NULL)) != 0)) return;
     Sections s;
     if (!page_sections(pg, ck, s)) return;                 // k_decode reports it
     const int enc = pg.encoding;
@@ -2414,7 +2421,9 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
     const uint64_t slot_base = uint64_t(pg.entry_start);   // flat: slot == entry
     if (blk > 0 && blk * bsz >= ne) return;
     const uint32_t* T = pg.runtab;
-    const bool tab = T != nullptr && T[3] == 1u && T[0] <= uint32_t(RUN_CAP);   // k_runs: levels all present
+    uint32_t t0 = 0, t3 = 0;
+    if (T != nullptr) { t0 = T[0]; t3 = T[3]; }
+    const bool tab = (t3 == 1u) & (t0 <= uint32_t(RUN_CAP));   // k_runs: levels all present
     if (tid == 0) S.allp = tab ? 1 : (ck.max_def == 0 ? 1 : all_present(s.def, s.def_n, bwd, ne, uint32_t(ck.max_def)));
     __syncthreads();
     const bool split = S.allp;
