@@ -127,7 +127,10 @@ struct WinPub {
     uint64_t e;
     uint64_t pad;
 };
-constexpr uint32_t NEST_WIN = 8192;         // k_nest_lvl window bytes
+#ifndef PF_NEST_WIN
+#define PF_NEST_WIN 2048
+#endif
+constexpr uint32_t NEST_WIN = PF_NEST_WIN;  // k_nest_lvl window bytes (power of two)
 constexpr uint32_t DBP_WIN = 8192;          // k_dbp_pos window bytes
 constexpr int32_t DBP_PAR_MIN = 16384;      // DELTA_BINARY_PACKED pages with at least this many entries go block-parallel
 

@@ -1100,7 +1100,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                                 pp.seg_len = int32_t(sl);
                                 pp.nseg = int32_t(ns);
                                 pp.seg_off = take(scratch, nest_seg_bytes(pp.nseg), 256);
-                                pp.nwin = int32_t((uint64_t(std::max(pd.uncompressed_size, pd.compressed_size)) + NEST_WIN - 1) / NEST_WIN + 1);
+                                // windows over the longer level stream (v2: its length is in the header; v1: the page bounds it)
+                                const uint64_t lvl_bytes = v2 ? uint64_t(std::max(pd.rep_bytes, pd.def_bytes))
+                                                              : uint64_t(std::max(pd.uncompressed_size, pd.compressed_size));
+                                pp.nwin = int32_t((lvl_bytes + NEST_WIN - 1) / NEST_WIN + 1);
                                 pp.pub_off = nest_pub;   // (the window hand-overs of all pages: one block, zeroed per batch)
                                 nest_pub += 2ull * uint64_t(pp.nwin) * sizeof(WinPub);
                             }
