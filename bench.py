@@ -96,9 +96,11 @@ WORKLOADS = {
     "sf100": dict(rows=8_000_000, rg_rows=4_000_000, seed=43, kind="lineitem", batch=1, logical=150),
     "wide": dict(rows=1_000_000, rg_rows=1_000_000, seed=4, kind="wide", batch=1),
     # (configs[4]) l optional LIST<STRUCT<a INT64 (DELTA_BINARY_PACKED), b UTF8 (dictionary)>>, v2 pages
-    "nested": dict(rows=1_000_000, rg_rows=250_000, seed=5, kind="nested", batch=1),
+    # batch 0: the column split (as sf1): 0.84 vs 0.905 ms with one row group per batch (r04)
+    "nested": dict(rows=1_000_000, rg_rows=250_000, seed=5, kind="nested", batch=0),
     # (configs[0]) INT64 / DOUBLE / nullable INT32 / dictionary UTF8, uncompressed
-    "flat": dict(rows=1_000_000, rg_rows=250_000, seed=1, kind="flat", batch=1),
+    # (batch 0: 0.278 vs 0.380 ms with one row group per batch, r04)
+    "flat": dict(rows=1_000_000, rg_rows=250_000, seed=1, kind="flat", batch=0),
 }
 
 
@@ -161,6 +163,12 @@ def chunk_cost(pf, p, c, kind):
     return sum(d.pages[i].uncompressed_size for i in range(d.n_pages))
 
 
+def wl_batch(args):
+    """Row groups per decode batch: the workload's (0 = the column split over all row groups), or --rg-batch."""
+    b = getattr(args, "rg_batch", None)
+    return WORKLOADS[args.workload]["batch"] if b is None else b
+
+
 def units_for_rank(args, pf, world, rank, S, batch=None):
     """This rank's work units (logical rg, physical rg, columns), dealt to S contexts, then grouped
     into decode batches: [[batch, ...] per context], batch = list of units."""
@@ -177,7 +185,7 @@ def units_for_rank(args, pf, world, rank, S, batch=None):
         k = max(1, min(S, len(cols)))
         units = [(g, p, cols[i::k]) for i in range(k)] + units[1:]
     elif getattr(args, "split", "rowgroups") == "kinds" and units and S > 2 and batch is None and \
-            WORKLOADS[args.workload]["batch"] <= 0:
+            wl_batch(args) <= 0:
         # A context's time is the sum of its stages' latencies, and every kind of page it holds adds
         # stages: BYTE_ARRAY columns add the value walk, the chars count and scan and the string
         # gather; fixed-width columns add the run tables and the fixed gather. Keep the kinds apart:
@@ -210,7 +218,7 @@ def units_for_rank(args, pf, world, rank, S, batch=None):
             per += gper
         return [[[(g, p, sorted(cs)) for (g, p), cs in sorted(d.items())]] for d in per if d], n_log, mine
     elif getattr(args, "split", "rowgroups") in ("columns", "kinds") and units and S > 1 and batch is None and \
-            WORKLOADS[args.workload]["batch"] <= 0:
+            wl_batch(args) <= 0:
         # Each context decodes a few columns over the rank's row groups: a stage's latency is set by
         # its slowest item (a heavy column's Snappy pieces, string blocks) more than by how many items
         # it has, so heavy columns go to different contexts and their stage chains overlap instead
@@ -238,7 +246,7 @@ def units_for_rank(args, pf, world, rank, S, batch=None):
         return [[[(g, p, sorted(cs)) for (g, p), cs in sorted(d.items())]] for d in per if d], n_log, mine
     S = max(1, min(S, len(units)))
     per_ctx = [units[k::S] for k in range(S)]
-    bsz = WORKLOADS[args.workload]["batch"] if batch is None else batch
+    bsz = wl_batch(args) if batch is None else batch
     out = []
     for us in per_ctx:
         if bsz <= 0:
@@ -370,7 +378,8 @@ def measure_pmc(args, kernel_re):
         cmd = [prof, "--pmc", cnt, "--kernel-include-regex", kernel_re, "--output-format", "csv", "-d", d, "-o", "run",
                "--", sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
                "--data-dir", args.data_dir, "--streams", str(args.streams), "--split", args.split, "--pool", str(args.pool),
-               "--string-ctx", str(args.string_ctx), "--lpt-cost", args.lpt_cost, "--string-weight", str(args.string_weight)]
+               "--string-ctx", str(args.string_ctx), "--lpt-cost", args.lpt_cost, "--string-weight", str(args.string_weight)] + \
+              (["--rg-batch", str(args.rg_batch)] if args.rg_batch is not None else [])
         t0 = time.time()
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
         log(f"[bench] rocprofv3 --pmc {cnt}: rc {r.returncode} in {time.time() - t0:.1f}s")
@@ -681,6 +690,8 @@ def main():
     ap.add_argument("--data-dir", default=os.environ.get("PF_BENCH_DIR", "/tmp/pfloor_bench"))
     ap.add_argument("--streams", type=int, default=4,
                     help="decode contexts (HIP streams) per GPU; work units are dealt round-robin to them")
+    ap.add_argument("--rg-batch", type=int, default=None,
+                    help="row groups per decode batch (default: the workload's; 0 = each context decodes a few columns over all row groups)")
     ap.add_argument("--split", choices=("columns", "kinds", "rowgroups"), default="columns",
                     help="sf1: give each context all row groups of a column subset (default), the same with "
                          "BYTE_ARRAY and fixed-width columns on separate contexts (kinds), or whole row groups")
