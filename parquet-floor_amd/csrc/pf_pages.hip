@@ -1009,7 +1009,11 @@ struct DecodeRange {
     int nseg;
     uint32_t* buf[3];     // LDS for the segment's rep / def / dictionary-id bytes (stage_seg)
 };
-constexpr uint32_t SEG_LVL_CAP = 8192, SEG_VAL_CAP = 16384;
+#ifndef PF_SEG_LVL_CAP
+#define PF_SEG_LVL_CAP 4096
+#endif
+// LDS for one segment's level / dictionary-id bytes (a segment whose bytes do not fit reads them from HBM)
+constexpr uint32_t SEG_LVL_CAP = PF_SEG_LVL_CAP, SEG_VAL_CAP = 2 * PF_SEG_LVL_CAP;
 
 __device__ __forceinline__ void decode_page(const DevChunk* __restrict__ chunks, DevPage* pages, const int pi, DevChunkResult* res,
                             DecodeLds& S, const DecodeRange* R = nullptr) {
