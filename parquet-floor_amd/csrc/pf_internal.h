@@ -131,7 +131,10 @@ struct WinPub {
 #define PF_NEST_WIN 2048
 #endif
 constexpr uint32_t NEST_WIN = PF_NEST_WIN;  // k_nest_lvl window bytes (power of two)
-constexpr uint32_t DBP_WIN = 8192;          // k_dbp_pos window bytes
+#ifndef PF_DBP_WIN
+#define PF_DBP_WIN 4096
+#endif
+constexpr uint32_t DBP_WIN = PF_DBP_WIN;    // k_dbp_pos window bytes (power of two)
 constexpr int32_t DBP_PAR_MIN = 16384;      // DELTA_BINARY_PACKED pages with at least this many entries go block-parallel
 
 // One segment of a nested page: its level counts (k_count_seg), their exclusive prefixes over the
