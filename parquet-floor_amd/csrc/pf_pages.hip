@@ -4070,7 +4070,10 @@ __global__ __launch_bounds__(64) void k_nest_chars(const DevChunk* __restrict__ 
     if (lane == 0) pg.n_chars = int64_t(cc);
 }
 
-__global__ __launch_bounds__(NT) void k_decode_seg(const DevChunk* __restrict__ chunks, DevPage* pages,
+#ifndef PF_DSEG_WAVES
+#define PF_DSEG_WAVES 4
+#endif
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PF_DSEG_WAVES))) void k_decode_seg(const DevChunk* __restrict__ chunks, DevPage* pages,
                                                    const int2* __restrict__ list, DevChunkResult* res) {
     __shared__ DecodeLds S;
     __shared__ uint32_t bufR[SEG_LVL_CAP / 4], bufD[SEG_LVL_CAP / 4], bufV[SEG_VAL_CAP / 4];
