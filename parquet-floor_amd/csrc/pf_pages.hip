@@ -3761,11 +3761,15 @@ constexpr int NL_NT = 256;
 constexpr uint32_t NL_END = 0xFFFFFFu;        // exit field: the chain ends inside the window (no run at its last position)
 constexpr uint32_t NL_FAR = 0xFFFFFEu;        // exit field: leaves the window for a position >= w0 + NL_FAR (exact exit by a walk)
 constexpr uint64_t NL_CMAX = (1ull << 40) - 1;   // count field saturates (the exact count is then walked)
+constexpr uint32_t NL_JNONE = 0xFFFu, NL_JCMAX = 0xFFFFFu;   // J: no exit inside the window; saturated entries
+static_assert(NEST_WIN <= 2048, "J packs window-relative exits in 12 bits");
 __global__ __launch_bounds__(NL_NT) void k_nest_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
                                                     DevChunkResult* res) {
     __shared__ __attribute__((aligned(16))) uint32_t st[(NEST_WIN + 64) / 4];
     __shared__ uint64_t X[NEST_WIN];   // per position: entries to the exit << 24 | exit (window-relative, NL_END, NL_FAR)
-    __shared__ uint64_t J[NEST_WIN];   // the same after 5 rounds: jumps over >= 32 runs (or to the exit), for the checkpoint walk
+    // the same after 5 rounds, packed in 32 bits: jumps over >= 32 runs (or to the exit), for the checkpoint
+    // walk; exit in the low 12 bits (NL_JNONE: none inside the window), entries (saturating) above
+    __shared__ uint32_t J[NEST_WIN];
     __shared__ uint64_t s_hand[3];
     const int tid = threadIdx.x;
     const int pi = list[blockIdx.z];
@@ -3819,7 +3823,11 @@ __global__ __launch_bounds__(NL_NT) void k_nest_lvl(const DevChunk* __restrict__
         }
         __syncthreads();
         if (span == 16) {
-            for (uint32_t i = tid; i < NEST_WIN; i += NL_NT) J[i] = X[i];
+            for (uint32_t i = tid; i < NEST_WIN; i += NL_NT) {
+                const uint64_t x = X[i];
+                const uint32_t e = uint32_t(x & 0xFFFFFFu);
+                J[i] = (e < NEST_WIN ? e : NL_JNONE) | (uint32_t(min<uint64_t>(x >> 24, NL_JCMAX)) << 12);
+            }
         }
     }
     __syncthreads();
@@ -3879,10 +3887,10 @@ __global__ __launch_bounds__(NL_NT) void k_nest_lvl(const DevChunk* __restrict__
                 const uint64_t t = k * sl;
                 // jump over runs before the target: >= 32 at a time
                 while (true) {
-                    const uint64_t x = J[tp - w0];
-                    const uint32_t e = uint32_t(x & 0xFFFFFFu);
-                    if (e >= NEST_WIN || te + (x >> 24) > t) break;
-                    te += x >> 24;
+                    const uint32_t x = J[tp - w0];
+                    const uint32_t e = x & 0xFFFu, c = x >> 12;
+                    if (e >= NEST_WIN || c == NL_JCMAX || te + c > t) break;   // (saturated: the header walk)
+                    te += c;
                     tp = w0 + e;
                 }
                 HybRun r;
