@@ -904,43 +904,55 @@ __global__ __launch_bounds__(64) void k_snappy_repair(const SnappyJob* __restric
     }
 }
 
-// One wave per page: check the output total, then find the input position of the token that
-// starts at each 64 KiB output boundary (window prefix sums -> lane region -> bitmap walk).
-__global__ __launch_bounds__(64) void k_snappy_splits(const SnappyJob* __restrict__ jobs, const SnapWin* __restrict__ win,
-                                                      const uint32_t* __restrict__ lane_out, uint32_t* __restrict__ splits,
-                                                      int* __restrict__ fb) {
+// One workgroup per page: wave 0 checks the output total (window prefix sums into LDS); then each
+// wave takes pieces in turn and finds the input position of the token that starts at the piece's
+// 64 KiB output boundary with all of its loads issued together: the window's 64 lane-region output
+// counts (one per lane; a ballot picks the region), then the region's 128 bytes (+ 8 for the last
+// token's length bytes) and its 4 token-start bitmap words, then one token per lane position and a
+// wave scan of their output lengths. (Round 3 walked the region counts and the tokens one dependent
+// load at a time per piece: ~50 us per launch.)
+constexpr int SP_NT = 256;
+__global__ __launch_bounds__(SP_NT) void k_snappy_splits(const SnappyJob* __restrict__ jobs, const SnapWin* __restrict__ win,
+                                                         const uint32_t* __restrict__ lane_out, uint32_t* __restrict__ splits,
+                                                         int* __restrict__ fb) {
     __shared__ uint32_t s_pre[FIX_MAXW + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_reg[SP_NT / 64][SNAP_RB + 16];
+    __shared__ uint32_t s_tm[SP_NT / 64][4];
+    __shared__ int s_ok;
     const int j = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const SnappyJob job = jobs[j];
-    if (fb[j] >= FB_SERIAL) return;
+    if (fb[j] >= FB_SERIAL) return;   // (block-uniform)
     const uint32_t nw = job.n_win;
     const uint64_t n = job.src_len;
     const SnapWin* Wn = win + job.win_base;
     const uint32_t* LO = lane_out + size_t(job.win_base) * 64;
-    uint32_t run = 0;
-    bool ovf = false;
-    for (uint32_t w0i = 0; w0i < nw; w0i += 64) {
-        const uint32_t w = w0i + lane;
-        const uint32_t o = w < nw ? Wn[w].out : 0u;
-        uint64_t x = o;
-        #pragma unroll
-        for (int dd = 1; dd < 64; dd <<= 1) {
-            const uint64_t y = __shfl_up(x, dd, 64);
-            if (lane >= dd) x += y;
+    if (wv == 0) {
+        uint32_t run = 0;
+        bool ovf = false;
+        for (uint32_t w0i = 0; w0i < nw; w0i += 64) {
+            const uint32_t w = w0i + lane;
+            const uint32_t o = w < nw ? Wn[w].out : 0u;
+            uint64_t x = o;
+            #pragma unroll
+            for (int dd = 1; dd < 64; dd <<= 1) {
+                const uint64_t y = __shfl_up(x, dd, 64);
+                if (lane >= dd) x += y;
+            }
+            if (w < nw) s_pre[w] = uint32_t(run + x - o);
+            const uint64_t t = uint64_t(run) + __shfl(x, 63, 64);
+            ovf |= t > 0xffffffffull;
+            run = uint32_t(t);
         }
-        if (w < nw) s_pre[w] = uint32_t(run + x - o);
-        const uint64_t t = uint64_t(run) + __shfl(x, 63, 64);
-        ovf |= t > 0xffffffffull;
-        run = uint32_t(t);
-    }
-    if (ovf || run != job.dst_len) {
-        if (lane == 0) fb[j] = FB_SERIAL;
-        return;
+        const bool ok = !ovf && run == job.dst_len;
+        if (lane == 0) { s_ok = ok; if (!ok) fb[j] = FB_SERIAL; }
     }
     __syncthreads();
+    if (!s_ok) return;
     uint32_t* sp = splits + job.split_base;
-    for (uint32_t k = 1 + lane; k < job.n_pieces; k += 64) {
+    uint8_t* R = s_reg[wv];
+    const PF_GLOBAL uint8_t* src = gptr(job.src);
+    for (uint32_t k = 1 + uint32_t(wv); k < job.n_pieces; k += SP_NT / 64) {
         const uint32_t B = k * SNAP_BLOCK;
         uint32_t a = 0, b = nw;   // last window with s_pre <= B
         while (b - a > 1) {
@@ -948,29 +960,62 @@ __global__ __launch_bounds__(64) void k_snappy_splits(const SnappyJob* __restric
             if (s_pre[m] <= B) a = m; else b = m;
         }
         const uint32_t w = a;
-        uint32_t cum = s_pre[w];
-        const uint32_t* lo = LO + size_t(w) * 64;
-        int l = 0;
-        for (; l < 63; l++) {
-            const uint32_t v = lo[l];
-            if (B < cum + v) break;
-            cum += v;
+        // the lane region holding output byte B: the first of regions 0..62 whose end passes B (else 63)
+        const uint32_t v = LO[size_t(w) * 64 + lane];
+        uint64_t x = v;
+        #pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint64_t y = __shfl_up(x, dd, 64);
+            if (lane >= dd) x += y;
         }
+        const uint64_t base = s_pre[w];
+        const uint64_t past = __ballot(lane < 63 && uint64_t(B) < base + x);
+        const int l = past ? __ffsll((unsigned long long)past) - 1 : 63;
+        const uint64_t cum0 = base + __shfl(x - v, l, 64);   // output before region l
+        // the region's bytes (zero past the stream) and its token-start bitmap
         const uint32_t rs = w * SNAP_WIN + uint32_t(l) * SNAP_RB;
-        const uint32_t* tm = job.tokmap + size_t(w) * SNAP_WWORDS + l * 4;
-        uint32_t found = SNAP_INVALID;
-        bool done = false;
-        for (int wd = 0; wd < 4 && !done; wd++) {
-            uint32_t mm = tm[wd];
-            while (mm) {
-                const uint32_t p = rs + uint32_t(wd) * 32 + uint32_t(__ffs(mm) - 1);
-                mm &= mm - 1;
-                if (cum == B) { found = p; done = true; break; }
-                if (cum > B) { done = true; break; }
-                cum += snap_tok(glb_read8(job.src, n, p)).ol;
-            }
+        const uint64_t q0 = uint64_t(rs) + uint32_t(lane), q1 = q0 + 64, q2 = q0 + 128;
+        const uint8_t c0 = q0 < n ? src[q0] : uint8_t(0), c1 = q1 < n ? src[q1] : uint8_t(0);
+        const uint8_t c2 = (lane < 16 && q2 < n) ? src[q2] : uint8_t(0);
+        const uint32_t tw = lane < 4 ? job.tokmap[size_t(w) * SNAP_WWORDS + uint32_t(l) * 4 + uint32_t(lane)] : 0u;
+        R[lane] = c0; R[64 + lane] = c1;
+        if (lane < 16) R[128 + lane] = c2;
+        if (lane < 4) s_tm[wv][lane] = tw;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // one position per lane and half: output length of the token starting there (0: none)
+        uint32_t ol[2];
+        bool st[2];
+        for (int h = 0; h < 2; h++) {
+            const uint32_t i = uint32_t(h) * 64 + uint32_t(lane);
+            st[h] = (s_tm[wv][i >> 5] >> (i & 31)) & 1u;
+            uint64_t t8 = 0;
+            #pragma unroll
+            for (int u = 0; u < 8; u++) t8 |= uint64_t(R[i + u]) << (8 * u);
+            ol[h] = st[h] ? snap_tok(t8).ol : 0u;
         }
-        sp[k] = found;
+        // the first token whose preceding output reaches B: found when it equals B
+        uint32_t found = SNAP_INVALID;
+        uint64_t cum = cum0;
+        for (int h = 0; h < 2; h++) {
+            uint64_t y = ol[h];
+            #pragma unroll
+            for (int dd = 1; dd < 64; dd <<= 1) {
+                const uint64_t z = __shfl_up(y, dd, 64);
+                if (lane >= dd) y += z;
+            }
+            const uint64_t before = cum + y - ol[h];
+            const uint64_t hit = __ballot(st[h] && before >= uint64_t(B));
+            if (hit) {
+                const int f = __ffsll((unsigned long long)hit) - 1;
+                if (__shfl(before, f, 64) == uint64_t(B)) found = rs + uint32_t(h) * 64 + uint32_t(f);
+                break;
+            }
+            cum += __shfl(y, 63, 64);
+        }
+        if (lane == 0) sp[k] = found;
+        __builtin_amdgcn_wave_barrier();   // (the region buffer is rewritten by the next piece)
     }
 }
 
@@ -1782,7 +1827,7 @@ void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins
 #endif
     hipLaunchKernelGGL(k_snappy_repair, dim3(std::min(n_wins, PF_REPAIR_GRID)), dim3(64), 0, s, d_jobs, d_wins, n_wins,
                        (const SnapWin*)d_win, d_lane_out, d_fb);
-    hipLaunchKernelGGL(k_snappy_splits, dim3(n_jobs), dim3(64), 0, s, d_jobs, (const SnapWin*)d_win,
+    hipLaunchKernelGGL(k_snappy_splits, dim3(n_jobs), dim3(SP_NT), 0, s, d_jobs, (const SnapWin*)d_win,
                        (const uint32_t*)d_lane_out, d_splits, d_fb);
 }
 
