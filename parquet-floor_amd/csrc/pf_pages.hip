@@ -885,13 +885,38 @@ __device__ void count_page(const DevChunk* __restrict__ chunks, DevPage* pages, 
 // Grid-stride over the BYTE_ARRAY / nested pages with a small grid: nearly every page is counted by
 // k_count_flat or k_count_seg and skipped here, and a block per page (22 KiB of LDS each) waited for
 // CUs held by the other streams' kernels (13-96 us per no-op launch in the r04 kernel trace).
+// Grid-stride over a batch's page list for kernels most of whose pages are already done: a block
+// tests NT of its pages at once (one round of loads instead of a few dependent loads per page in
+// series) and runs `body` only on those `need` accepts, in turn (page order does not matter: each
+// page writes its own outputs).
+template <typename Need, typename Body>
+__device__ __forceinline__ void stride_pages(const int* page_list, int n, Need need, Body body) {
+    __shared__ int s_idx[NT];
+    __shared__ int s_cnt;
+    for (int c0 = 0; int(blockIdx.x) + c0 * int(gridDim.x) < n; c0 += NT) {
+        const int i = int(blockIdx.x) + (c0 + int(threadIdx.x)) * int(gridDim.x);
+        const int pi = i < n ? page_list[i] : -1;
+        const bool w = pi >= 0 && need(pi);
+        if (threadIdx.x == 0) s_cnt = 0;
+        __syncthreads();
+        if (w) s_idx[atomicAdd(&s_cnt, 1)] = pi;
+        __syncthreads();
+        const int m = s_cnt;
+        for (int k = 0; k < m; k++) {
+            body(s_idx[k]);
+            __syncthreads();
+        }
+        __syncthreads();   // (everyone has read s_cnt before the next round resets it)
+    }
+}
+
 __global__ __launch_bounds__(NT) void k_count(const DevChunk* __restrict__ chunks, DevPage* pages,
                                               const int* page_list, int n, DevChunkResult* res, BaJob* bajobs) {
     __shared__ CountLds C;
-    for (int i = blockIdx.x; i < n; i += gridDim.x) {
-        count_page(chunks, pages, page_list[i], res, bajobs, C);
-        __syncthreads();
-    }
+    // (count_page's own early exits, tested for a block's pages at once)
+    stride_pages(page_list, n,
+                 [&](int pi) { const DevPage& pg = pages[pi]; return (res[pg.chunk].status == 0) & (pg.counted != 1) & (pg.seg_ok != 1); },
+                 [&](int pi) { count_page(chunks, pages, pi, res, bajobs, C); });
 }
 
 // ---- k_scan (one wave per chunk) ------------------------------------------------------------
@@ -900,13 +925,31 @@ __global__ __launch_bounds__(64) void k_scan(DevChunk* chunks, DevPage* pages, c
                                              unsigned long long* arena_used) {
     const int c = chunk_list[blockIdx.x];
     DevChunk& ck = chunks[c];
-    if (threadIdx.x != 0) return;
+    const int lane = threadIdx.x;
+    // page prefixes: 64 pages' counts loaded at once, wave scans (a serial loop put its loads in series)
+    const int np = ck.n_pages, fp = ck.first_page;
     int64_t s = 0, v = 0, r = 0, ch = 0;
-    for (int i = 0; i < ck.n_pages; i++) {
-        DevPage& pg = pages[ck.first_page + i];
-        pg.slot_start = s; pg.value_start = v; pg.row_start = r; pg.char_start = ch;
-        s += pg.n_slots; v += pg.n_values; r += pg.n_rows; ch += pg.n_chars;
+    for (int i0 = 0; i0 < np; i0 += 64) {
+        const int i = i0 + lane;
+        int64_t a[4] = {0, 0, 0, 0};
+        if (i < np) { const DevPage& pg = pages[fp + i]; a[0] = pg.n_slots; a[1] = pg.n_values; a[2] = pg.n_rows; a[3] = pg.n_chars; }
+        int64_t x[4] = {a[0], a[1], a[2], a[3]};
+        #pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            #pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int64_t y = __shfl_up(x[q], d, 64);
+                if (lane >= d) x[q] += y;
+            }
+        }
+        if (i < np) {
+            DevPage& pg = pages[fp + i];
+            pg.slot_start = s + x[0] - a[0]; pg.value_start = v + x[1] - a[1];
+            pg.row_start = r + x[2] - a[2]; pg.char_start = ch + x[3] - a[3];
+        }
+        s += __shfl(x[0], 63, 64); v += __shfl(x[1], 63, 64); r += __shfl(x[2], 63, 64); ch += __shfl(x[3], 63, 64);
     }
+    if (lane != 0) return;
     res[c].num_slots = s; res[c].num_values = v; res[c].num_rows = r; res[c].num_chars = ch;
     if (ck.ptype == 6) {
         if (ch > int64_t(0x7fffffff)) { set_status(res, c, ST_CAPACITY, -1); ck.chars = nullptr; }
@@ -1259,10 +1302,10 @@ __device__ __forceinline__ void decode_page(const DevChunk* __restrict__ chunks,
 __global__ __launch_bounds__(NT) void k_decode(const DevChunk* __restrict__ chunks, DevPage* pages,
                                                const int* page_list, int n, DevChunkResult* res) {
     __shared__ DecodeLds S;
-    for (int i = blockIdx.x; i < n; i += gridDim.x) {
-        decode_page(chunks, pages, page_list[i], res, S);
-        __syncthreads();
-    }
+    // (decode_page's own early exits, tested for a block's pages at once)
+    stride_pages(page_list, n,
+                 [&](int pi) { const DevPage& pg = pages[pi]; return (pg.done == 0) & (pg.seg_ok != 1) & (res[pg.chunk].status == 0); },
+                 [&](int pi) { decode_page(chunks, pages, pi, res, S); });
 }
 
 // ---- k_flat: data pages of flat columns (max_rep == 0) ------------------------------------------
