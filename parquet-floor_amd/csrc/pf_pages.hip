@@ -2843,8 +2843,12 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     // LDS copies of the page's level runs and of its dictionary-id runs (k_runs): the block-table
     // pass below scans them serially, one dependent load per run, which from HBM cost ~1 us each
     __shared__ uint32_t s_runs[4 * LVL_RUNS_LDS];
-    __shared__ uint32_t s_T[4 + 2 * RUN_CAP];
-    __shared__ uint16_t s_nxt[LVL_NXT];   // position of the next run header, per byte position
+    // the next-header table lives only in the chain phase and the id-run copy only after it: one LDS
+    // region (8 KiB instead of 10: nine waves per CU instead of eight)
+    __shared__ union { uint16_t nxt[LVL_NXT]; uint32_t T[4 + 2 * RUN_CAP]; } s_u;
+    static_assert(sizeof(uint16_t) * LVL_NXT >= sizeof(uint32_t) * (4 + 2 * RUN_CAP), "s_u sized by the header table");
+    uint16_t* const s_nxt = s_u.nxt;   // position of the next run header, per byte position
+    uint32_t* const s_T = s_u.T;
     const int pi = list[blockIdx.x];
     DevPage& pg = pages[pi];
     uint32_t* LT = pg.lvltab;
