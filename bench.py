@@ -51,15 +51,19 @@ sys.path.insert(0, os.path.join(ROOT, "parquet-floor_amd"))
 SF1_ROWS = 6001215
 RG_ROWS = 1 << 20
 SEED = 42
-# PF_DEBUG_SKIP (stage ablation, pf_runtime.hip): skipped stages leave chunks failed by design
-_SKIP = bool(os.environ.get("PF_DEBUG_SKIP"))
+# PF_* switches act only on the diagnostics build (PFLOOR_LIB_PATH=parquet-floor_amd/diag/libpfloor_diag.so,
+# PfOpts in pf_internal.h); the product library reads no environment.
+_DIAG = "libpfloor_diag" in os.environ.get("PFLOOR_LIB_PATH", "")
+# PF_DEBUG_SKIP (stage ablation, diagnostics build): skipped stages leave chunks failed by design
+_SKIP = _DIAG and bool(os.environ.get("PF_DEBUG_SKIP"))
+_EXEC = os.environ.get("PF_EXEC", "5")[:1] if _DIAG else "5"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PCIE_GBS = 63.0         # MI355X_MICROARCH.md: PCIe Gen5 x16 per direction
 # kernels of each stage (rocprof names, pf_runtime.hip's launch order between the stage events), for
 # the PMC traffic and the label of the roofline object
 STAGE_KERNELS = {
     "snappy_parse": r"k_snappy_(head|litcopy|index|chain|repair|splits)$",
-    "snappy_exec": r"k_snappy_(exec2|exec5|serial)$",
+    "snappy_exec": r"k_snappy_(exec2|exec5|exec6|serial)$",
     "delta": r"k_(dbp_pos|dbp_blk|dbp_scan|delta)$",
     "levels": r"k_(runs|lvl|dlen)$",
     "count": r"k_(nest_lvl|count|count_flat|count_seg|nest_scan|nest_ids|nest_chars|ba_[a-z]+)$",
@@ -67,8 +71,7 @@ STAGE_KERNELS = {
     "flat": r"k_flat(_all|_fixed|_null)?$",
     "decode": r"k_(decode|decode_seg|dba_chars)$",
 }
-STAGE_LABEL = {"snappy_exec": "Snappy executor stage: %s (+ redo, serial fallback)"
-               % ("k_snappy_exec2" if os.environ.get("PF_EXEC", "")[:1] == "2" else "k_snappy_exec5"),
+STAGE_LABEL = {"snappy_exec": "Snappy executor stage: k_snappy_exec%s (+ redo, serial fallback)" % _EXEC,
                "snappy_parse": "Snappy parse stage: k_snappy_head + index + chain + repair + splits",
                "delta": "DELTA_BINARY_PACKED stage: k_dbp_pos / k_dbp_blk / k_dbp_scan + k_delta",
                "levels": "level / id run stage: k_runs + k_lvl + k_dlen",

@@ -13,6 +13,30 @@
 
 namespace pf {
 
+// Decoder options. The product library (libpfloor.so) always runs these defaults and reads no
+// environment. The diagnostics build (-DPF_DIAG, diag/libpfloor_diag.so) takes them from PF_*
+// environment variables once per context, at pf_ctx_create: A/B selectors for the tools and the
+// switches tests use to force rare paths (forced fallbacks, segment lengths, skipped stages).
+struct PfOpts {
+    int exec = 5;             // PF_EXEC: block-parallel Snappy executor: 5 producer/consumer | 6 LDS image | 2 one wave
+    bool ba_fused = true;     // PF_BA_FUSED=0: the round-3 PLAIN BYTE_ARRAY walk kernels
+    bool page_null = false;   // PF_PAGE_NULL=1: k_page_null before k_lvl
+    bool null_dict_lds = true;   // PF_NULL_DICT_LDS=0: k_flat_null never stages its dictionary
+    int null_stagger = 0;     // PF_DEBUG_NULL_STAGGER=k: k_flat_null's blocks > 0 wait k rounds (race tests)
+    bool flat_split = false;  // PF_FLAT_SPLIT=1: k_flat_fixed + k_flat instead of k_flat_all
+    bool piece_order = true;  // PF_PIECE_ORDER=0: Snappy pieces in page order
+    unsigned debug_skip = 0;  // PF_DEBUG_SKIP=parse,exec,ba,levels,count,flat,decode (results are wrong)
+    int force_serial = 0;     // PF_DEBUG_FORCE_SERIAL=k: every k-th Snappy job to the serial kernel
+    int force_redo = 0;       // PF_DEBUG_FORCE_REDO=k: every k-th Snappy job rejected by the block executor
+    bool exec_stream = false; // PF_EXEC_STREAM=1: the executor on a low-priority stream of its own
+    bool zc = true;           // PF_ZC=0: SDMA copies for the batch tables instead of k_copy_words
+    bool debug_plan = false;  // PF_DEBUG_PLAN=1: host planning phase times on stderr
+    int64_t nest_seg = 0;     // PF_NEST_SEG=n: nested segment length, forced (0: default, not forced)
+    bool nest_seg_set = false;
+    bool dbp_par = true;      // PF_DBP_PAR=0: every DELTA_BINARY_PACKED page on k_delta
+    int fix_shift = 1;        // PF_FIX_BLK=4096|8192|16384: fixed-width flat blocks (log2 of the multiple of 4096)
+};
+
 enum : int32_t {
     PG_V2 = 1,            // DATA_PAGE_V2
     PG_COMPRESSED = 2,    // body lives in scratch after k_snappy

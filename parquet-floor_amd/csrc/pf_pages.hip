@@ -3110,9 +3110,12 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     __shared__ __attribute__((aligned(16))) NullLds S;
     extern __shared__ __attribute__((aligned(16))) uint64_t DL[];
     const int2 pbk = blocks[blockIdx.x];
-    // diagnostics (tests): blocks after a page's first start late, after it has finished
+#ifdef PF_DIAG   // diagnostics build (tests): blocks after a page's first start late, after it has finished
     if (stagger && pbk.y > 0)
         for (int i = 0; i < stagger; i++) __builtin_amdgcn_s_sleep(127);
+#else
+    (void)stagger;
+#endif
     if (pbk.x < 0) return;   // padding of the XCD-grouped block list (runtime)
 #ifdef PF_STAMPS   // phase cycles per block: 0 blocks, 1 tables, 2 LDS stage, 3 levels + scan, 4 gather + store
     unsigned long long t_ph = __builtin_amdgcn_s_memtime(), t_beg = t_ph;
@@ -4178,9 +4181,8 @@ void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevC
                bool short_values) {
     if (n_jobs <= 0 || n_tiles <= 0) return;
     // candidates, both link levels, the count and the chain check in one kernel (k_ba_tile) for batches
-    // of short values; otherwise (or PF_BA_FUSED=0) the round-3 kernels
-    const char* fe = std::getenv("PF_BA_FUSED");
-    const bool fused = short_values && !(fe && fe[0] == '0');
+    // of short values (short_values; the diagnostics option ba_fused=0 clears it); otherwise the round-3 kernels
+    const bool fused = short_values;
     if (!fused) {
         hipLaunchKernelGGL(k_ba_cand, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
         hipLaunchKernelGGL(k_ba_link, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles, 1);
@@ -4308,27 +4310,21 @@ void launch_runs(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
     if (n > 0) hipLaunchKernelGGL(k_runs, dim3(n), dim3(128), 0, st, d_chunks, d_pages, d_list, d_res);
 }
 void launch_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
-                hipStream_t st) {
+                hipStream_t st, bool page_null) {
     if (n <= 0) return;
-    // PF_PAGE_NULL=1: k_page_null first (one 512-thread workgroup and ~57 KiB of LDS per page; under the
-    // bench's four streams its workgroups wait for whole CUs: config 4 5.57 ms with it, 4.47 without)
-    const char* pe = std::getenv("PF_PAGE_NULL");   // (read per launch: tests switch it in-process)
-    const bool page_null = pe && pe[0] == '1';
+    // page_null (diagnostics option): k_page_null first (one 512-thread workgroup and ~57 KiB of LDS per
+    // page; under the bench's four streams its workgroups wait for whole CUs: config 4 5.57 ms with it, 4.47 without)
     if (page_null) hipLaunchKernelGGL(k_page_null, dim3(n), dim3(PN_NT), 0, st, d_chunks, d_pages, d_list, d_res);
     hipLaunchKernelGGL(k_lvl, dim3(n), dim3(LT_NT), 0, st, d_chunks, d_pages, d_list, d_res);
 }
 void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
-                 hipStream_t st, bool nullable, uint32_t null_dict_lds) {   // d_list: n (page, block) pairs
+                 hipStream_t st, bool nullable, uint32_t dl, int stagger, bool split) {   // d_list: n (page, block) pairs
     if (n <= 0) return;
     const int2* blocks = reinterpret_cast<const int2*>(d_list);
     // pages with nulls first (k_flat_null marks them DONE_NULL), then every other page in one launch
-    static const bool no_dl = [] { const char* e = std::getenv("PF_NULL_DICT_LDS"); return e && e[0] == '0'; }();
-    const uint32_t dl = no_dl ? 0u : null_dict_lds;
-    // PF_DEBUG_NULL_STAGGER=k (tests): k_flat_null's blocks > 0 of a page wait k sleep rounds (~3 us each)
-    const char* se = std::getenv("PF_DEBUG_NULL_STAGGER");   // (read per launch: tests set it in-process)
-    const int stagger = se ? std::atoi(se) : 0;
+    // dl: bytes of dictionary k_flat_null stages in LDS; stagger (diagnostics build, tests): blocks > 0 of a
+    // page wait that many sleep rounds (~3 us each) for block 0
     if (nullable) hipLaunchKernelGGL(k_flat_null, dim3(n), dim3(NTN), dl, st, d_chunks, d_pages, blocks, d_res, dl, stagger);
-    static const bool split = [] { const char* e = std::getenv("PF_FLAT_SPLIT"); return e && e[0] == '1'; }();
     if (split) {   // A/B: the two kernels in stream order
         hipLaunchKernelGGL(k_flat_fixed, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
         hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);

@@ -25,10 +25,10 @@
 
 namespace pf {
 void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, const int2*, int, uint32_t*,
-                   int*, DevChunkResult*, int, hipStream_t);
+                   int*, DevChunkResult*, int, int, hipStream_t);
 void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, int*, int,
                          hipStream_t);
-void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*, DevChunkResult*, hipStream_t);
+void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*, DevChunkResult*, int, hipStream_t);
 void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t, bool);
 void launch_snappy_head(SnappyJob*, int, DevPage*, const DevChunk*, int*, const DevChunkResult*, hipStream_t);
 void launch_snappy_litcopy(const SnappyJob*, const int*, int, const int*, hipStream_t);
@@ -37,8 +37,8 @@ void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hi
 void launch_dba_chars(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, BaJob*, hipStream_t);
 void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
-void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool, uint32_t);
-void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
+void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool, uint32_t, int, bool);
+void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool);
 void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
 void launch_nest_lvl(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
@@ -131,6 +131,7 @@ struct Streams {
 
 struct pf_ctx {
     int device = 0;
+    pf::PfOpts opts;                       // defaults; the diagnostics build reads PF_* at creation
     std::shared_ptr<Streams> streams;
     hipStream_t stream = nullptr;          // = streams->stream
     // PF_EXEC_STREAM=1: the Snappy executor runs on a low-priority stream of its own (event-ordered
@@ -254,18 +255,13 @@ int enqueue_kernels(pf_ctx* ctx) {
     int* d_fallback = reinterpret_cast<int*>(meta + ctx->off_fallback);
     const int2* d_wins = reinterpret_cast<const int2*>(meta + ctx->off_wins);
 
-    // diagnostics (bench analysis only, results are wrong): PF_DEBUG_SKIP=parse,exec,ba,levels,count,flat,decode
-    // leaves those stages' kernels out, so a step's time without them shows what they cost under load
-    static const unsigned skip = [] {
-        const char* e = std::getenv("PF_DEBUG_SKIP");
-        unsigned m = 0;
-        if (e) {
-            const char* names[] = {"parse", "exec", "ba", "levels", "count", "flat", "decode"};
-            for (int i = 0; i < 7; i++)
-                if (std::strstr(e, names[i])) m |= 1u << i;
-        }
-        return m;
-    }();
+    // diagnostics build only (bench analysis, results are wrong): stages left out of every batch, so a
+    // step's time without them shows what they cost under load
+#ifdef PF_DIAG
+    const unsigned skip = ctx->opts.debug_skip;
+#else
+    constexpr unsigned skip = 0;
+#endif
     if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
     if (ctx->npub_bytes)
         HIPCHK(ctx, hipMemsetAsync(static_cast<uint8_t*>(ctx->d_scratch.p) + ctx->off_npub, 0, ctx->npub_bytes, st));
@@ -281,23 +277,24 @@ int enqueue_kernels(pf_ctx* ctx) {
         HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->exec_stream, ctx->ev_fork, 0));
         launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res,
-                           ctx->exec_stream);
+                           ctx->opts.exec, ctx->exec_stream);
         HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->exec_stream));
         HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_join, 0));
     } else {
-        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res, st);
+        launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res,
+                           ctx->opts.exec, st);
     }
     EVREC(ctx, ctx->ev[3], st);
     BaJob* d_bajobs = reinterpret_cast<BaJob*>(meta + ctx->off_bajobs);
     const int2* d_batiles = reinterpret_cast<const int2*>(meta + ctx->off_batiles);
     const int n_ba = int(ctx->bajobs.size()), n_bt = int(ctx->ba_tiles.size());
     (void)d_dictbin;
-    if (!(skip & 4u)) launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st, ctx->ba_short_dict);
+    if (!(skip & 4u)) launch_ba(d_bajobs, ctx->n_ba_dict, d_batiles, ctx->n_ba_dict_tiles, d_res, st, ctx->ba_short_dict && ctx->opts.ba_fused);
     EVREC(ctx, ctx->ev[4], st);
     launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), ctx->max_dbp_nwin, d_res, st);
     EVREC(ctx, ctx->ev[5], st);
     if (!(skip & 8u)) launch_runs(d_chunks, d_pages, d_runs, int(ctx->l_runs.size()), d_res, st);
-    if (!(skip & 8u)) launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st);
+    if (!(skip & 8u)) launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st, ctx->opts.page_null);
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
     EVREC(ctx, ctx->ev[6], st);
     launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, ctx->max_nwin, d_res, st);
@@ -305,12 +302,13 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_nest_count(d_chunks, d_pages, d_nest, n_nest, d_nseg, n_nseg, d_res, st);
     if (!(skip & 4u))
         launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
-                  d_res, st, ctx->ba_short_data);
+                  d_res, st, ctx->ba_short_data && ctx->opts.ba_fused);
     EVREC(ctx, ctx->ev[7], st);
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
     EVREC(ctx, ctx->ev[8], st);
-    if (!(skip & 32u)) launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty(), ctx->null_dict_lds);
+    if (!(skip & 32u)) launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty(),
+                                     ctx->opts.null_dict_lds ? ctx->null_dict_lds : 0u, ctx->opts.null_stagger, ctx->opts.flat_split);
     EVREC(ctx, ctx->ev[9], st);
     if (!(skip & 64u)) launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), ctx->n_decode_first, d_res, st);
     launch_nest_decode(d_chunks, d_pages, d_nseg, n_nseg, d_res, st);
@@ -354,7 +352,7 @@ int plan_snappy(pf_ctx* ctx) {
     // Dispatch the pieces with the most compressed bytes per 64 KiB of output first (more tokens per
     // piece -> more executor steps), so the longest pieces do not start last (k_snappy_exec alone
     // 1.50 -> 1.39 ms per launch on SF1). PF_PIECE_ORDER=0 keeps page order (A/B).
-    static const bool lpt = [] { const char* e = std::getenv("PF_PIECE_ORDER"); return !(e && e[0] == '0'); }();
+    const bool lpt = ctx->opts.piece_order;
     std::vector<uint64_t> keyed(lpt ? tp : 0);
     size_t wi = 0, pi = 0;
     for (size_t j = 0; j < ctx->jobs.size(); j++) {
@@ -416,18 +414,16 @@ int upload_meta(pf_ctx* ctx) {
         std::copy(v->begin(), v->end(), lists + lo);
         lo += v->size();
     }
-    {   // diagnostics: PF_DEBUG_FORCE_SERIAL=k sends every k-th Snappy job to the serial kernel
-        // (tests of k_snappy_serial's grid-stride over many jobs; valid streams never fall back)
-        const char* e = std::getenv("PF_DEBUG_FORCE_SERIAL");
-        const int k = e ? std::atoi(e) : 0;
+    {   // diagnostics: force_serial = k sends every k-th Snappy job to the serial kernel (tests of
+        // k_snappy_serial's grid-stride over many jobs; valid streams never fall back)
+        const int k = ctx->opts.force_serial;
         int* fbh = reinterpret_cast<int*>(h + ctx->off_fallback);
         if (k > 0)
             for (size_t j = 0; j < ctx->jobs.size(); j++)
                 if (int(j % size_t(k)) == k - 1) fbh[j] = FB_SERIAL;
-        // PF_DEBUG_FORCE_REDO=k: the block-parallel executor rejects every k-th job (after
-        // k_snappy_head), so direct pages are also decoded through the redo path (tests)
-        const char* r = std::getenv("PF_DEBUG_FORCE_REDO");
-        const int kr = r ? std::atoi(r) : 0;
+        // force_redo = k: the block-parallel executor rejects every k-th job (after k_snappy_head), so
+        // direct pages are also decoded through the redo path (tests)
+        const int kr = ctx->opts.force_redo;
         SnappyJob* jh = reinterpret_cast<SnappyJob*>(h + ctx->off_jobs);
         if (kr > 0)
             for (size_t j = 0; j < ctx->jobs.size(); j++)
@@ -811,15 +807,49 @@ int pf_device_count(int* count) {
 }
 
 namespace {
+#ifdef PF_DIAG
+// Diagnostics build only: the options from the environment (PfOpts, pf_internal.h).
+void opts_from_env(pf::PfOpts& o) {
+    auto on = [](const char* name, bool dflt) { const char* e = std::getenv(name); return e ? e[0] == '1' : dflt; };
+    auto num = [](const char* name, int dflt) { const char* e = std::getenv(name); return e ? std::atoi(e) : dflt; };
+    o.exec = num("PF_EXEC", o.exec);
+    o.ba_fused = on("PF_BA_FUSED", o.ba_fused);
+    o.page_null = on("PF_PAGE_NULL", o.page_null);
+    o.null_dict_lds = on("PF_NULL_DICT_LDS", o.null_dict_lds);
+    o.null_stagger = num("PF_DEBUG_NULL_STAGGER", o.null_stagger);
+    o.flat_split = on("PF_FLAT_SPLIT", o.flat_split);
+    o.piece_order = on("PF_PIECE_ORDER", o.piece_order);
+    if (const char* e = std::getenv("PF_DEBUG_SKIP")) {
+        const char* names[] = {"parse", "exec", "ba", "levels", "count", "flat", "decode"};
+        for (int i = 0; i < 7; i++)
+            if (std::strstr(e, names[i])) o.debug_skip |= 1u << i;
+    }
+    o.force_serial = num("PF_DEBUG_FORCE_SERIAL", o.force_serial);
+    o.force_redo = num("PF_DEBUG_FORCE_REDO", o.force_redo);
+    o.exec_stream = on("PF_EXEC_STREAM", o.exec_stream);
+    o.zc = on("PF_ZC", o.zc);
+    o.debug_plan = on("PF_DEBUG_PLAN", o.debug_plan);
+    if (const char* e = std::getenv("PF_NEST_SEG")) {
+        o.nest_seg = std::atoll(e);
+        o.nest_seg_set = true;
+    }
+    o.dbp_par = on("PF_DBP_PAR", o.dbp_par);
+    const int fb = num("PF_FIX_BLK", 8192);
+    o.fix_shift = fb >= 16384 ? 2 : (fb >= 8192 ? 1 : 0);
+}
+#endif
+
 int ctx_init(pf_ctx* ctx, pf_ctx* peer) {
+#ifdef PF_DIAG
+    opts_from_env(ctx->opts);
+#endif
     HIPCHK(nullptr, hipSetDevice(ctx->device));
     if (peer) {
         ctx->streams = peer->streams;
     } else {
         ctx->streams = std::make_shared<Streams>();
         ctx->streams->device = ctx->device;
-        const char* es = std::getenv("PF_EXEC_STREAM");
-        if (es && es[0] && es[0] != '0') {
+        if (ctx->opts.exec_stream) {
             int least = 0, greatest = 0;
             HIPCHK(nullptr, hipDeviceGetStreamPriorityRange(&least, &greatest));
             HIPCHK(nullptr, hipStreamCreateWithPriority(&ctx->streams->stream, hipStreamNonBlocking, greatest));
@@ -830,10 +860,7 @@ int ctx_init(pf_ctx* ctx, pf_ctx* peer) {
     }
     ctx->stream = ctx->streams->stream;
     ctx->exec_stream = ctx->streams->exec_stream;
-    {
-        const char* z = std::getenv("PF_ZC");
-        ctx->zc = !(z && z[0] == '0');
-    }
+    ctx->zc = ctx->opts.zc;
     if (ctx->exec_stream) {
         HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
@@ -941,7 +968,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     // diagnostics: PF_DEBUG_PLAN=1 prints the host time of each planning phase (microseconds)
-    static const bool dbg_plan = [] { const char* e = std::getenv("PF_DEBUG_PLAN"); return e && e[0] == '1'; }();
+    const bool dbg_plan = ctx->opts.debug_plan;
     using clk = std::chrono::steady_clock;
     clk::time_point tp[8];
     int ntp = 0;
@@ -958,8 +985,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     // eligible nested page, one segment or more, down the segment path (0: none)
     int64_t nest_seg_len = NEST_SEG;
     bool nest_seg_forced = false;
-    if (const char* e = std::getenv("PF_NEST_SEG")) {
-        nest_seg_len = std::atoll(e);
+    if (ctx->opts.nest_seg_set) {
+        nest_seg_len = ctx->opts.nest_seg;
         nest_seg_forced = nest_seg_len > 0;
         if (nest_seg_len <= 0) nest_seg_len = int64_t(1) << 40;   // every page stays on k_count / k_decode
     }
@@ -990,7 +1017,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->max_nwin = 0;
     ctx->max_dbp_nwin = 0;
     // PF_DBP_PAR=0: every DELTA_BINARY_PACKED page on the one-workgroup k_delta (tests)
-    const bool dbp_par = [] { const char* e = std::getenv("PF_DBP_PAR"); return !(e && e[0] == '0'); }();
+    const bool dbp_par = ctx->opts.dbp_par;
     uint64_t chars_hint = 0;
     struct OutPlan { size_t values, validity, offsets, list_offsets, list_validity, def, rep; };
     std::vector<OutPlan> oplan(n_chunks);
@@ -1300,11 +1327,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             // fixed-width pages without a level table (no nulls) take blocks of FLAT_BLK << fix_shift
             // entries (the block index carries the shift in bits 28..31): a block's metadata chain and
             // run-table load are paid once per 8192 entries instead of per 4096 (PF_FIX_BLK=4096|8192|16384)
-            static const int fix_shift = [] {
-                const char* e = std::getenv("PF_FIX_BLK");
-                const int v = e ? std::atoi(e) : 8192;
-                return v >= 16384 ? 2 : (v >= 8192 ? 1 : 0);
-            }();
+            const int fix_shift = ctx->opts.fix_shift;
             const int sh = (ck.ptype != PF_BYTE_ARRAY && pg.lvltab == nullptr) ? fix_shift : 0;
             const int64_t bsz = FLAT_BLK << sh;
             const int nb = std::max(1, int((int64_t(pg.num_values) + bsz - 1) / bsz));
@@ -1690,7 +1713,8 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     launch_snappy(reinterpret_cast<const SnappyJob*>(d + o_job), 1, reinterpret_cast<const int2*>(d + o_wn),
                   int(ctx->wins.size()), ctx->d_win, ctx->d_ent, ctx->d_lane_out, reinterpret_cast<const int2*>(d + o_pc),
                   int(ctx->pieces.size()), reinterpret_cast<uint32_t*>(d + o_sp), reinterpret_cast<int*>(d + o_fb),
-                  reinterpret_cast<DevChunkResult*>(d + o_res), int(ctx->jobs.empty() ? 1 : ctx->jobs[0].n_win), st);
+                  reinterpret_cast<DevChunkResult*>(d + o_res), int(ctx->jobs.empty() ? 1 : ctx->jobs[0].n_win),
+                  ctx->opts.exec, st);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, ctx->h_res.ensure(512));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_res.p, d + o_res, sizeof(DevChunkResult), hipMemcpyDeviceToHost, st));

@@ -3,12 +3,16 @@
 This is the Python analogue of the FFM binding a Java maintainer adds:
 plain C structs, plain pointers, no torch types. Loading fails loudly if the in-tree
 library is missing — there is no CPU fallback on the product path."""
+import contextlib
 import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PFLOOR_LIB_PATH: diagnostics only (e.g. the stamp build from `make stamps`).
 LIB_PATH = os.environ.get("PFLOOR_LIB_PATH") or os.path.join(_HERE, "libpfloor.so")
+# The diagnostics build (`make -C parquet-floor_amd diag`): the same library compiled with -DPF_DIAG,
+# which reads the PF_* switches (include/pfloor.h is unchanged) from the environment at pf_ctx_create.
+DIAG_PATH = os.path.join(os.path.dirname(_HERE), "diag", "libpfloor_diag.so")
 
 PF_OK = 0
 STATUS = {0: "PF_OK", -1: "PF_ERR_INVALID_ARG", -2: "PF_ERR_CORRUPT_PAGE", -3: "PF_ERR_UNSUPPORTED_ENCODING",
@@ -76,17 +80,38 @@ class PfError(RuntimeError):
 
 
 _lib = None
+_loaded = {}
 
 
 def lib():
     """Load libpfloor.so once. Raises if it has not been built (no fallback)."""
     global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"{LIB_PATH} missing: build it with `make -C parquet-floor_amd` "
+    if _lib is None:
+        _lib = _load(LIB_PATH)
+    return _lib
+
+
+@contextlib.contextmanager
+def diagnostics():
+    """Route lib() to the diagnostics build for the duration of the block (tests that force rare paths
+    with PF_* switches, A/B tools). Contexts created inside must be closed inside. Never used by the
+    product path."""
+    global _lib
+    saved = lib()
+    _lib = _load(DIAG_PATH)
+    try:
+        yield _lib
+    finally:
+        _lib = saved
+
+
+def _load(path):
+    if path in _loaded:
+        return _loaded[path]
+    if not os.path.exists(path):
+        raise ImportError(f"{path} missing: build it with `make -C parquet-floor_amd` "
                           "(or __graft_entry__.build()); the HIP path has no CPU fallback")
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     vp, i32, i64p, sz = C.c_void_p, C.c_int, C.POINTER(C.c_int64), C.c_size_t
     sig = {
         "pf_abi_version": ([], C.c_int),
@@ -139,7 +164,7 @@ def lib():
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
-    _lib = L
+    _loaded[path] = L
     return L
 
 

@@ -31,6 +31,27 @@ def oracle():
     return Oracle(lib)
 
 
+@pytest.fixture
+def switches(monkeypatch):
+    """switches(PF_NAME=value, ...): a context in which decoders run the diagnostics build of the
+    library with those PfOpts switches (read at pf_ctx_create; the product library reads no
+    environment). Decoders made inside must be closed inside."""
+    import contextlib
+    from pfloor import _native
+
+    @contextlib.contextmanager
+    def ctx(**env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, str(v))
+        try:
+            with _native.diagnostics():
+                yield
+        finally:
+            for k in env:
+                monkeypatch.delenv(k, raising=False)
+    return ctx
+
+
 def golden_files():
     return sorted(f[:-len(".parquet")] for f in os.listdir(GOLDEN) if f.endswith(".parquet"))
 

@@ -1,9 +1,11 @@
-"""Worker for test_gpu_page_null.py::test_null_blocks_concurrent (runs in its own process so that
-PF_PAGE_NULL=0 is read before the library's first level launch). Two threads, each with its own
+"""Worker for test_gpu_page_null.py::test_null_blocks_concurrent (runs in its own process: with
+PF_PAGE_NULL=1 it decodes on the diagnostics build, where that switch is read at pf_ctx_create; with 0,
+the default, on the product library). Two threads, each with its own
 decode context (HIP stream), decode halves of a wide nullable file together, three times; every
 chunk is compared with the oracle. Under that contention k_flat_null's blocks of one page start at
 different times, which is what the r04 race needed (a block skipping its page once a sibling block
 had finished)."""
+import contextlib
 import os
 import sys
 import threading
@@ -17,6 +19,7 @@ import pyarrow.parquet as pq  # noqa: E402
 
 from golden_util import assert_chunk_equal  # noqa: E402
 from oracle_binding import Oracle  # noqa: E402
+from pfloor import _native  # noqa: E402
 from pfloor.decoder import GpuDecoder, decode_file  # noqa: E402
 
 
@@ -58,4 +61,6 @@ def main(path):
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1]))
+    with (_native.diagnostics() if os.environ.get("PF_PAGE_NULL") == "1" else contextlib.nullcontext()):
+        rc = main(sys.argv[1])
+    sys.exit(rc)

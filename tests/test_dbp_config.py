@@ -164,28 +164,34 @@ def test_gpu_dbp_configs(tmp_path, block, nmini):
 @pytest.mark.gpu
 @pytest.mark.parametrize("block,nmini", CONFIGS_OK)
 @pytest.mark.parametrize("par", ["1", "0"])
-def test_gpu_dbp_large_pages(tmp_path, monkeypatch, block, nmini, par):
+def test_gpu_dbp_large_pages(tmp_path, switches, block, nmini, par):
     from pfloor.decoder import decode_file
-    monkeypatch.setenv("PF_DBP_PAR", par)
     v = _values(n=60001, seed=block + nmini)
     path = str(tmp_path / f"dbp_big_{block}_{nmini}.parquet")
     _write(path, v, block, nmini, junk_tail=True)
-    got = decode_file(path, device=0)
+    if par == "1":   # the default: the product library
+        got = decode_file(path, device=0)
+    else:
+        with switches(PF_DBP_PAR=par):
+            got = decode_file(path, device=0)
     assert got["_status"] == 0, got["_error"]
     assert np.array_equal(np.frombuffer(got[(0, 0)]["values"].tobytes(), np.int64), v)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("par", ["1", "0"])
-def test_gpu_dbp_large_page_bad_width(oracle, tmp_path, monkeypatch, par):
+def test_gpu_dbp_large_page_bad_width(oracle, tmp_path, switches, par):
     from pfloor.decoder import decode_file
-    monkeypatch.setenv("PF_DBP_PAR", par)
     v = _values(n=40000, seed=9)
     path = str(tmp_path / "dbp_big_bad.parquet")
     _write(path, v, 128, 4, bad_block=100)
     with oracle.open(path) as of:
         assert of.decode(0, 0)["status"] != 0
-    assert decode_file(path, device=0)["_status"] != 0
+    if par == "1":
+        assert decode_file(path, device=0)["_status"] != 0
+    else:
+        with switches(PF_DBP_PAR=par):
+            assert decode_file(path, device=0)["_status"] != 0
 
 
 def _paths(decoder):
@@ -268,14 +274,14 @@ def test_gpu_dbp_par_nullable(decoder, oracle, tmp_path, ptype):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("block,nmini", CONFIGS_OK)
-def test_gpu_dbp_large_pages_took_parallel_path(decoder, tmp_path, monkeypatch, block, nmini):
-    from pfloor.decoder import decode_file
+def test_gpu_dbp_large_pages_took_parallel_path(tmp_path, switches, block, nmini):
+    from pfloor.decoder import GpuDecoder, decode_file
     v = _values(n=60001, seed=block + nmini)
     path = str(tmp_path / f"dbp_big_{block}_{nmini}.parquet")
     _write(path, v, block, nmini, junk_tail=True)
     for par, want in (("1", 1), ("0", 0)):
-        monkeypatch.setenv("PF_DBP_PAR", par)
-        got = decode_file(path, decoder=decoder)
-        assert got["_status"] == 0, got["_error"]
-        assert np.array_equal(np.frombuffer(got[(0, 0)]["values"].tobytes(), np.int64), v)
-        assert [p[1] for p in _paths(decoder)] == [want], par
+        with switches(PF_DBP_PAR=par), GpuDecoder(0) as decoder:
+            got = decode_file(path, decoder=decoder)
+            assert got["_status"] == 0, got["_error"]
+            assert np.array_equal(np.frombuffer(got[(0, 0)]["values"].tobytes(), np.int64), v)
+            assert [p[1] for p in _paths(decoder)] == [want], par

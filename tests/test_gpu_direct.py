@@ -94,21 +94,20 @@ def test_direct_and_inplace_pages(decoder, oracle, tmp_path, version):
         assert d.count(DIRECT_INPLACE) >= 1, d
 
 
-def test_direct_pages_through_the_redo_path(decoder, oracle, tmp_path, monkeypatch):
-    from pfloor.decoder import decode_file
+def test_direct_pages_through_the_redo_path(oracle, tmp_path, switches):
+    from pfloor.decoder import GpuDecoder, decode_file
     path = _file(tmp_path, "1.0")
-    monkeypatch.setenv("PF_DEBUG_FORCE_REDO", "2")
-    got = decode_file(path, decoder=decoder)
-    monkeypatch.delenv("PF_DEBUG_FORCE_REDO")
-    assert got["_status"] == 0, got["_error"]
-    assert _check(got, oracle, path, "forced redo") == 16
-    from pfloor import _native
-    L = _native.lib()
-    L.pf_debug_snappy_fallback.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
-    nj = L.pf_debug_snappy_fallback(decoder.h, None, 0)
-    rec = (C.c_int * (5 * nj))()
-    L.pf_debug_snappy_fallback(decoder.h, rec, nj)
-    d = _direct(decoder)
+    with switches(PF_DEBUG_FORCE_REDO=2), GpuDecoder(0) as decoder:
+        got = decode_file(path, decoder=decoder)
+        assert got["_status"] == 0, got["_error"]
+        assert _check(got, oracle, path, "forced redo") == 16
+        from pfloor import _native
+        L = _native.lib()
+        L.pf_debug_snappy_fallback.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
+        nj = L.pf_debug_snappy_fallback(decoder.h, None, 0)
+        rec = (C.c_int * (5 * nj))()
+        L.pf_debug_snappy_fallback(decoder.h, rec, nj)
+        d = _direct(decoder)
     redone = [rec[5 * j + 4] for j in range(nj) if rec[5 * j] == 2]
     assert any(d[p] == DIRECT_VALUES for p in redone)   # accepted as direct, then decoded from scratch
 

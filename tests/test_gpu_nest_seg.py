@@ -18,6 +18,16 @@ pytestmark = pytest.mark.gpu
 SEGS = ["64", "500", "4096"]
 
 
+def _decode(switches, path, seg, decoder=None):
+    """Decode with the product library (seg None: default segments) or with a forced segment length
+    (PF_NEST_SEG, the diagnostics build; a decoder of its own)."""
+    from pfloor.decoder import decode_file
+    if seg is None:
+        return decode_file(path, decoder=decoder)
+    with switches(PF_NEST_SEG=seg):
+        return decode_file(path)
+
+
 @pytest.fixture(scope="module")
 def decoder():
     from pfloor.decoder import GpuDecoder
@@ -27,13 +37,11 @@ def decoder():
 
 
 @pytest.mark.parametrize("seg", SEGS)
-def test_golden_files_in_segments(decoder, oracle, monkeypatch, seg):
-    from pfloor.decoder import decode_file
-    monkeypatch.setenv("PF_NEST_SEG", seg)
+def test_golden_files_in_segments(oracle, switches, seg):
     for name in golden_files():
         path = os.path.join(GOLDEN, name + ".parquet")
         exp = load_expected(name)
-        got = decode_file(path, decoder=decoder)
+        got = _decode(switches, path, seg)
         with oracle.open(path) as of:
             for key, e in sorted(exp.items()):
                 g = got[key]
@@ -87,12 +95,9 @@ def _nested_file(tmp_path, v2, rows=60000, seed=21):
 
 @pytest.mark.parametrize("v2", [False, True])
 @pytest.mark.parametrize("seg", [None, "300", "2048"])
-def test_generated_nested_in_segments(decoder, oracle, monkeypatch, tmp_path, v2, seg):
-    from pfloor.decoder import decode_file
+def test_generated_nested_in_segments(decoder, oracle, switches, tmp_path, v2, seg):
     path = _nested_file(tmp_path, v2)
-    if seg is not None:
-        monkeypatch.setenv("PF_NEST_SEG", seg)
-    got = decode_file(path, decoder=decoder)
+    got = _decode(switches, path, seg, decoder)
     with oracle.open(path) as of:
         for rg in range(of.num_row_groups):
             for c in range(of.num_columns):
@@ -101,7 +106,7 @@ def test_generated_nested_in_segments(decoder, oracle, monkeypatch, tmp_path, v2
                 assert_chunk_equal(g, of.decode(rg, c), f"nest rg{rg} c{c} v2={v2} seg={seg}")
 
 
-def test_damaged_nested_pages_same_status(decoder, monkeypatch, tmp_path):
+def test_damaged_nested_pages_same_status(decoder, switches, tmp_path):
     """Byte damage in nested page bodies: the segment path reports what the whole-page path
     reports (same status per chunk, same data when both decode) and never faults."""
     from pfloor.decoder import decode_file
@@ -113,9 +118,8 @@ def test_damaged_nested_pages_same_status(decoder, monkeypatch, tmp_path):
         p.write_bytes(bad)
         res = {}
         for seg in ("0", "100"):
-            monkeypatch.setenv("PF_NEST_SEG", seg)
             try:
-                res[seg] = decode_file(str(p), decoder=decoder)
+                res[seg] = _decode(switches, str(p), seg)
             except Exception as e:   # metadata-level rejection on the host
                 res[seg] = repr(e)
         a, b = res["0"], res["100"]
@@ -128,7 +132,6 @@ def test_damaged_nested_pages_same_status(decoder, monkeypatch, tmp_path):
             assert a[k]["status"] == b[k]["status"], (i, k)
             if a[k]["status"] == 0:
                 assert_chunk_equal(b[k], a[k], f"damaged {i} {k}")
-    monkeypatch.delenv("PF_NEST_SEG")
     got = decode_file(os.path.join(GOLDEN, "ref_roundtrip.parquet"), decoder=decoder)
     assert got["_status"] == 0
 
@@ -175,12 +178,9 @@ def _nested_types_file(tmp_path, rows=30000, seed=33):
 
 
 @pytest.mark.parametrize("seg", [None, "100", "777"])
-def test_nested_leaf_types_in_segments(decoder, oracle, monkeypatch, tmp_path, seg):
-    from pfloor.decoder import decode_file
+def test_nested_leaf_types_in_segments(decoder, oracle, switches, tmp_path, seg):
     path = _nested_types_file(tmp_path)
-    if seg is not None:
-        monkeypatch.setenv("PF_NEST_SEG", seg)
-    got = decode_file(path, decoder=decoder)
+    got = _decode(switches, path, seg, decoder)
     with oracle.open(path) as of:
         for rg in range(of.num_row_groups):
             for c in range(of.num_columns):

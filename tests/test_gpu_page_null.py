@@ -18,15 +18,20 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module", autouse=True)
 def page_null_on():
-    """k_page_null is opt-in (PF_PAGE_NULL=1, read per launch): this module tests it."""
+    """k_page_null is opt-in (a diagnostics-build option, PF_PAGE_NULL=1 read at pf_ctx_create): this
+    module runs on the diagnostics build with it on."""
     import os
+    from pfloor import _native
     old = os.environ.get("PF_PAGE_NULL")
     os.environ["PF_PAGE_NULL"] = "1"
-    yield
-    if old is None:
-        os.environ.pop("PF_PAGE_NULL", None)
-    else:
-        os.environ["PF_PAGE_NULL"] = old
+    try:
+        with _native.diagnostics():
+            yield
+    finally:
+        if old is None:
+            os.environ.pop("PF_PAGE_NULL", None)
+        else:
+            os.environ["PF_PAGE_NULL"] = old
 
 
 @pytest.fixture(scope="module")
@@ -104,7 +109,7 @@ def test_page_null_many_runs(decoder, oracle, tmp_path):
 
 
 @pytest.mark.parametrize("page_null", ["0", "1"])
-def test_null_blocks_staggered(decoder, oracle, tmp_path, monkeypatch, page_null):
+def test_null_blocks_staggered(oracle, tmp_path, switches, page_null):
     """Blocks after a page's first start only once it has finished (PF_DEBUG_NULL_STAGGER), with
     k_page_null off (every page through k_lvl + k_flat_null) and on: bit-exact vs the oracle. r04
     regression: a k_flat_null block skipped its page (values and count lost) once a sibling block
@@ -113,8 +118,6 @@ def test_null_blocks_staggered(decoder, oracle, tmp_path, monkeypatch, page_null
     import pyarrow as pa
     import pyarrow.parquet as pq
     from pfloor.decoder import decode_file
-    monkeypatch.setenv("PF_PAGE_NULL", page_null)
-    monkeypatch.setenv("PF_DEBUG_NULL_STAGGER", "100")
     rng = np.random.default_rng(5)
     n = 60_000
     cols = {}
@@ -125,7 +128,8 @@ def test_null_blocks_staggered(decoder, oracle, tmp_path, monkeypatch, page_null
     path = str(tmp_path / "stagger.parquet")
     pq.write_table(pa.table(cols), path, compression="snappy", row_group_size=n,
                    use_dictionary=["c0", "c1", "c2"])
-    got = decode_file(path, decoder=decoder)
+    with switches(PF_PAGE_NULL=page_null, PF_DEBUG_NULL_STAGGER=100):
+        got = decode_file(path)
     assert got["_status"] == 0, got["_error"]
     with oracle.open(path) as of:
         for c in range(4):

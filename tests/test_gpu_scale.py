@@ -61,21 +61,20 @@ def test_wide_config4_shape(decoder, oracle, tmp_path):
     assert 0.25 < 1 - valid.mean() < 0.35
 
 
-def test_serial_snappy_kernel_many_jobs(decoder, oracle, monkeypatch):
-    from pfloor.decoder import decode_file
-    path = os.path.join(os.path.dirname(__file__), "golden", "c2_lineitem.parquet")
-    monkeypatch.setenv("PF_DEBUG_FORCE_SERIAL", "3")
-    got = decode_file(path, decoder=decoder)
-    monkeypatch.delenv("PF_DEBUG_FORCE_SERIAL")
-    assert got["_status"] == 0, got["_error"]
+def test_serial_snappy_kernel_many_jobs(oracle, switches):
     import ctypes as C
     from pfloor import _native
-    L = _native.lib()
-    L.pf_debug_snappy_fallback.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
-    nj = L.pf_debug_snappy_fallback(decoder.h, None, 0)
-    assert nj > 3 * 64, nj                     # forced jobs reach far past the serial kernel's 64 blocks
-    rec = (C.c_int * (5 * nj))()
-    assert L.pf_debug_snappy_fallback(decoder.h, rec, nj) == nj
+    from pfloor.decoder import GpuDecoder, decode_file
+    path = os.path.join(os.path.dirname(__file__), "golden", "c2_lineitem.parquet")
+    with switches(PF_DEBUG_FORCE_SERIAL=3), GpuDecoder(0) as decoder:
+        got = decode_file(path, decoder=decoder)
+        assert got["_status"] == 0, got["_error"]
+        L = _native.lib()
+        L.pf_debug_snappy_fallback.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
+        nj = L.pf_debug_snappy_fallback(decoder.h, None, 0)
+        assert nj > 3 * 64, nj                     # forced jobs reach far past the serial kernel's 64 blocks
+        rec = (C.c_int * (5 * nj))()
+        assert L.pf_debug_snappy_fallback(decoder.h, rec, nj) == nj
     forced = [j for j in range(nj) if rec[5 * j] == 3]
     assert len(forced) == nj // 3 and max(forced) >= 128
     assert _check_all(got, oracle, path, "forced-serial") > 0
