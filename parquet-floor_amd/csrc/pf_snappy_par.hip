@@ -1484,24 +1484,36 @@ __device__ __forceinline__ void x5_barrier() { asm volatile("s_waitcnt lgkmcnt(0
 // Compiler ordering point for one wave's LDS accesses (the hardware runs them in order).
 __device__ __forceinline__ void x5_order() { asm volatile("" ::: "memory"); }
 
-__global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
-                                                      const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
-    __shared__ __attribute__((aligned(16))) uint8_t L[X5_LDS];
-    __shared__ uint16_t tokpos[XCHUNK / 2];
-    __shared__ uint32_t D0[2][64], D1[2][64];     // packed token descriptors (exec2's d0 / d1)
-    __shared__ uint32_t SB[2][X5_W], WP[2][X5_W];   // token starts of the batch's output, tokens in earlier words
-    __shared__ uint32_t REC[2][4];                  // kind, output start, output bytes, long literal input position
-    __shared__ uint16_t jv[256];
+struct X5Lds {
+    __attribute__((aligned(16))) uint8_t L[X5_LDS];
+    uint16_t tokpos[XCHUNK / 2];
+    uint32_t D0[2][64], D1[2][64];     // packed token descriptors (exec2's d0 / d1)
+    uint32_t SB[2][X5_W], WP[2][X5_W];   // token starts of the batch's output, tokens in earlier words
+    uint32_t REC[2][4];                  // kind, output start, output bytes, long literal input position
+    uint16_t jv[256];
+};
+
+// One piece (mode 0: pieces[item]) or one whole-page redo (mode 1: job item) by the workgroup's two waves.
+__device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
+                                            const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode, int item) {
+    uint8_t* const L = S.L;
+    uint16_t* const tokpos = S.tokpos;
+    auto& D0 = S.D0;
+    auto& D1 = S.D1;
+    auto& SB = S.SB;
+    auto& WP = S.WP;
+    auto& REC = S.REC;
+    uint16_t* const jv = S.jv;
     uint8_t* const ring = L;
     const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
     const int lane = int(threadIdx.x) & 63;
     int j, k;
     if (mode == 0) {
-        const int2 pc = pieces[blockIdx.x];
+        const int2 pc = pieces[item];
         j = pc.x;
         k = pc.y;
     } else {
-        j = blockIdx.x;
+        j = item;
         k = 0;
     }
     const int f = fb[j];
@@ -1547,9 +1559,17 @@ __global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restric
     // consumer state
     uint32_t F = out_start, cop = out_start;
     uint32_t last = R5_END;
+#ifdef PF_STAMPS   // per phase cycles: producer slots 0-4 (wave 0), consumer 6-9 (wave 1), 12 batches, 13 pieces
+    unsigned long long x5t = __builtin_amdgcn_s_memtime();
+#define X5T(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (lane == 0) STAMP_ADD(i, t_ - x5t); x5t = t_; } while (0)
+    if (threadIdx.x == 0) STAMP_ADD(13, 1);
+#else
+#define X5T(i) ((void)0)
+#endif
     for (uint32_t it = 0;; it++) {
         const uint32_t b = it & 1u;
         if (wv == 0) {
+            if (lane == 0) STAMP_ADD(12, 1);
             // ---------------- producer: batch it into buffer b
             uint32_t kind = R5_BAD, b_op = op, b_tot = 0, b_s0 = 0;
             // landed frontier: the consumer finished batch it-2 before the last barrier
@@ -1584,6 +1604,7 @@ __global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restric
                     if (T == 0) ok = false;
                 }
             }
+            X5T(0);   // chunk staging + token enumeration
             if (ok) {
                 const uint8_t* stg = L + X5_STAGE0 + cb * X5_STG;
                 const uint32_t t = sb + uint32_t(lane);
@@ -1640,6 +1661,7 @@ __global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restric
                         if (__any(cp && (off == 0 || off > otok - out_start))) ok = false;
                         // a far source straddling the direct split (level bytes | values) is not one window
                         if (od.dd != nullptr && __any(far && a < od.dlo && a + ol > od.dlo)) ok = false;
+                        X5T(1);   // token decode, chain checks, cuts
                         if (ok) {
                             uint32_t* fl = reinterpret_cast<uint32_t*>(L + X5_FBUF0 + b * X5_FSL) + frank * FBUF_W;
                             if (far) {
@@ -1654,6 +1676,7 @@ __global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restric
                                 for (int u = 0; u < int(FBUF_W); u++)
                                     if (uint32_t(u) < nwd) fl[u] = fw[u];
                             }
+                            X5T(2);   // far-copy source loads
                             const uint32_t rel = otok - op;
                             uint32_t d0 = 0, d1 = 0;
                             if (inb) {
@@ -1693,6 +1716,7 @@ __global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restric
                 REC[b][2] = b_tot;
                 REC[b][3] = b_s0;
             }
+            X5T(3);   // descriptors, token-start words
             k_m2 = k_m1;
             k_m1 = kind;
             ops_m1 = b_op;
@@ -1759,9 +1783,12 @@ __global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restric
                     for (int u = 0; u < 4; u++)
                         if (act[u]) ring[(s1 + 64u * uint32_t(u) + uint32_t(lane)) & XRMASK] = uint8_t(W[u]);
                 }
+                X5T(6);   // windows
                 flush_slots(ring, od, F, s0 + btot, lane);
                 cop = s0 + btot;
+                X5T(7);   // flush
                 asm volatile("s_waitcnt vmcnt(1)" ::: "memory");   // all but the newest store have landed
+                X5T(8);   // store drain
             } else if (kind == R5_LONG) {
                 const uint32_t sl = __builtin_amdgcn_readfirstlane(REC[pb][3]);
                 for (uint32_t d0 = 0; d0 < btot; d0 += XLIT) {
@@ -1783,7 +1810,9 @@ __global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restric
                 wait_vmem();
             }
         }
+        X5T(9);   // (long literal / empty batch)
         x5_barrier();
+        if (wv == 0) X5T(4); else X5T(10);   // barrier wait
         last = __builtin_amdgcn_readfirstlane(REC[b][0]);
         if (last >= R5_END) break;
     }
@@ -1795,6 +1824,30 @@ __global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restric
         for (uint32_t a = F + uint32_t(lane) * 16u; a + 16u <= cop; a += 1024u)
             put16(od, a, *reinterpret_cast<const u32x4*>(ring + (a & XRMASK)));
         for (uint32_t a = F + ((cop - F) & ~15u) + uint32_t(lane); a < cop; a += 64) put1(od, a, ring[a & XRMASK]);
+    }
+#undef X5T
+}
+
+// ctr == null: one workgroup per item (grid = items). Else a capped grid whose workgroups take items
+// from the counter in list order (pieces are listed densest first) until none are left: the executor
+// holds a fixed share of the CUs' LDS and wave slots instead of flooding them, so the other streams'
+// kernels are not starved of CUs for the whole stage.
+__global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
+                                                      const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode,
+                                                      uint32_t* __restrict__ ctr, int n_items) {
+    __shared__ X5Lds S;
+    __shared__ uint32_t s_item;
+    if (ctr == nullptr) {
+        exec5_piece(S, jobs, pieces, splits, fb, mode, int(blockIdx.x));
+        return;
+    }
+    for (;;) {
+        if (threadIdx.x == 0) s_item = atomicAdd(ctr, 1u);
+        __syncthreads();
+        const uint32_t it = s_item;
+        __syncthreads();   // the previous item's LDS work and this read are done before anything is reused
+        if (it >= uint32_t(n_items)) break;
+        exec5_piece(S, jobs, pieces, splits, fb, mode, int(it));
     }
 }
 
@@ -2236,6 +2289,9 @@ extern "C" int pf_debug_stamps(unsigned long long* out, int n, int reset) {
 
 void launch_snappy_serial(const SnappyJob*, int, const int*, DevChunkResult*, hipStream_t);
 
+// compute units of the current device (persistent grids), set once by the runtime
+int g_num_cus = 256;
+
 // Parse stage (token-start bitmaps, chain, 64 KiB split points) and execute stage, separately so
 // the runtime can time them apart.
 void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int n_wins, SnapWin* d_win,
@@ -2256,7 +2312,7 @@ void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins
 }
 
 void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
-                        int* d_fb, DevChunkResult* d_res, int exec, hipStream_t s) {
+                        int* d_fb, DevChunkResult* d_res, int exec, int exec_wpc, uint32_t* d_ctr, hipStream_t s) {
     if (n_jobs <= 0) return;
     // exec (PfOpts; the diagnostics build's PF_EXEC): 5 = producer / consumer waves (default), 6 = the
     // LDS-image workgroup, 2 = one wave per piece. The whole-page redo is always k_snappy_exec5's mode 1.
@@ -2265,11 +2321,20 @@ void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_piece
         // whole-page redo of pages whose pieces were not independent
         hipLaunchKernelGGL(k_snappy_exec2, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
     } else {
-        if (exec == 6)
+        if (exec == 6) {
             hipLaunchKernelGGL(k_snappy_exec6, dim3(n_pieces), dim3(X6_NT), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb);
-        else
-            hipLaunchKernelGGL(k_snappy_exec5, dim3(n_pieces), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
-        hipLaunchKernelGGL(k_snappy_exec5, dim3(n_jobs), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
+        } else {
+            // exec_wpc > 0: at most that many workgroups per CU, taking pieces from d_ctr (zeroed with the batch tables)
+            const int cap = exec_wpc > 0 && d_ctr != nullptr ? exec_wpc * g_num_cus : 0;
+            if (cap > 0 && cap < n_pieces)
+                hipLaunchKernelGGL(k_snappy_exec5, dim3(cap), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0,
+                                   d_ctr, n_pieces);
+            else
+                hipLaunchKernelGGL(k_snappy_exec5, dim3(n_pieces), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0,
+                                   (uint32_t*)nullptr, n_pieces);
+        }
+        hipLaunchKernelGGL(k_snappy_exec5, dim3(n_jobs), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1,
+                           (uint32_t*)nullptr, n_jobs);
     }
     launch_snappy_serial(d_jobs, n_jobs, d_fb, d_res, s);
 }
@@ -2279,7 +2344,7 @@ void launch_snappy(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int 
                    SnapEnt* d_ent, uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
                    int* d_fb, DevChunkResult* d_res, int max_nwin, int exec, hipStream_t s) {
     launch_snappy_parse(d_jobs, n_jobs, d_wins, n_wins, d_win, d_ent, d_lane_out, d_splits, d_fb, max_nwin, s);
-    launch_snappy_exec(d_jobs, n_jobs, d_pieces, n_pieces, d_splits, d_fb, d_res, exec, s);
+    launch_snappy_exec(d_jobs, n_jobs, d_pieces, n_pieces, d_splits, d_fb, d_res, exec, 0, nullptr, s);
 }
 
 }  // namespace pf
