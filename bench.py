@@ -63,7 +63,7 @@ PCIE_GBS = 63.0         # MI355X_MICROARCH.md: PCIe Gen5 x16 per direction
 # the PMC traffic and the label of the roofline object
 STAGE_KERNELS = {
     "snappy_parse": r"k_snappy_(head|litcopy|index|chain|repair|splits)$",
-    "snappy_exec": r"k_snappy_(exec2|exec5|exec6|serial)$",
+    "snappy_exec": r"k_snappy_(exec2|exec5|serial)$",
     "delta": r"k_(dbp_pos|dbp_blk|dbp_scan|delta)$",
     "levels": r"k_(runs|lvl|dlen)$",
     "count": r"k_(nest_lvl|count|count_flat|count_seg|nest_scan|nest_ids|nest_chars|ba_[a-z]+)$",

@@ -18,8 +18,7 @@ namespace pf {
 // environment variables once per context, at pf_ctx_create: A/B selectors for the tools and the
 // switches tests use to force rare paths (forced fallbacks, segment lengths, skipped stages).
 struct PfOpts {
-    int exec = 5;             // PF_EXEC: block-parallel Snappy executor: 5 producer/consumer | 6 LDS image | 2 one wave
-    int exec_wpc = 0;         // PF_EXEC_WPC=k: exec5 as a grid of k workgroups per CU taking pieces from a counter (0: one per piece)
+    int exec = 5;             // PF_EXEC: block-parallel Snappy executor: 5 producer / consumer | 2 one wave
     bool ba_fused = true;     // PF_BA_FUSED=0: the round-3 PLAIN BYTE_ARRAY walk kernels
     bool page_null = false;   // PF_PAGE_NULL=1: k_page_null before k_lvl
     bool null_dict_lds = true;   // PF_NULL_DICT_LDS=0: k_flat_null never stages its dictionary

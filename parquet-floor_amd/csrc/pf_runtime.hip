@@ -28,9 +28,7 @@ void launch_snappy(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, 
                    int*, DevChunkResult*, int, int, hipStream_t);
 void launch_snappy_parse(const SnappyJob*, int, const int2*, int, SnapWin*, SnapEnt*, uint32_t*, uint32_t*, int*, int,
                          hipStream_t);
-void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*, DevChunkResult*, int, int, uint32_t*,
-                        hipStream_t);
-extern int g_num_cus;
+void launch_snappy_exec(const SnappyJob*, int, const int2*, int, uint32_t*, int*, DevChunkResult*, int, hipStream_t);
 void launch_ba(BaJob*, int, const int2*, int, DevChunkResult*, hipStream_t, bool);
 void launch_snappy_head(SnappyJob*, int, DevPage*, const DevChunk*, int*, const DevChunkResult*, hipStream_t);
 void launch_snappy_litcopy(const SnappyJob*, const int*, int, const int*, hipStream_t);
@@ -252,7 +250,6 @@ int enqueue_kernels(pf_ctx* ctx) {
     const int2* d_nseg = reinterpret_cast<const int2*>(lists + lo); lo += ctx->l_nseg.size();
     const int n_nest = int(ctx->l_nest.size()), n_nseg = int(ctx->l_nseg.size() / 2);
     unsigned long long* used = reinterpret_cast<unsigned long long*>(meta + ctx->meta_bytes - 256);
-    uint32_t* piece_ctr = reinterpret_cast<uint32_t*>(meta + ctx->meta_bytes - 128);   // zeroed with the tables
     const int2* d_pieces = reinterpret_cast<const int2*>(meta + ctx->off_pieces);
     uint32_t* d_splits = reinterpret_cast<uint32_t*>(meta + ctx->off_splits);
     int* d_fallback = reinterpret_cast<int*>(meta + ctx->off_fallback);
@@ -280,12 +277,12 @@ int enqueue_kernels(pf_ctx* ctx) {
         HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->exec_stream, ctx->ev_fork, 0));
         launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res,
-                           ctx->opts.exec, ctx->opts.exec_wpc, piece_ctr, ctx->exec_stream);
+                           ctx->opts.exec, ctx->exec_stream);
         HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->exec_stream));
         HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_join, 0));
     } else {
         launch_snappy_exec(d_jobs, int(ctx->jobs.size()), d_pieces, int(ctx->pieces.size()), d_splits, d_fallback, d_res,
-                           ctx->opts.exec, ctx->opts.exec_wpc, piece_ctr, st);
+                           ctx->opts.exec, st);
     }
     EVREC(ctx, ctx->ev[3], st);
     BaJob* d_bajobs = reinterpret_cast<BaJob*>(meta + ctx->off_bajobs);
@@ -816,7 +813,6 @@ void opts_from_env(pf::PfOpts& o) {
     auto on = [](const char* name, bool dflt) { const char* e = std::getenv(name); return e ? e[0] == '1' : dflt; };
     auto num = [](const char* name, int dflt) { const char* e = std::getenv(name); return e ? std::atoi(e) : dflt; };
     o.exec = num("PF_EXEC", o.exec);
-    o.exec_wpc = num("PF_EXEC_WPC", o.exec_wpc);
     o.ba_fused = on("PF_BA_FUSED", o.ba_fused);
     o.page_null = on("PF_PAGE_NULL", o.page_null);
     o.null_dict_lds = on("PF_NULL_DICT_LDS", o.null_dict_lds);
@@ -848,11 +844,6 @@ int ctx_init(pf_ctx* ctx, pf_ctx* peer) {
     opts_from_env(ctx->opts);
 #endif
     HIPCHK(nullptr, hipSetDevice(ctx->device));
-    {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess && cus > 0)
-            pf::g_num_cus = cus;
-    }
     if (peer) {
         ctx->streams = peer->streams;
     } else {

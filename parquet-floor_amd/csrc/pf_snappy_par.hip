@@ -1828,452 +1828,11 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
 #undef X5T
 }
 
-// ctr == null: one workgroup per item (grid = items). Else a capped grid whose workgroups take items
-// from the counter in list order (pieces are listed densest first) until none are left: the executor
-// holds a fixed share of the CUs' LDS and wave slots instead of flooding them, so the other streams'
-// kernels are not starved of CUs for the whole stage.
+// One workgroup per item: mode 0 = a 64 KiB piece (pieces[blockIdx.x]), mode 1 = a whole-page redo.
 __global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
-                                                      const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode,
-                                                      uint32_t* __restrict__ ctr, int n_items) {
+                                                      const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
     __shared__ X5Lds S;
-    __shared__ uint32_t s_item;
-    if (ctr == nullptr) {
-        exec5_piece(S, jobs, pieces, splits, fb, mode, int(blockIdx.x));
-        return;
-    }
-    for (;;) {
-        if (threadIdx.x == 0) s_item = atomicAdd(ctr, 1u);
-        __syncthreads();
-        const uint32_t it = s_item;
-        __syncthreads();   // the previous item's LDS work and this read are done before anything is reused
-        if (it >= uint32_t(n_items)) break;
-        exec5_piece(S, jobs, pieces, splits, fb, mode, int(it));
-    }
-}
-
-// ======================================================================== executor v6
-//
-// One 256-thread workgroup (four waves) per 64 KiB piece, the piece's whole output image in LDS.
-// Google Snappy's copies never leave their 64 KiB block, so every copy source is in the image: no
-// far copies, no ring, no HBM round trip inside the piece; the image goes out once at the end with
-// 16-byte stores. The piece is decoded in batches of one 2 KiB input chunk (at most 4 KiB of output),
-// five workgroup barriers per batch:
-//   tokens   each thread owns 8 input bytes of the staged chunk and decodes the (at most 4) tokens
-//            starting there in registers; one block scan numbers them and gives their output
-//            offsets. The chain check needs no table: every token marks where it ends, and every
-//            token but the batch's first must start on a mark (the first at the batch's input
-//            position). The batch is cut before the first token that would leave the 4 KiB window.
-//   window   each thread owns 16 consecutive output bytes. A byte is final at once when it is a
-//            literal byte or a copy byte whose source precedes the batch (a byte of the image);
-//            otherwise it holds a pointer to its source byte in the window. Pointer doubling
-//            resolves the pointers inside each wave's 1 KiB quarter (the wave's own LDS operations
-//            run in order: no barrier); after one barrier every remaining pointer leads into an
-//            earlier quarter, whose published words no longer change: at most three static hops.
-//   image    the resolved bytes go into the image with one 16-byte LDS store per thread.
-// All per-byte work is branch-free, with the LDS reads of a phase issued together. The next chunk's
-// input and bitmap are loaded into registers while the current batch resolves.
-// Pointer words (16 bits): bit 15 set = pending, bits 0-14 = window index of the source byte;
-// else bits 0-7 = the byte.
-constexpr uint32_t X6_NT = 256;
-constexpr uint32_t X6_CH = 2048;                  // input bytes per batch (8 per thread)
-constexpr uint32_t X6_STG = X6_CH + 256;          // staged: the chunk + lookahead for its last tokens' bytes
-constexpr uint32_t X6_STGC = (X6_STG + 16u) / 16u;   // 16-byte stage loads (alignment shift included)
-constexpr uint32_t X6_W = 4096;                   // output window of a batch (16 bytes per thread)
-constexpr uint32_t X6_SUB = X6_W / 4;             // a wave's quarter of the window
-constexpr uint32_t X6_TMAX = X6_CH / 2;           // tokens of a batch (a token is at least 2 input bytes)
-constexpr uint32_t X6_IMG = SNAP_BLOCK;
-constexpr uint32_t X6_U = X6_TMAX * 8u;           // DA, DB (u32 per token) | PT (u16 per window byte)
-static_assert(X6_U >= X6_W * 2u, "pointer table aliases the token tables");
-static_assert(X6_STGC <= X6_NT, "one stage load per thread");
-enum : uint32_t { X6_CUT = 0, X6_BAD = 1, X6_OE = 2, X6_IE = 3 };
-
-// Inclusive wave min / max (DPP; identity for lanes without a source).
-__device__ __forceinline__ uint32_t dpp_incl_max(uint32_t v) {
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false)));
-    return v;
-}
-__device__ __forceinline__ uint32_t dpp_incl_min(uint32_t v) {
-    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(~0u, v, 0x111, 0xf, 0xf, false)));
-    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(~0u, v, 0x112, 0xf, 0xf, false)));
-    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(~0u, v, 0x114, 0xf, 0xf, false)));
-    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(~0u, v, 0x118, 0xf, 0xf, false)));
-    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(~0u, v, 0x142, 0xa, 0xf, false)));
-    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(~0u, v, 0x143, 0xc, 0xf, false)));
-    return v;
-}
-
-// Prefetch of one chunk: a thread's 16-byte stage load and its 8 bits of the token-start bitmap.
-struct X6Chunk {
-    u32x4 v;
-    uint32_t bits, I, woff;
-};
-__device__ __forceinline__ X6Chunk x6_load(const uint8_t* in, uint64_t n, const PF_GLOBAL uint8_t* tm8, uint32_t ip,
-                                           int t) {
-    X6Chunk c;
-    c.I = ip & ~15u;
-    const uintptr_t ga = reinterpret_cast<uintptr_t>(in + c.I);
-    c.woff = uint32_t(ga & 15u);
-    c.v = u32x4{0u, 0u, 0u, 0u};
-    const int64_t cs = int64_t(c.I) - int64_t(c.woff) + 16 * int64_t(t);
-    if (uint32_t(t) < X6_STGC && cs < int64_t(n)) c.v = reinterpret_cast<const PF_GLOBAL u32x4*>(ga - c.woff)[t];
-    const uint32_t p8 = c.I + 8u * uint32_t(t);
-    uint32_t bits = uint64_t(p8) < n ? uint32_t(tm8[p8 >> 3]) : 0u;
-    if (uint64_t(p8) < n && uint64_t(p8) + 8u > n) bits &= (1u << uint32_t(n - p8)) - 1u;
-    if (p8 + 8u <= ip) bits = 0;
-    else if (p8 < ip) bits &= ~((1u << (ip - p8)) - 1u);
-    c.bits = bits;
-    return c;
-}
-
-__global__ __launch_bounds__(X6_NT) void k_snappy_exec6(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
-                                                        const uint32_t* __restrict__ splits, int* __restrict__ fb) {
-    __shared__ __attribute__((aligned(16))) uint8_t img[X6_IMG];
-    __shared__ __attribute__((aligned(16))) uint8_t stg[X6_STGC * 16u];
-    __shared__ __attribute__((aligned(16))) uint8_t U[X6_U];
-    __shared__ uint32_t sbits[X6_W / 32], mark[X6_CH / 32];
-    __shared__ uint32_t ws[2][4], red[4], ll[4], vt[4];
-    uint32_t* const DA = reinterpret_cast<uint32_t*>(U);                 // token: window output offset | kind | copy offset
-    uint32_t* const DB = DA + X6_TMAX;                                   // token: literal data position (stream)
-    uint16_t* const PT = reinterpret_cast<uint16_t*>(U);                 // window pointer words (after the token tables)
-    const int t = int(threadIdx.x);
-    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int lane = t & 63;
-    const int2 pc = pieces[blockIdx.x];
-    const int j = pc.x, k = pc.y;
-    const int f = fb[j];
-    if (f >= FB_REDO || (f == FB_WHOLE && k > 0)) return;
-    const bool whole = f == FB_WHOLE;
-    const SnappyJob job = jobs[j];
-    const uint8_t* in = job.src;
-    const uint64_t n = job.src_len;
-    const uint32_t* sp = splits + job.split_base;
-    uint64_t pos0 = 0, ulen = 0;
-    if (!uvarint(in, n, pos0, ulen) || ulen != job.dst_len) {
-        if (t == 0) atomicMax(&fb[j], FB_SERIAL);
-        return;
-    }
-    if (job.dflags & 1u) {   // diagnostics: forced redo
-        if (t == 0) atomicMax(&fb[j], FB_REDO);
-        return;
-    }
-    uint32_t ip, out_start, out_end = job.dst_len;
-    if (whole) {
-        ip = uint32_t(pos0);
-        out_start = 0;
-    } else {
-        if (k > 0 && sp[k] == SNAP_INVALID) return;   // no token at this boundary: an earlier piece covers it
-        ip = k == 0 ? uint32_t(pos0) : sp[k];
-        out_start = uint32_t(k) * SNAP_BLOCK;
-        for (uint32_t k2 = k + 1; k2 < job.n_pieces; k2++)
-            if (sp[k2] != SNAP_INVALID) { out_end = k2 * SNAP_BLOCK; break; }
-    }
-    const uint32_t plen = out_end - out_start;   // piece bytes; positions below are piece-relative
-    if (plen > X6_IMG) {                          // not one Google Snappy block: the whole-page redo decodes it
-        if (t == 0) atomicMax(&fb[j], FB_REDO);
-        return;
-    }
-    if (plen == 0) return;
-    const PF_GLOBAL uint8_t* tm8 = (const PF_GLOBAL uint8_t*)(job.tokmap);
-    const PF_GLOBAL uint8_t* gin = gptr(in);
-    // first chunk; per batch afterwards the next one is loaded during the window phase
-    X6Chunk cur = x6_load(in, n, tm8, ip, t);
-    if (t < int(X6_STGC)) reinterpret_cast<u32x4*>(stg)[t] = cur.v;
-    if (t < int(X6_W / 32)) sbits[t] = 0;
-    if (t < int(X6_CH / 32)) mark[t] = 0;
-    if (t == 0) {
-        red[X6_CUT] = ~0u;
-        red[X6_BAD] = ~0u;
-        red[X6_OE] = 0;
-        red[X6_IE] = 0;
-    }
-    __syncthreads();
-    uint32_t op = 0;
-    bool bad = false;
-#ifdef PF_STAMPS   // phase cycles of wave 0 (tools/probe_exec6.py)
-    unsigned long long x6t = __builtin_amdgcn_s_memtime(), x6t0 = x6t;
-#define X6T(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (t == 0) STAMP_ADD(i, t_ - x6t); x6t = t_; } while (0)
-#define X6C(i) do { if (t == 0) STAMP_ADD(i, 1); } while (0)
-    if (t == 0) STAMP_ADD(13, 1);
-#else
-#define X6T(i) ((void)0)
-#define X6C(i) ((void)0)
-#endif
-    for (;;) {
-        X6C(0);
-        const uint32_t I = cur.I, woff = cur.woff;
-        const uint32_t wbase = op & ~15u;
-        const uint32_t r8 = 8u * uint32_t(t);   // this thread's input bytes: chunk offsets [r8, r8 + 8)
-        // ---- pass 1: the thread's tokens (<= 4 in 8 bytes: a token is at least 2 bytes)
-        uint32_t tb[4], tol[4], targ[4], tkind[4];
-        uint64_t tend[4];
-        bool tv[4];
-        uint32_t bl = cur.bits;
-        #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            tv[q] = bl != 0;
-            tb[q] = tv[q] ? uint32_t(__ffs(bl) - 1) : 0u;
-            bl &= bl - 1u;
-        }
-        const bool over4 = bl != 0;
-        uint64_t v8[4];
-        #pragma unroll
-        for (int q = 0; q < 4; q++) v8[q] = lds_read8(stg, woff + r8 + tb[q]);
-        uint32_t cnt = 0, olsum = 0;
-        #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const SnapTok tk = snap_tok(v8[q]);
-            tol[q] = tk.ol;
-            targ[q] = tk.arg;
-            tkind[q] = tk.kind;
-            tend[q] = uint64_t(I + r8 + tb[q]) + tk.tl;
-            const uint64_t er = tend[q] - I;
-            if (tv[q] && er < X6_CH) atomicOr(&mark[uint32_t(er) >> 5], 1u << (uint32_t(er) & 31u));
-            cnt += tv[q] ? 1u : 0u;
-            olsum += tv[q] ? min(tk.ol, 0x20000u) : 0u;   // any longer token fails the checks
-        }
-        // ---- one block scan of (token count, output bytes)   [barrier 1]
-        uint32_t g0, ob, T;
-        {
-            const uint32_t i1 = dpp_incl_scan(cnt), i2 = dpp_incl_scan(olsum);
-            if (lane == 63) {
-                ws[0][wv] = i1;
-                ws[1][wv] = i2;
-            }
-            __syncthreads();
-            uint32_t p1 = 0, p2 = 0;
-            T = 0;
-            #pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const uint32_t a1 = ws[0][w], a2 = ws[1][w];
-                T += a1;
-                p1 += w < wv ? a1 : 0u;
-                p2 += w < wv ? a2 : 0u;
-            }
-            g0 = p1 + i1 - cnt;
-            ob = p2 + i2 - olsum;
-        }
-        X6T(1);
-        // ---- pass 2: checks, cut, token tables, window token-start bits   [barrier 2]
-        {
-            uint32_t g = g0, o = op + ob;
-            uint32_t myCut = ~0u, myBad = over4 ? g0 : ~0u, myOE = 0, myIE = 0;
-            const uint32_t mw0 = mark[r8 >> 5];
-            #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t pr = r8 + tb[q];   // chunk offset of the token
-                const uint32_t ol = min(tol[q], 0x20000u);
-                const bool cp = tkind[q] != 0;
-                const bool onchain = g == 0 ? I + pr == ip : ((mw0 >> (pr & 31u)) & 1u) != 0u;
-                const bool wrong = !onchain || tend[q] > n || (cp && (targ[q] == 0 || targ[q] > o)) ||
-                                   (o < plen && o + ol > plen) || tol[q] == 0;
-                const bool fit = o < plen && o + ol <= wbase + X6_W;
-                if (tv[q]) {
-                    if (fit) {
-                        const uint32_t rel = o - wbase;
-                        DA[g] = rel | (cp ? (1u << 13) | (targ[q] << 16) : 0u);
-                        DB[g] = I + pr + targ[q];
-                        atomicOr(&sbits[rel >> 5], 1u << (rel & 31u));
-                        myOE = max(myOE, o + ol);
-                        myIE = max(myIE, uint32_t(min(tend[q], uint64_t(0xffffffffu))));
-                    } else {
-                        myCut = min(myCut, g);
-                    }
-                    if (wrong) myBad = min(myBad, g);
-                    if (g == 0) {
-                        ll[0] = tkind[q];
-                        ll[1] = ol;
-                        ll[2] = I + pr + targ[q];
-                        ll[3] = uint32_t(min(tend[q], uint64_t(0xffffffffu)));
-                    }
-                    g++;
-                    o += ol;
-                }
-            }
-            myCut = dpp_incl_min(myCut);
-            myBad = dpp_incl_min(myBad);
-            myOE = dpp_incl_max(myOE);
-            myIE = dpp_incl_max(myIE);
-            if (lane == 63) {
-                atomicMin(&red[X6_CUT], myCut);
-                atomicMin(&red[X6_BAD], myBad);
-                atomicMax(&red[X6_OE], myOE);
-                atomicMax(&red[X6_IE], myIE);
-            }
-        }
-        __syncthreads();
-        X6T(2);
-        const uint32_t cut = min(red[X6_CUT], T);
-        const uint32_t badg = red[X6_BAD];
-        if (T == 0 || badg < cut || (cut == 0 && badg == 0)) { bad = true; break; }
-        const bool lng = cut == 0;   // the first token alone is longer than the window: a long literal
-        if (lng && ll[0] != 0) { bad = true; break; }
-        const uint32_t oe = lng ? op + ll[1] : red[X6_OE];
-        const uint32_t nip = lng ? ll[3] : red[X6_IE];
-        // ---- the next chunk into registers (consumed after barrier 3)
-        const bool more = oe < plen;
-        X6Chunk nxt = cur;
-        if (more) nxt = x6_load(in, n, tm8, nip, t);
-        // ---- window bytes: final values or pointers
-        const uint32_t r0 = 16u * uint32_t(t);
-        uint32_t w[16];
-        if (!lng) {
-            // token index of each byte: bit words' exclusive popcount prefix (each wave scans all 128 words)
-            const uint32_t c0 = __popc(sbits[2 * lane]), c1 = __popc(sbits[2 * lane + 1]);
-            const uint32_t ex = dpp_incl_scan(c0 + c1) - c0 - c1;
-            const int src = 16 * wv + (lane >> 2);
-            const uint32_t pe = uint32_t(__shfl(int(ex), src, 64)), po = uint32_t(__shfl(int(ex + c0), src, 64));
-            const uint32_t sw = sbits[r0 >> 5];
-            const uint32_t hsh = r0 & 31u;
-            const uint32_t bits16 = (sw >> hsh) & 0xffffu;
-            const uint32_t base = ((lane >> 1) & 1 ? po : pe) + __popc(sw & ((1u << hsh) - 1u)) - 1u;
-            uint32_t A[16], B[16];
-            #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const uint32_t x = wbase + r0 + uint32_t(i);
-                const bool inw = x >= op && x < oe;
-                const uint32_t ti = inw ? base + __popc(bits16 & ((2u << i) - 1u)) : 0u;
-                A[i] = DA[ti];
-                B[i] = DB[ti];
-            }
-            const uint8_t* ad[16];
-            bool pend[16], glb[16];
-            uint32_t gs[16];
-            #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const uint32_t x = wbase + r0 + uint32_t(i);
-                const bool inw = x >= op && x < oe;
-                const bool cp = (A[i] >> 13) & 1u;
-                const uint32_t y = x - (A[i] >> 16);
-                const uint32_t s = B[i] + (r0 + uint32_t(i) - (A[i] & 0x1fffu));
-                const uint32_t sr = s - I;
-                const bool instg = sr < X6_STG;
-                pend[i] = inw && cp && y >= op;
-                glb[i] = inw && !cp && !instg;
-                gs[i] = s;
-                w[i] = 0x8000u | (y - wbase);
-                ad[i] = !inw ? img + (x < op ? x : 0u) : (cp ? img + (y < op ? y : 0u) : stg + (instg ? woff + sr : 0u));
-            }
-            uint32_t v[16];
-            #pragma unroll
-            for (int i = 0; i < 16; i++) v[i] = *ad[i];
-            #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const uint32_t x = wbase + r0 + uint32_t(i);
-                w[i] = pend[i] ? w[i] : (x < oe ? v[i] : 0u);
-            }
-            bool anyg = false;
-            #pragma unroll
-            for (int i = 0; i < 16; i++) anyg |= glb[i];
-            if (__any(anyg)) {   // literal bytes past the staged chunk (a long literal inside the window)
-                #pragma unroll
-                for (int i = 0; i < 16; i++)
-                    if (glb[i]) w[i] = gin[gs[i]];
-            }
-        } else {
-            // the long literal straight from the input into the image
-            const uint32_t L0 = ll[1], s0 = ll[2];
-            for (uint32_t i = uint32_t(t); i < L0; i += X6_NT) img[op + i] = gin[s0 + i];
-        }
-        X6T(3);
-        __syncthreads();   // [barrier 3] the token tables, stage, bit words and red are dead
-        X6T(4);
-        if (more) {
-            if (t < int(X6_STGC)) reinterpret_cast<u32x4*>(stg)[t] = nxt.v;
-        }
-        if (t < int(X6_W / 32)) sbits[t] = 0;
-        if (t < int(X6_CH / 32)) mark[t] = 0;
-        if (t == 0) {
-            red[X6_CUT] = ~0u;
-            red[X6_BAD] = ~0u;
-            red[X6_OE] = 0;
-            red[X6_IE] = 0;
-        }
-        uint32_t* const ptw = reinterpret_cast<uint32_t*>(PT) + 8u * uint32_t(t);
-        if (!lng) {
-            // ---- pointer doubling inside the wave's quarter (in-order LDS, no barrier): a word reads the
-            // word its pointer names when that lies in its own quarter, else its own slot (unchanged)
-            const uint32_t sub0 = X6_SUB * uint32_t(wv);
-            for (;;) {
-                bool loc = false;
-                #pragma unroll
-                for (int i = 0; i < 16; i++) loc |= (w[i] & 0x8000u) && (w[i] & 0x7fffu) >= sub0;
-                if (!__any(loc)) break;
-                X6C(7);
-                #pragma unroll
-                for (int i = 0; i < 8; i++) ptw[i] = w[2 * i] | (w[2 * i + 1] << 16);
-                x5_order();
-                uint32_t G[16];
-                #pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const bool l = (w[i] & 0x8000u) && (w[i] & 0x7fffu) >= sub0;
-                    G[i] = PT[l ? (w[i] & 0x7fffu) : r0 + uint32_t(i)];
-                }
-                #pragma unroll
-                for (int i = 0; i < 16; i++) w[i] = G[i];
-                x5_order();
-            }
-            #pragma unroll
-            for (int i = 0; i < 8; i++) ptw[i] = w[2 * i] | (w[2 * i + 1] << 16);
-        }
-        X6T(5);
-        __syncthreads();   // [barrier 4] every quarter's words published
-        X6T(6);
-        if (!lng) {
-            // ---- across quarters: published words are final or lead into an earlier quarter (static)
-            for (int hop = 0;; hop++) {
-                bool pd = false;
-                #pragma unroll
-                for (int i = 0; i < 16; i++) pd |= (w[i] & 0x8000u) != 0u;
-                if (!__any(pd)) break;
-                X6C(9);
-                if (hop >= 3) { bad = true; break; }
-                uint32_t G[16];
-                #pragma unroll
-                for (int i = 0; i < 16; i++) G[i] = PT[(w[i] & 0x8000u) ? (w[i] & 0x7fffu) : r0 + uint32_t(i)];
-                #pragma unroll
-                for (int i = 0; i < 16; i++) w[i] = (w[i] & 0x8000u) ? G[i] : w[i];
-            }
-            // ---- the window's bytes into the image
-            if (wbase + r0 < oe) {
-                u32x4 qv;
-                #pragma unroll
-                for (int d = 0; d < 4; d++)
-                    qv[d] = (w[4 * d] & 0xffu) | ((w[4 * d + 1] & 0xffu) << 8) | ((w[4 * d + 2] & 0xffu) << 16) |
-                            ((w[4 * d + 3] & 0xffu) << 24);
-                *reinterpret_cast<u32x4*>(img + wbase + r0) = qv;
-            }
-        }
-        X6T(8);
-        // a hop count above three is impossible for a valid chain; every wave votes before leaving
-        if (lane == 0) vt[wv] = bad ? 1u : 0u;
-        __syncthreads();   // [barrier 5] image, next stage and cleared tables ready
-        X6T(10);
-        if (vt[0] | vt[1] | vt[2] | vt[3]) { bad = true; break; }
-        op = oe;
-        ip = nip;
-        cur = nxt;
-        if (!more) break;
-    }
-    if (bad) {
-        if (t == 0) atomicMax(&fb[j], whole ? FB_SERIAL : FB_REDO);
-        return;
-    }
-    // ---- the piece's bytes to HBM (16-byte stores; a direct job's values straight into its column)
-    const OutDst od{gptr(job.dst), gptr(job.ddst), job.dlo, job.dgran};
-    for (uint32_t a = 16u * uint32_t(t); a + 16u <= plen; a += 16u * X6_NT)
-        put16(od, out_start + a, *reinterpret_cast<const u32x4*>(img + a));
-    for (uint32_t a = (plen & ~15u) + uint32_t(t); a < plen; a += X6_NT) put1(od, out_start + a, img[a]);
-#ifdef PF_STAMPS
-    X6T(14);
-    if (t == 0) STAMP_ADD(12, __builtin_amdgcn_s_memtime() - x6t0);
-#endif
-#undef X6T
-#undef X6C
+    exec5_piece(S, jobs, pieces, splits, fb, mode, int(blockIdx.x));
 }
 
 #ifdef PF_STAMPS
@@ -2288,9 +1847,6 @@ extern "C" int pf_debug_stamps(unsigned long long* out, int n, int reset) {
 #endif
 
 void launch_snappy_serial(const SnappyJob*, int, const int*, DevChunkResult*, hipStream_t);
-
-// compute units of the current device (persistent grids), set once by the runtime
-int g_num_cus = 256;
 
 // Parse stage (token-start bitmaps, chain, 64 KiB split points) and execute stage, separately so
 // the runtime can time them apart.
@@ -2312,29 +1868,17 @@ void launch_snappy_parse(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins
 }
 
 void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
-                        int* d_fb, DevChunkResult* d_res, int exec, int exec_wpc, uint32_t* d_ctr, hipStream_t s) {
+                        int* d_fb, DevChunkResult* d_res, int exec, hipStream_t s) {
     if (n_jobs <= 0) return;
-    // exec (PfOpts; the diagnostics build's PF_EXEC): 5 = producer / consumer waves (default), 6 = the
-    // LDS-image workgroup, 2 = one wave per piece. The whole-page redo is always k_snappy_exec5's mode 1.
+    // exec (PfOpts; the diagnostics build's PF_EXEC): 5 = producer / consumer waves (default), 2 = one wave
+    // per piece. The whole-page redo is always the same kernel's mode 1.
     if (exec == 2) {
         hipLaunchKernelGGL(k_snappy_exec2, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
         // whole-page redo of pages whose pieces were not independent
         hipLaunchKernelGGL(k_snappy_exec2, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
     } else {
-        if (exec == 6) {
-            hipLaunchKernelGGL(k_snappy_exec6, dim3(n_pieces), dim3(X6_NT), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb);
-        } else {
-            // exec_wpc > 0: at most that many workgroups per CU, taking pieces from d_ctr (zeroed with the batch tables)
-            const int cap = exec_wpc > 0 && d_ctr != nullptr ? exec_wpc * g_num_cus : 0;
-            if (cap > 0 && cap < n_pieces)
-                hipLaunchKernelGGL(k_snappy_exec5, dim3(cap), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0,
-                                   d_ctr, n_pieces);
-            else
-                hipLaunchKernelGGL(k_snappy_exec5, dim3(n_pieces), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0,
-                                   (uint32_t*)nullptr, n_pieces);
-        }
-        hipLaunchKernelGGL(k_snappy_exec5, dim3(n_jobs), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1,
-                           (uint32_t*)nullptr, n_jobs);
+        hipLaunchKernelGGL(k_snappy_exec5, dim3(n_pieces), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
+        hipLaunchKernelGGL(k_snappy_exec5, dim3(n_jobs), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
     }
     launch_snappy_serial(d_jobs, n_jobs, d_fb, d_res, s);
 }
@@ -2344,7 +1888,7 @@ void launch_snappy(const SnappyJob* d_jobs, int n_jobs, const int2* d_wins, int 
                    SnapEnt* d_ent, uint32_t* d_lane_out, const int2* d_pieces, int n_pieces, uint32_t* d_splits,
                    int* d_fb, DevChunkResult* d_res, int max_nwin, int exec, hipStream_t s) {
     launch_snappy_parse(d_jobs, n_jobs, d_wins, n_wins, d_win, d_ent, d_lane_out, d_splits, d_fb, max_nwin, s);
-    launch_snappy_exec(d_jobs, n_jobs, d_pieces, n_pieces, d_splits, d_fb, d_res, exec, 0, nullptr, s);
+    launch_snappy_exec(d_jobs, n_jobs, d_pieces, n_pieces, d_splits, d_fb, d_res, exec, s);
 }
 
 }  // namespace pf

@@ -54,17 +54,12 @@ def test_block_parallel_path(dec, oracle, seed):
         assert fb == 0, name
 
 
-@pytest.mark.parametrize("executor", ["5", "6"])
-def test_unaligned_stream_single_piece(oracle, switches, executor):
-    """No token at the 64 KiB marks (not Google Snappy's block structure): the page decodes as one
-    piece (copies may reach far back) -- by exec5 in place, while exec6 (whose image holds one 64 KiB
-    block) hands it to the whole-page redo (fallback 2). Bit-exact either way."""
-    from pfloor.decoder import GpuDecoder
+def test_unaligned_stream_single_piece(dec, oracle):
+    """No token at the 64 KiB marks: the page decodes as one piece (copies may reach far back)."""
     rng = np.random.default_rng(7)
     data = _payloads(rng)["text"] * 3
-    with switches(PF_EXEC=executor), GpuDecoder(0) as dec:
-        got, fb = dec.snappy_decompress(oracle.snappy_compress(data, mode=1))
-    assert got == data and fb == (0 if executor == "5" else 2)
+    got, fb = dec.snappy_decompress(oracle.snappy_compress(data, mode=1))
+    assert got == data and fb == 0
 
 
 def test_cross_block_streams_fall_back(dec, oracle):
@@ -120,11 +115,11 @@ def _far_after_literal(seed):
     return bytes(out)
 
 
-@pytest.mark.parametrize("executor", ["6", "5", "2"])
+@pytest.mark.parametrize("executor", ["5", "2"])
 def test_executors_agree(oracle, switches, executor):
-    """Every block-parallel executor (default 5: producer / consumer waves; the diagnostics
-    build's PF_EXEC=6: the LDS-image workgroup per piece; PF_EXEC=2: one wave per piece) on
-    the seeded payloads and on far copies right after long literals."""
+    """Both block-parallel executors (default 5: producer / consumer waves; the diagnostics
+    build's PF_EXEC=2: one wave per piece) on the seeded payloads and on far copies right after long
+    literals."""
     from pfloor.decoder import GpuDecoder
     rng = np.random.default_rng(11)
     cases = dict(_payloads(rng), far1=_far_after_literal(1), far2=_far_after_literal(2))
