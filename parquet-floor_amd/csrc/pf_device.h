@@ -79,6 +79,29 @@ __device__ __forceinline__ uint64_t bits_le64(const uint8_t* p, uint64_t n, uint
 
 __device__ __forceinline__ int bit_width(uint32_t max_level) { return max_level ? 32 - __clz(max_level) : 0; }
 
+// ---- 64-bit block-wide exclusive scan (lds_wave: NT / 64 words) ----------------------------
+template <int NT>
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, unsigned long long* lds_wave, uint64_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t x = v;
+    #pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up((unsigned long long)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) lds_wave[wid] = x;
+    __syncthreads();
+    uint64_t base = 0, tot = 0;
+    #pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+        const uint64_t t = lds_wave[w];
+        if (w < wid) base += t;
+        tot += t;
+    }
+    total = tot;
+    return base + x - v;
+}
+
 // ---- block-wide exclusive scan (blockDim.x == 256, 4 waves) -----------------------------
 template <int NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds_wave /*[NT/64]*/, uint32_t& total) {

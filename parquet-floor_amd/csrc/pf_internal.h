@@ -35,6 +35,8 @@ struct PfOpts {
     bool nest_seg_set = false;
     bool dbp_par = true;      // PF_DBP_PAR=0: every DELTA_BINARY_PACKED page on k_delta
     int fix_shift = 1;        // PF_FIX_BLK=4096|8192|16384: fixed-width flat blocks (log2 of the multiple of 4096)
+    int decode_grid = 32;     // PF_DECODE_GRID: k_decode blocks when no page is known to need it (grid-stride check)
+    int count_grid = 64;      // PF_COUNT_GRID: k_count blocks (grid-stride; nearly every page is counted by k_count_flat)
 };
 
 enum : int32_t {

@@ -2832,23 +2832,31 @@ __device__ __forceinline__ uint32_t id_run_at(const uint32_t* T, uint32_t nr, ui
     return lo;
 }
 
-constexpr int LT_NT = 64;   // k_lvl: one wave per page
-constexpr uint32_t LVL_RUNS_LDS = 256;   // level runs k_lvl keeps in LDS (pages with more read them from HBM)
-constexpr uint32_t LVL_NXT = 4096;        // = LVL_STAGE: k_lvl's all-positions header chain covers its sections
+constexpr int LT_NT = 256;                // k_lvl: four waves per page
+constexpr uint32_t LVL_RUNS_LDS = 512;    // level runs k_lvl keeps in LDS (pages with more read them from HBM)
+constexpr uint32_t LVL_NXT = 4096;        // = LVL_STAGE: k_lvl's all-positions header tables cover its sections
+constexpr uint32_t LVL_JUMP = 8;          // runs per step of k_lvl's chain walk (jump table: 3 doubling passes)
+constexpr uint32_t LVL_S8 = LVL_NXT / LVL_JUMP;   // walk steps (a run is at least one byte)
+constexpr uint32_t LVL_PPT = LVL_NXT / LT_NT;     // section positions per thread in the table passes
+static_assert(LVL_PPT == 16, "k_lvl's mark words: two threads per 32 positions");
 __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
                                                DevChunkResult* res) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[LVL_STAGE + 48];
-    __shared__ uint32_t scan_tmp[1];
-    __shared__ uint32_t s_nr, s_ok;
-    // LDS copies of the page's level runs and of its dictionary-id runs (k_runs): the block-table
-    // pass below scans them serially, one dependent load per run, which from HBM cost ~1 us each
-    __shared__ uint32_t s_runs[4 * LVL_RUNS_LDS];
-    // the next-header table lives only in the chain phase and the id-run copy only after it: one LDS
-    // region (8 KiB instead of 10: nine waves per CU instead of eight)
+    __shared__ uint32_t scan_tmp[LT_NT / 64];
+    __shared__ uint32_t s_ns8, s_ok, s_nr;
+    // next-header positions of every byte position (0xffff: not a header, or its run passes the
+    // section end; dn: the chain ends there), then the page's dictionary-id runs (k_runs) for the
+    // block table
     __shared__ union { uint16_t nxt[LVL_NXT]; uint32_t T[4 + 2 * RUN_CAP]; } s_u;
+    // the 8-run jump table during the chain walk, then the LDS copy of the level runs
+    __shared__ union { uint16_t jmp[LVL_NXT]; uint32_t runs[4 * LVL_RUNS_LDS]; } s_a;
+    __shared__ uint16_t s_s8[LVL_S8];         // chain positions of runs 0, 8, 16, ...
+    __shared__ uint32_t s_mark[LVL_NXT / 32];  // chain positions (run headers)
     static_assert(sizeof(uint16_t) * LVL_NXT >= sizeof(uint32_t) * (4 + 2 * RUN_CAP), "s_u sized by the header table");
-    uint16_t* const s_nxt = s_u.nxt;   // position of the next run header, per byte position
+    uint16_t* const s_nxt = s_u.nxt;
     uint32_t* const s_T = s_u.T;
+    uint16_t* const s_jmp = s_a.jmp;
+    uint32_t* const s_runs = s_a.runs;
     const int pi = list[blockIdx.x];
     DevPage& pg = pages[pi];
     uint32_t* LT = pg.lvltab;
@@ -2869,6 +2877,14 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
     const int bw = bit_width(uint32_t(ck.max_def));
     const uint32_t maxd = uint32_t(ck.max_def);
     const uint32_t dn = uint32_t(s.def_n);
+#ifdef PF_STAMPS   // phase cycles per page (tools/probe_wide.py): 8 pages, 9 stage, 10 header table, 11 chain,
+                   // 12 run decode, 13 present counts, 14 block table, 15 total; 6 runs, 7 level bytes
+    unsigned long long lt_ = __builtin_amdgcn_s_memtime(), lt0_ = lt_;
+#define LTS(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) PSTAMP(i, t_ - lt_); lt_ = t_; } while (0)
+    if (tid == 0) { PSTAMP(8, 1); PSTAMP(7, dn); }
+#else
+#define LTS(i) ((void)0)
+#endif
     // stage the level section with aligned 16-byte loads: section byte i is stage[woff + i]; bytes
     // past the section read as zero (parquet-mr zero-pads a truncated bit-packed run)
     const uintptr_t sa = reinterpret_cast<uintptr_t>(s.def);
@@ -2881,101 +2897,151 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
         const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(sa - woff);
         const uint32_t nchunk = (woff + dn + 15u) / 16u;
         for (uint32_t c = tid; c < nchunk; c += LT_NT) reinterpret_cast<u32x4*>(stage)[c] = src[c];
+        if (uint32_t(tid) < LVL_NXT / 32) s_mark[tid] = 0;
         __syncthreads();
         for (uint32_t i = woff + dn + uint32_t(tid); i < nchunk * 16u + 16u; i += LT_NT) stage[i] = 0;
         __syncthreads();
     }
+    LTS(9);
     uint32_t* runs = LT + 4;
     const uint32_t cap = pg.lvl_cap;
-    {   // (dn <= LVL_STAGE == LVL_NXT) all-positions chain: every byte position is decoded as a header in parallel (the position
-        // of the next header, 0xffff when it is not one), the chain from 0 is then one LDS load per
-        // run, and the runs are decoded at their headers in parallel, their first entries a prefix
-        // scan of the counts (north_star K2: run boundaries by wavefront scans)
-        const uint8_t* const stw = stage + woff;
-        for (uint32_t p = tid; p < dn; p += LT_NT) {
-            uint32_t h = 0, hl = 0, nx = 0xffffu;
-            #pragma unroll
-            for (uint32_t k = 0; k < 3; k++) {   // headers over 2^21 are no runs of a <= 4 KiB section
-                const uint32_t c = p + k < dn ? uint32_t(stw[p + k]) : 0x80u;
-                h |= (c & 0x7fu) << (7 * k);
-                if (!(c & 0x80u)) { hl = k + 1; break; }
-            }
-            if (hl) {
-                const uint32_t pay = (h & 1u) ? (h >> 1) * uint32_t(bw) : (uint32_t(bw) + 7u) >> 3;
-                if (p + hl + pay <= dn) nx = p + hl + pay;   // a truncated run ends the chain
-            }
-            s_nxt[p] = uint16_t(nx);
+    const uint8_t* const stw = stage + woff;
+    // (1) every byte position decoded as a run header: the position of the next header
+    for (uint32_t p = tid; p < dn; p += LT_NT) {
+        uint32_t h = 0, hl = 0, nx = 0xffffu;
+        #pragma unroll
+        for (uint32_t k = 0; k < 3; k++) {   // headers over 2^21 are no runs of a <= 4 KiB section
+            const uint32_t c = p + k < dn ? uint32_t(stw[p + k]) : 0x80u;
+            h |= (c & 0x7fu) << (7 * k);
+            if (!(c & 0x80u)) { hl = k + 1; break; }
         }
-        __syncthreads();
-        uint32_t nh = 0;
-        {
-            uint32_t p = 0;
-            while (p < dn && nh < cap) {
-                if (tid == 0) runs[4 * nh + 1] = p;   // header positions, decoded below
-                nh++;
-                const uint32_t q = s_nxt[p];
-                if (q == 0xffffu) break;
-                p = q;
-            }
+        if (hl) {
+            const uint32_t pay = (h & 1u) ? (h >> 1) * uint32_t(bw) : (uint32_t(bw) + 7u) >> 3;
+            if (p + hl + pay <= dn) nx = p + hl + pay;   // a truncated run ends the chain
         }
-        __syncthreads();   // lane 0's header positions are visible to the wave
-        uint64_t carry = 0;
-        uint32_t nr = 0, ok = 1;
-        for (uint32_t c0 = 0; c0 < nh && carry < ne; c0 += LT_NT) {
-            const uint32_t k = c0 + uint32_t(tid);
-            uint32_t cnt = 0, data = 0, packed = 0;
-            bool bad = false;
-            if (k < nh && s_nxt[runs[4 * k + 1]] != 0xffffu) {   // (the chain's last position may be no header)
-                const uint32_t P = runs[4 * k + 1];
-                uint32_t h = 0, hl = 0;
-                for (uint32_t b = 0; b < 3; b++) {
-                    const uint32_t c = stw[P + b];
-                    h |= (c & 0x7fu) << (7 * b);
-                    if (!(c & 0x80u)) { hl = b + 1; break; }
-                }
-                packed = h & 1u;
-                cnt = packed ? (h >> 1) * 8u : (h >> 1);
-                if (packed) data = (P + hl) * 8u;
-                else for (uint32_t b = 0; b < ((uint32_t(bw) + 7u) >> 3); b++) data |= uint32_t(stw[P + hl + b]) << (8 * b);
-            }
-            // first entry of each run: exclusive prefix of the counts (64-bit: counts up to 2^21 each)
-            uint64_t x = cnt;
-            #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint64_t y = __shfl_up(x, d, 64);
-                if (tid >= d) x += y;
-            }
-            const uint64_t first = carry + x - cnt;
-            const bool emit = k < nh && cnt > 0 && first < ne;
-            if (emit && !packed && data > maxd) bad = true;
-            const uint64_t em = __ballot(emit);
-            const uint32_t rank = nr + uint32_t(__popcll(em & ((1ull << tid) - 1ull)));
-            if (__any(bad) || nr + uint32_t(__popcll(em)) > cap) { ok = 0; break; }
-            __threadfence_block();   // every lane read its header position before the slots are rewritten
-            if (emit) {
-                const uint32_t c = uint32_t(min<uint64_t>(cnt, uint64_t(ne) - first));
-                runs[4 * rank + 0] = uint32_t(first);
-                runs[4 * rank + 1] = data;
-                runs[4 * rank + 2] = c | (packed << 31);
-                if (rank < LVL_RUNS_LDS) {
-                    s_runs[4 * rank + 0] = uint32_t(first);
-                    s_runs[4 * rank + 1] = data;
-                    s_runs[4 * rank + 2] = c | (packed << 31);
-                }
-            }
-            nr += uint32_t(__popcll(em));
-            carry += __shfl(x, 63, 64);
-        }
-        if (carry < ne) ok = 0;   // the chain ended (or broke) before the page's levels
-        if (tid == 0) { s_nr = nr; s_ok = ok; }
+        s_nxt[p] = uint16_t(nx);
     }
     __syncthreads();
-    if (!s_ok) {
+    LTS(10);
+    // (2) the chain from position 0 (north_star K2: run boundaries by wavefront passes). The 8-run jump
+    // table by three doubling passes, one thread walks it eight runs a step, then one thread per
+    // 8-run stretch walks the runs in between and marks their headers. Terminal values stay put:
+    // 0xffff (broken chain) and positions >= dn (the section end).
+    {
+        uint32_t J[LVL_PPT];
+        #pragma unroll
+        for (uint32_t k = 0; k < LVL_PPT; k++) {
+            const uint32_t p = uint32_t(tid) + k * LT_NT;
+            const uint32_t q = p < dn ? uint32_t(s_nxt[p]) : 0xffffu;
+            J[k] = q < dn ? uint32_t(s_nxt[q]) : q;
+        }
+        #pragma unroll
+        for (uint32_t k = 0; k < LVL_PPT; k++) s_jmp[uint32_t(tid) + k * LT_NT] = uint16_t(J[k]);
+        __syncthreads();
+        for (int pass = 0; pass < 2; pass++) {   // 2 -> 4 -> 8 runs
+            #pragma unroll
+            for (uint32_t k = 0; k < LVL_PPT; k++) J[k] = J[k] < dn ? uint32_t(s_jmp[J[k]]) : J[k];
+            __syncthreads();
+            #pragma unroll
+            for (uint32_t k = 0; k < LVL_PPT; k++) s_jmp[uint32_t(tid) + k * LT_NT] = uint16_t(J[k]);
+            __syncthreads();
+        }
+    }
+    if (tid == 0) {
+        uint32_t p = 0, k = 0;
+        while (p < dn && k < LVL_S8) {
+            s_s8[k++] = uint16_t(p);
+            const uint32_t q = s_jmp[p];
+            if (q >= dn) break;   // the chain ends (or breaks) within the next 8 runs
+            p = q;
+        }
+        s_ns8 = k;
+    }
+    __syncthreads();
+    const uint32_t ns8 = s_ns8;
+    for (uint32_t j = tid; j < ns8; j += LT_NT) {
+        uint32_t p = s_s8[j];
+        for (uint32_t i = 0; i < LVL_JUMP && p < dn; i++) {
+            const uint32_t q = s_nxt[p];
+            if (q == 0xffffu) break;   // no run header here: the chain is broken
+            atomicOr(&s_mark[p >> 5], 1u << (p & 31u));
+            p = q;
+        }
+    }
+    __syncthreads();
+    LTS(11);
+    // (3) the marked headers in position order: runs decoded at their headers in parallel, their
+    // first entries an exclusive scan of the counts, runs with entries at or past the page's dropped
+    const uint32_t mw = s_mark[tid >> 1];   // a thread's 16 positions: half a mark word
+    const uint32_t mbits = (mw >> (16u * (uint32_t(tid) & 1u))) & 0xffffu;
+    const uint32_t p0 = 16u * uint32_t(tid);
+    uint32_t hcnt[LVL_PPT], hdat[LVL_PPT], hpk = 0;
+    uint64_t csum = 0;
+    #pragma unroll
+    for (uint32_t k = 0; k < LVL_PPT; k++) {
+        hcnt[k] = 0;
+        hdat[k] = 0;
+        if (!((mbits >> k) & 1u)) continue;
+        const uint32_t P = p0 + k;
+        uint32_t h = 0, hl = 0;
+        for (uint32_t b = 0; b < 3; b++) {
+            const uint32_t c = stw[P + b];
+            h |= (c & 0x7fu) << (7 * b);
+            if (!(c & 0x80u)) { hl = b + 1; break; }
+        }
+        const uint32_t packed = h & 1u;
+        hcnt[k] = packed ? (h >> 1) * 8u : (h >> 1);
+        if (packed) hdat[k] = (P + hl) * 8u;
+        else for (uint32_t b = 0; b < ((uint32_t(bw) + 7u) >> 3); b++) hdat[k] |= uint32_t(stw[P + hl + b]) << (8 * b);
+        hpk |= packed << k;
+        csum += hcnt[k];
+    }
+    __shared__ unsigned long long scan64[LT_NT / 64];
+    uint64_t ctot;
+    const uint64_t cbase = block_excl_scan64<LT_NT>(csum, scan64, ctot);
+    uint32_t emask = 0, bad = 0;
+    {
+        uint64_t f = cbase;
+        #pragma unroll
+        for (uint32_t k = 0; k < LVL_PPT; k++) {
+            if (hcnt[k] > 0 && f < ne) {
+                emask |= 1u << k;
+                if (!((hpk >> k) & 1u) && hdat[k] > maxd) bad = 1;
+            }
+            f += hcnt[k];
+        }
+    }
+    __syncthreads();   // scan_tmp is reused
+    uint32_t nr;
+    const uint32_t rbase = block_excl_scan<LT_NT>(__popc(emask), scan_tmp, nr);
+    {
+        uint64_t f = cbase;
+        uint32_t rank = rbase;
+        #pragma unroll
+        for (uint32_t k = 0; k < LVL_PPT; k++) {
+            if ((emask >> k) & 1u && nr <= cap) {   // (emitted: f < ne)
+                const uint32_t c = uint32_t(min<uint64_t>(hcnt[k], uint64_t(ne) - f));
+                const uint32_t cw = c | (((hpk >> k) & 1u) << 31);
+                runs[4 * rank + 0] = uint32_t(f);
+                runs[4 * rank + 1] = hdat[k];
+                runs[4 * rank + 2] = cw;
+                if (rank < LVL_RUNS_LDS) {
+                    s_runs[4 * rank + 0] = uint32_t(f);
+                    s_runs[4 * rank + 1] = hdat[k];
+                    s_runs[4 * rank + 2] = cw;
+                }
+                rank++;
+            }
+            f += hcnt[k];
+        }
+    }
+    __threadfence_block();   // the run records (HBM and LDS) before the other waves read them
+    const bool ok = __syncthreads_or(bad) == 0 && nr <= cap && ctot >= ne;   // (a broken chain covers too few)
+    LTS(12);
+    if (!ok) {
         if (tid == 0) LT[1] = 0;
         return;
     }
-    __threadfence_block();
-    const uint32_t nr = s_nr;
     uint32_t* const R = nr <= LVL_RUNS_LDS ? s_runs : runs;   // the scans below read this copy
     uint32_t carry = 0;
     for (uint32_t r0 = 0; r0 < nr; r0 += LT_NT) {
@@ -3009,11 +3075,12 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
             if (R != runs) R[4 * r + 3] = carry + ex;
         }
         carry += tot;
+        __syncthreads();   // scan_tmp is reused
     }
+    LTS(13);
     // per FBLK block (k_flat_null): the runs it overlaps [r0, r1), the value indices of its first and
     // end entries, the level bytes its packed runs read and the dictionary-id bytes of its values
     __threadfence_block();
-    __syncthreads();
     uint32_t* BT = runs + 4 * cap;
     const uint32_t nblk = (ne + FBLK - 1) / FBLK;
     // dictionary id runs (k_runs, same stream): value index -> bit offset in the id stream
@@ -3078,8 +3145,14 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
         bt[0] = lo; bt[1] = a; bt[2] = vb; bt[3] = ve;
         bt[4] = d0; bt[5] = d1; bt[6] = i0; bt[7] = i1;
     }
-    fit = __all(fit) ? 1u : 0u;   // one wave
+    fit = __syncthreads_and(fit) ? 1u : 0u;
     if (tid == 0) { LT[0] = nr; LT[2] = carry; LT[1] = fit; }
+    LTS(14);
+#ifdef PF_STAMPS
+    if (tid == 0) PSTAMP(15, __builtin_amdgcn_s_memtime() - lt0_);
+    if (tid == 0) PSTAMP(6, nr);
+#endif
+#undef LTS
 }
 
 // k_flat_null: one 512-thread workgroup per 4096-entry block, 8 consecutive entries per thread. The
@@ -4171,10 +4244,10 @@ void launch_nest_decode(const DevChunk* d_chunks, DevPage* d_pages, const int2* 
     if (n_segs > 0) hipLaunchKernelGGL(k_decode_seg, dim3(n_segs), dim3(NT), 0, st, d_chunks, d_pages, d_segs, d_res);
 }
 void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
-                  BaJob* d_bajobs, hipStream_t st) {
+                  BaJob* d_bajobs, hipStream_t st, int idle_grid) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_count_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res, d_bajobs);
-    hipLaunchKernelGGL(k_count, dim3(std::min(n, 64)), dim3(NT), 0, st, d_chunks, d_pages, d_list, n, d_res, d_bajobs);
+    hipLaunchKernelGGL(k_count, dim3(std::min(n, idle_grid)), dim3(NT), 0, st, d_chunks, d_pages, d_list, n, d_res, d_bajobs);
 }
 // PLAIN BYTE_ARRAY walks of jobs [0, n_jobs) over tiles [0, n_tiles).
 void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevChunkResult* d_res, hipStream_t st,
@@ -4333,10 +4406,11 @@ void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
     }
 }
 void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int n_first,
-                   DevChunkResult* d_res, hipStream_t st) {
+                   DevChunkResult* d_res, hipStream_t st, int idle_grid) {
     // n_first: pages at the head of the list that will need k_decode (host-known); the rest are
-    // checked by the stride loop
-    const int g = std::min(n, std::max(32, n_first));   // (32: the stride loop is nearly always idle)
+    // checked by the stride loop, which is nearly always idle: idle_grid blocks (each needs ~23 KiB of
+    // LDS, and the launch ends only once every block has found a CU)
+    const int g = std::min(n, std::max(idle_grid, n_first));
     if (n > 0) hipLaunchKernelGGL(k_decode, dim3(g), dim3(NT), 0, st, d_chunks, d_pages, d_list, n, d_res);
 }
 

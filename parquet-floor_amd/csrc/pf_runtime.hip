@@ -35,12 +35,12 @@ void launch_snappy_litcopy(const SnappyJob*, const int*, int, const int*, hipStr
 void launch_delta(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
 void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_dba_chars(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
-void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, BaJob*, hipStream_t);
+void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, BaJob*, hipStream_t, int);
 void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
 void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool, uint32_t, int, bool);
 void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool);
 void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
-void launch_decode(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
+void launch_decode(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t, int);
 void launch_nest_lvl(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
 void launch_nest_count(const DevChunk*, DevPage*, const int*, int, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_nest_decode(const DevChunk*, DevPage*, const int2*, int, DevChunkResult*, hipStream_t);
@@ -298,7 +298,8 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
     EVREC(ctx, ctx->ev[6], st);
     launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, ctx->max_nwin, d_res, st);
-    if (!(skip & 16u)) launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st);
+    if (!(skip & 16u)) launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st,
+                                       ctx->opts.count_grid);
     launch_nest_count(d_chunks, d_pages, d_nest, n_nest, d_nseg, n_nseg, d_res, st);
     if (!(skip & 4u))
         launch_ba(d_bajobs + ctx->n_ba_dict, n_ba - ctx->n_ba_dict, d_batiles + ctx->n_ba_dict_tiles, n_bt - ctx->n_ba_dict_tiles,
@@ -310,7 +311,8 @@ int enqueue_kernels(pf_ctx* ctx) {
     if (!(skip & 32u)) launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty(),
                                      ctx->opts.null_dict_lds ? ctx->null_dict_lds : 0u, ctx->opts.null_stagger, ctx->opts.flat_split);
     EVREC(ctx, ctx->ev[9], st);
-    if (!(skip & 64u)) launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), ctx->n_decode_first, d_res, st);
+    if (!(skip & 64u)) launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), ctx->n_decode_first, d_res, st,
+                                       ctx->opts.decode_grid);
     launch_nest_decode(d_chunks, d_pages, d_nseg, n_nseg, d_res, st);
     launch_dba_chars(d_chunks, d_pages, d_dba, int(ctx->l_dba.size()), d_res, st);
     EVREC(ctx, ctx->ev[10], st);
@@ -834,6 +836,8 @@ void opts_from_env(pf::PfOpts& o) {
         o.nest_seg_set = true;
     }
     o.dbp_par = on("PF_DBP_PAR", o.dbp_par);
+    o.decode_grid = std::max(1, num("PF_DECODE_GRID", o.decode_grid));
+    o.count_grid = std::max(1, num("PF_COUNT_GRID", o.count_grid));
     const int fb = num("PF_FIX_BLK", 8192);
     o.fix_shift = fb >= 16384 ? 2 : (fb >= 8192 ? 1 : 0);
 }

@@ -30,3 +30,7 @@ for cols in ([0], [ncols - 1], list(range(ncols))):
     n = max(buf[0], 1)
     print(f"cols {len(cols):3d} k_flat_null blocks {buf[0]} | per block cycles: tables {buf[1] / n:.0f} stage {buf[2] / n:.0f} "
           f"levels+scan {buf[3] / n:.0f} gather+store {buf[4] / n:.0f} total {buf[5] / n:.0f}", "status", got["_status"])
+    m = max(buf[8], 1)
+    print(f"          k_lvl pages {buf[8]} runs/page {buf[6] / m:.0f} level bytes/page {buf[7] / m:.0f} | per page cycles: "
+          f"stage {buf[9] / m:.0f} headers {buf[10] / m:.0f} chain {buf[11] / m:.0f} runs {buf[12] / m:.0f} "
+          f"present {buf[13] / m:.0f} blocks {buf[14] / m:.0f} total {buf[15] / m:.0f}")
