@@ -23,6 +23,8 @@ struct PfOpts {
     bool page_null = false;   // PF_PAGE_NULL=1: k_page_null before k_lvl
     bool null_dict_lds = true;   // PF_NULL_DICT_LDS=0: k_flat_null never stages its dictionary
     int null_stagger = 0;     // PF_DEBUG_NULL_STAGGER=k: k_flat_null's blocks > 0 wait k rounds (race tests)
+    uint32_t null_dcap = 0;   // PF_NULL_DCAP=b: k_flat_null's level-byte stage instead of the batch's (16: blocks with
+                              // level bytes do not fit, so k_lvl refuses the page and k_flat_fb decodes it; tests)
     bool flat_split = false;  // PF_FLAT_SPLIT=1: k_flat_fixed + k_flat instead of k_flat_all
     bool piece_order = true;  // PF_PIECE_ORDER=0: Snappy pieces in page order
     unsigned debug_skip = 0;  // PF_DEBUG_SKIP=parse,exec,ba,levels,count,flat,decode (results are wrong)
@@ -189,9 +191,17 @@ constexpr uint32_t RT_BYTES = 16 + 8 * RT_CAP;
 // end value index, level bytes [d0, d1), dictionary-id bytes [i0, i1)} of the block.
 constexpr uint32_t LT_BLOCK_RUNS = 512;    // most runs one k_flat_null block may overlap (its LDS table)
 constexpr uint32_t LT_BT_WORDS = 8;
-constexpr uint32_t NL_DST = 4096;          // level bytes one k_flat_null block stages in LDS
+constexpr uint32_t NL_DST = 4096;          // most level bytes one k_flat_null block stages in LDS
 constexpr uint32_t NULL_DICT_LDS = 16384;   // k_flat_null stages dictionaries up to this many bytes in LDS
-constexpr uint32_t NL_IST = 12288;         // dictionary-id bytes one k_flat_null block stages in LDS
+constexpr uint32_t NL_IST = 12288;         // most dictionary-id bytes one k_flat_null block stages in LDS
+constexpr uint32_t NL_SLACK = 256;         // run-header bytes a block's level / id byte range may add
+// k_flat_null's dynamic LDS, per batch: level bytes (dcap), dictionary-id bytes (icap) a block may
+// stage -- from the batch's widest level / id bit width (host-known: max definition level, dictionary
+// size), FBLK values of it + NL_SLACK, at most NL_DST / NL_IST; k_lvl's block table is checked against
+// the same caps -- and the dictionary bytes it stages (dlds, 0: none). Multiples of 16.
+struct NullCaps {
+    uint32_t dcap, icap, dlds;
+};
 __host__ __device__ inline uint32_t lvl_table_cap(int32_t num_values) {
     // RLE runs are >= 8 repeats and bit-packed groups 8 values for the writers we know (parquet-mr,
     // Arrow): <= 2 runs per 16 entries; a page needing more is left to k_flat / k_decode

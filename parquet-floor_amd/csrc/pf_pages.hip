@@ -18,6 +18,9 @@
 //   k_decode      : per data page: levels -> validity / list offsets / levels; values -> slots
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <type_traits>
+
 #include "pf_device.h"
 #include "pf_snappy_par.h"
 
@@ -2773,6 +2776,26 @@ __global__ __launch_bounds__(NT, PF_FLAT_OCC) void k_flat_all(const DevChunk* __
     flat_block(S.g, chunks, pages, pbk, res);
 }
 
+// k_flat_fb: the blocks k_flat_null did not take (its fallback queue, filled earlier in stream order),
+// grid-stride over a small grid (the queue is nearly always empty: the page had no block table, or
+// k_page_null took it). Same bodies as k_flat_all.
+__global__ __launch_bounds__(NT) void k_flat_fb(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                const int* __restrict__ fbq, DevChunkResult* res) {
+    __shared__ union FlatAllLds {
+        FixedLds f;
+        FlatLds g;
+    } S;
+    const int n = fbq[0];
+    for (int i = int(blockIdx.x); i < n; i += int(gridDim.x)) {
+        const int2 pbk = reinterpret_cast<const int2*>(fbq + 4)[i];
+        if (!flat_fixed_block(S.f, chunks, pages, pbk, res)) {
+            __syncthreads();
+            flat_block(S.g, chunks, pages, pbk, res);
+        }
+        __syncthreads();   // the block's LDS reads are done before the next one reuses it
+    }
+}
+
 // ---- nullable flat pages: definition-level run table + block-parallel decode ------------------
 //
 // north_star K2/K6: "RLE/bit-packed-hybrid expansion of definition levels ... using prefix scans to
@@ -2840,7 +2863,7 @@ constexpr uint32_t LVL_S8 = LVL_NXT / LVL_JUMP;   // walk steps (a run is at lea
 constexpr uint32_t LVL_PPT = LVL_NXT / LT_NT;     // section positions per thread in the table passes
 static_assert(LVL_PPT == 16, "k_lvl's mark words: two threads per 32 positions");
 __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
-                                               DevChunkResult* res) {
+                                               DevChunkResult* res, uint32_t dcap, uint32_t icap) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[LVL_STAGE + 48];
     __shared__ uint32_t scan_tmp[LT_NT / 64];
     __shared__ uint32_t s_ns8, s_ok, s_nr;
@@ -3140,7 +3163,7 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
                 }
             }
         }
-        if (a - lo > LT_BLOCK_RUNS || d1 - d0 + 16u > NL_DST || i1 - i0 + 16u > NL_IST || ve < vb) fit = 0;
+        if (a - lo > LT_BLOCK_RUNS || d1 - d0 + 16u > dcap || i1 - i0 + 16u > icap || ve < vb) fit = 0;
         uint32_t* bt = BT + LT_BT_WORDS * b;
         bt[0] = lo; bt[1] = a; bt[2] = vb; bt[3] = ve;
         bt[4] = d0; bt[5] = d1; bt[6] = i0; bt[7] = i1;
@@ -3155,33 +3178,61 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
 #undef LTS
 }
 
-// k_flat_null: one 512-thread workgroup per 4096-entry block, 8 consecutive entries per thread. The
-// block's level runs, the page's id runs and the level / id bytes the block reads (k_lvl's block
-// table) are all fetched at once into LDS, so the workgroup waits on one round of loads, then on the
-// dictionary gather; no spread step: entry k of a thread takes the value of rank popc(fv & (2^k - 1)).
+// k_flat_null<W>: one 256-thread workgroup per 4096-entry block of a nullable W-byte page, 16
+// consecutive entries per thread. The block's level runs, the page's id runs and the level / id bytes
+// the block reads (k_lvl's block table) are all fetched at once into LDS, so the workgroup waits on one
+// round of loads, then on the dictionary gather; no spread step: entry k of a thread takes the value of
+// rank popc(fv & (2^k - 1)). The stage is latency-bound (Σ block latency / resident blocks), so what
+// sets it is the entries in flight per CU: 16 per lane (round 5; 8 per lane at 512 threads: config 4's
+// flat launch 0.97 -> 0.81 ms, gpurun_out/ntn). The runtime gives the kernel only nullable pages of its
+// width (its own block lists); a page it does not take goes to the fallback queue for k_flat_fb.
 #ifndef PF_NTN
-#define PF_NTN 512
+#define PF_NTN 256
 #endif
 constexpr int NTN = PF_NTN;
 constexpr int NEPT = FBLK / NTN;   // 8 (512 threads) or 16 (256)
 static_assert(NEPT % 4 == 0 && NEPT <= 16, "k_flat_null's stores and present masks");
+// Runs in LDS as {first | packed << 31, data}: a run ends where the next begins (k_lvl's level runs
+// and k_runs' id runs are contiguous), and one sentinel row after the last holds its end.
 struct NullLds {
-    Run drun[LT_BLOCK_RUNS];
-    Run vrun[RUN_CAP];
-    uint32_t dst[NL_DST / 4 + 8];
-    uint32_t ist[NL_IST / 4 + 8];
+    uint2 drun[LT_BLOCK_RUNS + 1];
+    uint2 vrun[RUN_CAP + 1];
     uint32_t vbits[FBLK / 32 + 2];
     uint32_t scan_tmp[NTN / 64];
 };
+__device__ __forceinline__ uint32_t rl_first(uint2 r) { return r.x & 0x7fffffffu; }
+__device__ __forceinline__ int rl_find(const uint2* runs, int nr, uint32_t i) {   // run holding i (runs[0] first <= i)
+    int lo = 0, hi = nr;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (rl_first(runs[mid]) <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
 
-// Dictionaries of at most dlds bytes (dynamic LDS sized by the host to the batch's largest fitting
-// dictionary, <= NULL_DICT_LDS; 0 when the batch has none) are staged in LDS and gathered from there
-// (north_star K3: "dictionary staged in LDS when it fits"); larger ones are gathered from L2 / HBM.
+// Dynamic LDS, sized by the host per batch (NullCaps): the block's level bytes (dcap + 32), its
+// dictionary-id bytes (icap + 32) -- caps from the batch's level and id bit widths, which k_lvl's
+// block table was checked against -- and dictionaries of at most dlds bytes (the batch's largest
+// fitting one, <= NULL_DICT_LDS; 0 when it has none), gathered from LDS (north_star K3: "dictionary
+// staged in LDS when it fits"); larger ones are gathered from L2 / HBM. Config 4 (1-bit levels,
+// 17-bit ids): ~16.6 KiB a workgroup, eight resident per CU (the VGPR limit) instead of five.
+// Fallback queue (device, zeroed with the batch metadata): word 0 counts the (page, block) pairs that
+// start at word 4; k_flat_null appends the blocks of pages it does not take, k_flat_fb decodes them.
+__device__ __forceinline__ void null_fallback(int* fbq, int2 pbk) {
+    if (threadIdx.x == 0) reinterpret_cast<int2*>(fbq + 4)[atomicAdd(fbq, 1)] = pbk;
+}
+
+template <int W>
 __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                                   const int2* __restrict__ blocks, DevChunkResult* res, uint32_t dlds,
-                                                   int stagger) {
+                                                   const int2* __restrict__ blocks, DevChunkResult* res, NullCaps nc,
+                                                   int stagger, int* fbq) {
+    using VT = typename std::conditional<W == 4, uint32_t, uint64_t>::type;
     __shared__ __attribute__((aligned(16))) NullLds S;
-    extern __shared__ __attribute__((aligned(16))) uint64_t DL[];
+    extern __shared__ __attribute__((aligned(16))) uint64_t DYN[];
+    uint32_t* const s_dst = reinterpret_cast<uint32_t*>(DYN);
+    uint32_t* const s_ist = s_dst + (nc.dcap + 32u) / 4u;
+    uint64_t* const DL = reinterpret_cast<uint64_t*>(s_ist + (nc.icap + 32u) / 4u);
+    const uint32_t dlds = nc.dlds;
     const int2 pbk = blocks[blockIdx.x];
 #ifdef PF_DIAG   // diagnostics build (tests): blocks after a page's first start late, after it has finished
     if (stagger && pbk.y > 0)
@@ -3202,23 +3253,27 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
     const uint32_t* LT = pg.lvltab;
-    if (!LT || res[pg.chunk].status != 0 || ck.max_rep != 0 || (ck.width != 4 && ck.width != 8) ||
-        (pg.done & (DONE_FIXED | DONE_PAGE)) || LT[1] != 1u)   // (other widths: k_flat / k_decode; k_page_null took it)
-        // (not DONE_NULL: blocks of this page that finished first set it, and a block starting later must still run)
+    // pages this kernel does not take (whole pages: the conditions are the page's) go to k_flat_fb
+    // (not DONE_NULL: blocks of this page that finished first set it, and a block starting later must still run)
+    if (!LT || res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.width != W ||
+        (pg.done & (DONE_FIXED | DONE_PAGE)) || LT[1] != 1u) {   // (k_page_null took it, or no block table)
+        null_fallback(fbq, pbk);
         return;
+    }
     Sections s;
-    if (!page_sections(pg, ck, s)) return;
     const int enc = pg.encoding;
     const bool dict = is_dict_enc(enc);
-    if (!dict && enc != 0) return;
     const uint32_t* T = pg.runtab;
-    if (dict && !(T != nullptr && T[2] == 1u && T[0] <= uint32_t(RUN_CAP) && s.val_n > 0 && ck.dict_data != nullptr))
+    if (!page_sections(pg, ck, s) || (!dict && enc != 0) ||
+        (dict && !(T != nullptr && T[2] == 1u && T[0] <= uint32_t(RUN_CAP) && s.val_n > 0 && ck.dict_data != nullptr))) {
+        null_fallback(fbq, pbk);
         return;
+    }
     const uint32_t ne = uint32_t(pg.num_values);
     const uint32_t e_begin = blk * FBLK;
     if (blk > 0 && e_begin >= ne) return;
     const uint32_t e_end = min(ne, e_begin + FBLK);
-    const int w = ck.width;
+    constexpr int w = W;
     const int bw = bit_width(uint32_t(ck.max_def));
     const uint32_t maxd = uint32_t(ck.max_def);
     const uint32_t nr = LT[0];
@@ -3230,8 +3285,8 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     const uint32_t idcov = dict ? T[1] : 0u;
     const uint8_t* ids = dict ? s.val + 1 : nullptr;
     const uint64_t ids_n = dict ? s.val_n - 1 : 0;
-    if (r1 < r0 || r1 - r0 > LT_BLOCK_RUNS || r1 > nr || id_bw > 32 || ve < vb || d1 < d0 || d1 - d0 + 16u > NL_DST ||
-        i1 < i0 || i1 - i0 + 16u > NL_IST || (dict && ve > idcov) || (!dict && uint64_t(ve) * uint64_t(w) > s.val_n)) {
+    if (r1 < r0 || (r1 == r0 && e_end > e_begin) || r1 - r0 > LT_BLOCK_RUNS || r1 > nr || id_bw > 32 || ve < vb || d1 < d0 || d1 - d0 + 16u > nc.dcap ||
+        i1 < i0 || i1 - i0 + 16u > nc.icap || (dict && ve > idcov) || (!dict && uint64_t(ve) * uint64_t(w) > s.val_n)) {
         if (tid == 0) set_status(res, pg.chunk, ST_CORRUPT, pi);
         return;
     }
@@ -3240,25 +3295,14 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     const uint32_t nrun = r1 - r0;
     for (uint32_t i = tid; i < nrun; i += NTN) {
         const uint32_t* q = runs + 4 * (r0 + i);
-        Run r;
-        r.first = q[0];
-        r.data = q[1];
-        r.count = q[2] & 0x7fffffffu;
-        r.packed = q[2] >> 31;
-        S.drun[i] = r;
+        const uint32_t f = q[0], d = q[1], c = q[2];
+        S.drun[i] = make_uint2(f | (c & 0x80000000u), d);
+        if (i + 1 == nrun) S.drun[nrun] = make_uint2(f + (c & 0x7fffffffu), 0u);
     }
-    for (uint32_t i = tid; i < vnr; i += NTN) {
-        const uint32_t f = T[4 + 2 * i];
-        const uint32_t nf = i + 1 < vnr ? (T[4 + 2 * (i + 1)] & 0x7fffffffu) : idcov;
-        Run r;
-        r.first = f & 0x7fffffffu;
-        r.count = nf - r.first;
-        r.data = T[5 + 2 * i];
-        r.packed = f >> 31;
-        S.vrun[i] = r;
-    }
-    const uint32_t doff = stage_bytes(S.dst, s.def, s.def_n, d0, d1);
-    const uint32_t ioff = dict ? stage_bytes(S.ist, ids, ids_n, i0, i1) : 0u;
+    for (uint32_t i = tid; i <= vnr; i += NTN)
+        S.vrun[i] = i < vnr ? make_uint2(T[4 + 2 * i], T[5 + 2 * i]) : make_uint2(idcov, 0u);
+    const uint32_t doff = stage_bytes(s_dst, s.def, s.def_n, d0, d1);
+    const uint32_t ioff = dict ? stage_bytes(s_ist, ids, ids_n, i0, i1) : 0u;
     for (uint32_t i = tid; i < FBLK / 32 + 2; i += NTN) S.vbits[i] = 0;
     const bool dl = dict && dlds != 0 && ck.dict_n > 0 && uint64_t(ck.dict_n) * uint64_t(w) <= dlds &&
                     (reinterpret_cast<uintptr_t>(ck.dict_data) & 7u) == 0;
@@ -3269,8 +3313,8 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     }
     __syncthreads();
     NSTAMP(2);
-    const uint8_t* dst8 = reinterpret_cast<const uint8_t*>(S.dst);
-    const uint8_t* ist8 = reinterpret_cast<const uint8_t*>(S.ist);
+    const uint8_t* dst8 = reinterpret_cast<const uint8_t*>(s_dst);
+    const uint8_t* ist8 = reinterpret_cast<const uint8_t*>(s_ist);
     const uint32_t dbase = d0 * 8u - doff * 8u;   // stream bit of LDS bit 0
     const uint32_t ibase = i0 * 8u - ioff * 8u;
     const uint32_t dlim = (d1 - d0 + doff + 16u) * 8u;   // readable LDS bits
@@ -3281,22 +3325,23 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     const uint32_t m = e < e_end ? min(uint32_t(NEPT), e_end - e) : 0u;
     uint32_t fv = 0;
     if (m) {
-        int r = run_find(S.drun, int(nrun), e);
-        const Run R = S.drun[r];
-        if (e + m <= R.first + R.count && (!R.packed || bw == 1)) {   // one run
-            if (!R.packed) fv = R.data == maxd ? ((1u << m) - 1u) : 0u;
+        int r = rl_find(S.drun, int(nrun), e);
+        const uint2 R = S.drun[r];
+        const uint32_t Rf = rl_first(R), Rp = R.x >> 31;
+        if (e + m <= rl_first(S.drun[r + 1]) && (!Rp || bw == 1)) {   // one run
+            if (!Rp) fv = R.y == maxd ? ((1u << m) - 1u) : 0u;
             else {
-                const uint32_t b = R.data + (e - R.first) - dbase;
+                const uint32_t b = R.y + (e - Rf) - dbase;
                 fv = b + m <= dlim ? lds_bits(dst8, b, m) : 0u;
                 bad |= b + m > dlim;
             }
         } else {
             for (uint32_t k = 0; k < m; k++) {
-                while (r + 1 < int(nrun) && e + k >= S.drun[r].first + S.drun[r].count) r++;
-                const Run& Rk = S.drun[r];
-                uint32_t dl = Rk.data;
-                if (Rk.packed) {
-                    const uint32_t b = Rk.data + (e + k - Rk.first) * uint32_t(bw) - dbase;
+                while (r + 1 < int(nrun) && e + k >= rl_first(S.drun[r + 1])) r++;
+                const uint2 Rk = S.drun[r];
+                uint32_t dl = Rk.y;
+                if (Rk.x >> 31) {
+                    const uint32_t b = Rk.y + (e + k - rl_first(Rk)) * uint32_t(bw) - dbase;
                     bad |= b + uint32_t(bw) > dlim;
                     dl = b + uint32_t(bw) <= dlim ? lds_bits(dst8, b, uint32_t(bw)) : 0u;
                 }
@@ -3310,7 +3355,7 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     if (tv != ve - vb) bad = 1;   // the block table disagrees with the levels
     NSTAMP(3);
     const uint32_t gv0 = vb + vo;   // value index of this thread's first present entry
-    uint64_t v[NEPT];
+    VT v[NEPT];
     #pragma unroll
     for (int k = 0; k < NEPT; k++) v[k] = 0;
     if (fv && !bad) {
@@ -3322,12 +3367,12 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
             uint32_t idv[NEPT];
             #pragma unroll
             for (int k = 0; k < NEPT; k++) idv[k] = 0;
-            int vr = run_find(S.vrun, int(vnr), gv0);
-            const Run V0 = S.vrun[vr];
+            int vr = rl_find(S.vrun, int(vnr), gv0);
+            const uint2 V0 = S.vrun[vr];
             // the thread's present values are gv0, gv0 + 1, ...: when one id run holds them all, their
             // ids are consecutive fields of that run (no run search per value)
-            const bool one_run = gv0 + uint32_t(__popc(fv)) <= V0.first + V0.count;
-            const uint32_t b0 = V0.packed ? uint32_t(uint64_t(V0.data) + uint64_t(gv0 - V0.first) * id_bw - ibase) : 0u;
+            const bool one_run = gv0 + uint32_t(__popc(fv)) <= rl_first(S.vrun[vr + 1]);
+            const uint32_t b0 = (V0.x >> 31) ? uint32_t(uint64_t(V0.y) + uint64_t(gv0 - rl_first(V0)) * id_bw - ibase) : 0u;
             const int64_t dn = ck.dict_n;
             uint32_t r = 0;
             #pragma unroll
@@ -3335,19 +3380,19 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
                 if (!((fv >> k) & 1u)) continue;
                 uint32_t id;
                 if (one_run) {
-                    id = V0.data;
-                    if (V0.packed) {
+                    id = V0.y;
+                    if (V0.x >> 31) {
                         const uint32_t b = b0 + r * id_bw;
                         bad |= b + id_bw > ilim;
                         id = b + id_bw <= ilim ? lds_bits(ist8, b, id_bw) : 0u;
                     }
                 } else {
                     const uint32_t gv = gv0 + r;
-                    while (vr + 1 < int(vnr) && gv >= S.vrun[vr].first + S.vrun[vr].count) vr++;
-                    const Run& V = S.vrun[vr];
-                    id = V.data;
-                    if (V.packed) {
-                        const uint32_t b = uint32_t(uint64_t(V.data) + uint64_t(gv - V.first) * id_bw - ibase);
+                    while (vr + 1 < int(vnr) && gv >= rl_first(S.vrun[vr + 1])) vr++;
+                    const uint2 V = S.vrun[vr];
+                    id = V.y;
+                    if (V.x >> 31) {
+                        const uint32_t b = uint32_t(uint64_t(V.y) + uint64_t(gv - rl_first(V)) * id_bw - ibase);
                         bad |= b + id_bw > ilim;
                         id = b + id_bw <= ilim ? lds_bits(ist8, b, id_bw) : 0u;
                     }
@@ -3359,23 +3404,16 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
             const uintptr_t da = reinterpret_cast<uintptr_t>(ck.dict_data);
             if (dl) {
                 #pragma unroll
-                for (int k = 0; k < NEPT; k++)
-                    v[k] = w == 4 ? uint64_t(reinterpret_cast<const uint32_t*>(DL)[idv[k]]) : DL[idv[k]];
+                for (int k = 0; k < NEPT; k++) v[k] = reinterpret_cast<const VT*>(DL)[idv[k]];
             } else if ((da & uintptr_t(w - 1)) == 0) {   // (dictionary pages start 16-byte aligned in scratch)
-                if (w == 4) {
-                    const PF_GLOBAL uint32_t* g = (const PF_GLOBAL uint32_t*)ck.dict_data;
-                    #pragma unroll
-                    for (int k = 0; k < NEPT; k++) v[k] = g[idv[k]];
-                } else {
-                    const PF_GLOBAL uint64_t* g = (const PF_GLOBAL uint64_t*)ck.dict_data;
-                    #pragma unroll
-                    for (int k = 0; k < NEPT; k++) v[k] = g[idv[k]];
-                }
+                const PF_GLOBAL VT* g = (const PF_GLOBAL VT*)ck.dict_data;
+                #pragma unroll
+                for (int k = 0; k < NEPT; k++) v[k] = g[idv[k]];
             } else {
                 #pragma unroll
                 for (int k = 0; k < NEPT; k++) {
                     const uint8_t* src = ck.dict_data + uint64_t(idv[k]) * uint64_t(w);
-                    v[k] = w == 4 ? uint64_t(ld_u32_any(src)) : ld_u64_any(src);
+                    if constexpr (W == 4) v[k] = ld_u32_any(src); else v[k] = ld_u64_any(src);
                 }
             }
         } else {
@@ -3386,20 +3424,14 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
             #pragma unroll
             for (int k = 0; k < NEPT; k++) vi[k] = min(gv0 + uint32_t(__popc(fv & ((1u << k) - 1u))), last);
             if ((reinterpret_cast<uintptr_t>(s.val) & uintptr_t(w - 1)) == 0) {
-                if (w == 4) {
-                    const PF_GLOBAL uint32_t* g = (const PF_GLOBAL uint32_t*)s.val;
-                    #pragma unroll
-                    for (int k = 0; k < NEPT; k++) v[k] = g[vi[k]];
-                } else {
-                    const PF_GLOBAL uint64_t* g = (const PF_GLOBAL uint64_t*)s.val;
-                    #pragma unroll
-                    for (int k = 0; k < NEPT; k++) v[k] = g[vi[k]];
-                }
+                const PF_GLOBAL VT* g = (const PF_GLOBAL VT*)s.val;
+                #pragma unroll
+                for (int k = 0; k < NEPT; k++) v[k] = g[vi[k]];
             } else {
                 #pragma unroll
                 for (int k = 0; k < NEPT; k++) {
                     const uint8_t* src = s.val + uint64_t(vi[k]) * uint64_t(w);
-                    v[k] = w == 4 ? uint64_t(ld_u32_any(src)) : ld_u64_any(src);
+                    if constexpr (W == 4) v[k] = ld_u32_any(src); else v[k] = ld_u64_any(src);
                 }
             }
         }
@@ -3412,10 +3444,9 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
         uint8_t* dst0 = ck.values + (slot_base + e) * uint64_t(w);
         if (m == NEPT && (reinterpret_cast<uintptr_t>(dst0) & 15u) == 0) {
             u32x4* d4 = reinterpret_cast<u32x4*>(dst0);
-            if (w == 4) {
+            if constexpr (W == 4) {
                 #pragma unroll
-                for (int q = 0; q < NEPT / 4; q++)
-                    d4[q] = u32x4{uint32_t(v[4 * q]), uint32_t(v[4 * q + 1]), uint32_t(v[4 * q + 2]), uint32_t(v[4 * q + 3])};
+                for (int q = 0; q < NEPT / 4; q++) d4[q] = u32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
             } else {
                 #pragma unroll
                 for (int q = 0; q < NEPT / 2; q++)
@@ -3425,7 +3456,7 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
             for (uint32_t k = 0; k < m; k++) {
                 uint32_t* d = reinterpret_cast<uint32_t*>(dst0 + uint64_t(k) * uint64_t(w));   // 4-byte aligned
                 d[0] = uint32_t(v[k]);
-                if (w == 8) d[1] = uint32_t(v[k] >> 32);
+                if constexpr (W == 8) d[1] = uint32_t(uint64_t(v[k]) >> 32);
             }
         }
     }
@@ -4383,21 +4414,26 @@ void launch_runs(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
     if (n > 0) hipLaunchKernelGGL(k_runs, dim3(n), dim3(128), 0, st, d_chunks, d_pages, d_list, d_res);
 }
 void launch_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
-                hipStream_t st, bool page_null) {
+                hipStream_t st, bool page_null, NullCaps nc) {
     if (n <= 0) return;
     // page_null (diagnostics option): k_page_null first (one 512-thread workgroup and ~57 KiB of LDS per
     // page; under the bench's four streams its workgroups wait for whole CUs: config 4 5.57 ms with it, 4.47 without)
     if (page_null) hipLaunchKernelGGL(k_page_null, dim3(n), dim3(PN_NT), 0, st, d_chunks, d_pages, d_list, d_res);
-    hipLaunchKernelGGL(k_lvl, dim3(n), dim3(LT_NT), 0, st, d_chunks, d_pages, d_list, d_res);
+    hipLaunchKernelGGL(k_lvl, dim3(n), dim3(LT_NT), 0, st, d_chunks, d_pages, d_list, d_res, nc.dcap, nc.icap);
 }
-void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
-                 hipStream_t st, bool nullable, uint32_t dl, int stagger, bool split) {   // d_list: n (page, block) pairs
-    if (n <= 0) return;
+void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int n4, int n8, int* d_fbq,
+                 DevChunkResult* d_res, hipStream_t st, NullCaps nc, int stagger, bool split) {
+    // d_list: n (page, block) pairs of k_flat_all, then n4 / n8 pairs of nullable 4 / 8-byte pages
+    // (k_flat_null<4> / <8>; they mark their pages DONE_NULL and queue the blocks they do not take in
+    // d_fbq for k_flat_fb). nc: k_flat_null's LDS stages (dictionary: nc.dlds bytes); stagger (diagnostics build,
+    // tests): blocks > 0 of a page wait that many sleep rounds (~3 us each) for block 0
     const int2* blocks = reinterpret_cast<const int2*>(d_list);
-    // pages with nulls first (k_flat_null marks them DONE_NULL), then every other page in one launch
-    // dl: bytes of dictionary k_flat_null stages in LDS; stagger (diagnostics build, tests): blocks > 0 of a
-    // page wait that many sleep rounds (~3 us each) for block 0
-    if (nullable) hipLaunchKernelGGL(k_flat_null, dim3(n), dim3(NTN), dl, st, d_chunks, d_pages, blocks, d_res, dl, stagger);
+    const size_t dyn = size_t(nc.dcap) + 32u + nc.icap + 32u + nc.dlds;
+    if (n4 > 0) hipLaunchKernelGGL(k_flat_null<4>, dim3(n4), dim3(NTN), dyn, st, d_chunks, d_pages, blocks + n, d_res, nc, stagger, d_fbq);
+    if (n8 > 0)
+        hipLaunchKernelGGL(k_flat_null<8>, dim3(n8), dim3(NTN), dyn, st, d_chunks, d_pages, blocks + n + n4, d_res, nc, stagger, d_fbq);
+    if (n4 + n8 > 0) hipLaunchKernelGGL(k_flat_fb, dim3(std::min(n4 + n8, 1024)), dim3(NT), 0, st, d_chunks, d_pages, d_fbq, d_res);
+    if (n <= 0) return;
     if (split) {   // A/B: the two kernels in stream order
         hipLaunchKernelGGL(k_flat_fixed, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
         hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);

@@ -37,8 +37,8 @@ void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hi
 void launch_dba_chars(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_count(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, BaJob*, hipStream_t, int);
 void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
-void launch_flat(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool, uint32_t, int, bool);
-void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool);
+void launch_flat(const DevChunk*, DevPage*, const int*, int, int, int, int*, DevChunkResult*, hipStream_t, NullCaps, int, bool);
+void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool, NullCaps);
 void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t, int);
 void launch_nest_lvl(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
@@ -171,6 +171,7 @@ struct pf_ctx {
     int n_ba_dict = 0, n_ba_dict_tiles = 0;
     bool ba_short_dict = true, ba_short_data = true;   // every walk job's values average <= BA_SHORT bytes: k_ba_tile
     uint32_t null_dict_lds = 0;            // bytes of the largest nullable-page dictionary that fits k_flat_null's LDS stage
+    uint32_t null_dcap = 16, null_icap = 16;   // k_flat_null's level / id byte stages (NullCaps)
     int max_snap_win = 1;                  // index windows of the batch's largest Snappy job (k_snappy_chain's tables)
     uint32_t n_splits = 0;
     SnapWin* d_win = nullptr;              // in d_tokmap: bitmap | lane outs | windows | entry tables
@@ -181,11 +182,12 @@ struct pf_ctx {
     std::vector<pf_column_info> info;
     size_t bits_bytes = 0;
     int n_decode_first = 0;                // l_decode: pages that will need k_decode come first
+    int n_flat_all = 0, n_null4 = 0, n_null8 = 0;   // l_flat: (page, block) pairs of k_flat_all, k_flat_null<4>, <8>
     size_t off_npub = 0, npub_bytes = 0;   // k_nest_lvl / k_dbp_pos window hand-overs (scratch), zeroed before the batch
     int max_nwin = 0, max_dbp_nwin = 0;
     size_t out_bytes = 0;                  // values / offsets / levels arena extent of the last decode
     size_t off_chunks = 0, off_pages = 0, off_jobs = 0, off_lists = 0, off_res = 0, meta_bytes = 0;
-    size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0, off_bajobs = 0, off_batiles = 0;
+    size_t off_pieces = 0, off_splits = 0, off_fallback = 0, off_wins = 0, off_bajobs = 0, off_batiles = 0, off_nfbq = 0;
     uint64_t chars_need = 0;
     const uint8_t* d_bytes = nullptr;
     int reruns = 0;
@@ -294,7 +296,9 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_delta(d_chunks, d_pages, d_delta, int(ctx->l_delta.size()), ctx->max_dbp_nwin, d_res, st);
     EVREC(ctx, ctx->ev[5], st);
     if (!(skip & 8u)) launch_runs(d_chunks, d_pages, d_runs, int(ctx->l_runs.size()), d_res, st);
-    if (!(skip & 8u)) launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st, ctx->opts.page_null);
+    const NullCaps ncaps{ctx->opts.null_dcap ? ctx->opts.null_dcap : ctx->null_dcap, ctx->null_icap,
+                         ctx->opts.null_dict_lds ? ctx->null_dict_lds : 0u};
+    if (!(skip & 8u)) launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st, ctx->opts.page_null, ncaps);
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
     EVREC(ctx, ctx->ev[6], st);
     launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, ctx->max_nwin, d_res, st);
@@ -308,8 +312,9 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_scan(d_chunks, d_pages, d_scan, int(ctx->l_scan.size()), d_res, static_cast<uint8_t*>(ctx->d_chars.p),
                 ctx->d_chars.cap, used, st);
     EVREC(ctx, ctx->ev[8], st);
-    if (!(skip & 32u)) launch_flat(d_chunks, d_pages, d_flat, int(ctx->l_flat.size() / 2), d_res, st, !ctx->l_lvl.empty(),
-                                     ctx->opts.null_dict_lds ? ctx->null_dict_lds : 0u, ctx->opts.null_stagger, ctx->opts.flat_split);
+    if (!(skip & 32u))
+        launch_flat(d_chunks, d_pages, d_flat, ctx->n_flat_all, ctx->n_null4, ctx->n_null8, reinterpret_cast<int*>(meta + ctx->off_nfbq),
+                    d_res, st, ncaps, ctx->opts.null_stagger, ctx->opts.flat_split);
     EVREC(ctx, ctx->ev[9], st);
     if (!(skip & 64u)) launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), ctx->n_decode_first, d_res, st,
                                        ctx->opts.decode_grid);
@@ -818,6 +823,7 @@ void opts_from_env(pf::PfOpts& o) {
     o.ba_fused = on("PF_BA_FUSED", o.ba_fused);
     o.page_null = on("PF_PAGE_NULL", o.page_null);
     o.null_dict_lds = on("PF_NULL_DICT_LDS", o.null_dict_lds);
+    o.null_dcap = uint32_t(std::max(0, num("PF_NULL_DCAP", 0))) & ~15u;
     o.null_stagger = num("PF_DEBUG_NULL_STAGGER", o.null_stagger);
     o.flat_split = on("PF_FLAT_SPLIT", o.flat_split);
     o.piece_order = on("PF_PIECE_ORDER", o.piece_order);
@@ -984,6 +990,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_flat.clear(); ctx->l_decode.clear();
     ctx->l_runs.clear(); ctx->l_dlen.clear(); ctx->l_dba.clear(); ctx->l_lvl.clear(); ctx->l_djobs.clear();
     ctx->null_dict_lds = 0;
+    ctx->null_dcap = ctx->null_icap = 16;
     ctx->l_nest.clear(); ctx->l_nseg.clear();
     // nested pages: entries per segment (k_nest_*); PF_NEST_SEG=n (tests) sets it and sends every
     // eligible nested page, one segment or more, down the segment path (0: none)
@@ -1243,6 +1250,15 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                 const uint64_t db = uint64_t(std::max<int64_t>(lc.dict_n, 0)) * uint64_t(std::max(lc.width, 0));
                 if (lc.dict_page >= 0 && db > 0 && db <= NULL_DICT_LDS)
                     ctx->null_dict_lds = std::max(ctx->null_dict_lds, uint32_t(align_up(db, 256)));
+                // level / id byte stages: FBLK values of the level width / the dictionary's id width
+                // (bit width of its largest index, as writers choose it) + run headers
+                auto bits = [](uint64_t v) { int b = 0; while (v) { b++; v >>= 1; } return b; };
+                auto cap = [](int b, uint32_t most) {
+                    return uint32_t(std::min<uint64_t>(most, align_up(uint64_t(FLAT_BLK) * uint64_t(b) / 8 + NL_SLACK, 16)));
+                };
+                ctx->null_dcap = std::max(ctx->null_dcap, cap(bits(uint64_t(std::max(lc.max_def, 0))), NL_DST));
+                if (lc.dict_page >= 0)
+                    ctx->null_icap = std::max(ctx->null_icap, cap(bits(uint64_t(std::max<int64_t>(lc.dict_n, 1) - 1)), NL_IST));
             }
             if (pp.dbp_off != ~0ull) {
                 pg.dbp = S + pp.dbp_off;
@@ -1316,10 +1332,12 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     // gathered through one XCD's L2 instead of all eight (config 4: 400 KB dictionaries); such chunks
     // go to the least loaded label, all other blocks then fill the labels evenly. Labels are
     // interleaved into the grid; short ones are padded with (-1, 0).
+    // Three such grids, one after the other in l_flat: k_flat_all's, then the blocks of nullable 4- and
+    // 8-byte pages (k_flat_null<4> / <8>, which queue what they do not take for k_flat_fb).
     constexpr uint32_t STICKY_DICT = 64u << 10;
-    std::vector<int> xq[8];
-    std::vector<int> spread;
-    std::vector<std::vector<int>> sticky(static_cast<size_t>(n_chunks));
+    std::vector<int> spread[3];
+    std::vector<std::vector<int>> sticky[3];
+    for (auto& v : sticky) v.resize(static_cast<size_t>(n_chunks));
     std::vector<int> decode_first;
     for (size_t i = 0; i < ctx->pages.size(); i++) {
         const DevPage& pg = ctx->pages[i];
@@ -1335,9 +1353,11 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             const int sh = (ck.ptype != PF_BYTE_ARRAY && pg.lvltab == nullptr) ? fix_shift : 0;
             const int64_t bsz = FLAT_BLK << sh;
             const int nb = std::max(1, int((int64_t(pg.num_values) + bsz - 1) / bsz));
-            const bool big_dict = ck.dict_page >= 0 && ctx->pages[size_t(ck.dict_page)].body_len > STICKY_DICT &&
-                                  (pg.encoding == PF_ENC_PLAIN_DICTIONARY || pg.encoding == PF_ENC_RLE_DICTIONARY);
-            std::vector<int>& q = big_dict ? sticky[size_t(pg.chunk)] : spread;
+            const bool dict_enc = pg.encoding == PF_ENC_PLAIN_DICTIONARY || pg.encoding == PF_ENC_RLE_DICTIONARY;
+            const bool big_dict = ck.dict_page >= 0 && ctx->pages[size_t(ck.dict_page)].body_len > STICKY_DICT && dict_enc;
+            const int grid = (pg.lvltab != nullptr && ck.ptype != PF_BYTE_ARRAY && (dict_enc || pg.encoding == PF_ENC_PLAIN))
+                                 ? (ck.width == 4 ? 1 : (ck.width == 8 ? 2 : 0)) : 0;
+            std::vector<int>& q = big_dict ? sticky[grid][size_t(pg.chunk)] : spread[grid];
             for (int b = 0; b < nb; b++) { q.push_back(int(i)); q.push_back(b | (sh << 28)); }
         }
         // k_decode does the pages the flat kernels do not take: nested pages and encodings other than
@@ -1351,34 +1371,39 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     }
     ctx->n_decode_first = int(decode_first.size());
     ctx->l_decode.insert(ctx->l_decode.begin(), decode_first.begin(), decode_first.end());
-    {
+    int n_grid[3] = {};
+    for (int gi = 0; gi < 3; gi++) {
+        std::vector<int> xq[8];
         size_t load[8] = {};
         std::vector<int> order(static_cast<size_t>(n_chunks));
         for (int c = 0; c < n_chunks; c++) order[size_t(c)] = c;
-        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return sticky[size_t(a)].size() > sticky[size_t(b)].size(); });
+        const auto& sk = sticky[gi];
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return sk[size_t(a)].size() > sk[size_t(b)].size(); });
         for (int c : order) {
-            if (sticky[size_t(c)].empty()) continue;
+            if (sk[size_t(c)].empty()) continue;
             const int x = int(std::min_element(load, load + 8) - load);
-            xq[x].insert(xq[x].end(), sticky[size_t(c)].begin(), sticky[size_t(c)].end());
-            load[x] += sticky[size_t(c)].size() / 2;
+            xq[x].insert(xq[x].end(), sk[size_t(c)].begin(), sk[size_t(c)].end());
+            load[x] += sk[size_t(c)].size() / 2;
         }
-        for (size_t k = 0; k + 1 < spread.size(); k += 2) {
+        const std::vector<int>& sp = spread[gi];
+        for (size_t k = 0; k + 1 < sp.size(); k += 2) {
             const int x = int(std::min_element(load, load + 8) - load);
-            xq[x].push_back(spread[k]);
-            xq[x].push_back(spread[k + 1]);
+            xq[x].push_back(sp[k]);
+            xq[x].push_back(sp[k + 1]);
             load[x]++;
         }
         const size_t longest = *std::max_element(load, load + 8);
-        if (longest) {
-            ctx->l_flat.assign(2 * 8 * longest, 0);
-            for (size_t k = 0; k < longest; k++)
-                for (int x = 0; x < 8; x++) {
-                    const bool have = k < load[x];
-                    ctx->l_flat[2 * (8 * k + x)] = have ? xq[x][2 * k] : -1;
-                    ctx->l_flat[2 * (8 * k + x) + 1] = have ? xq[x][2 * k + 1] : 0;
-                }
-        }
+        for (size_t k = 0; k < longest; k++)
+            for (int x = 0; x < 8; x++) {
+                const bool have = k < load[x];
+                ctx->l_flat.push_back(have ? xq[x][2 * k] : -1);
+                ctx->l_flat.push_back(have ? xq[x][2 * k + 1] : 0);
+            }
+        n_grid[gi] = int(8 * longest);
     }
+    ctx->n_flat_all = n_grid[0];
+    ctx->n_null4 = n_grid[1];
+    ctx->n_null8 = n_grid[2];
     mark();
     // k_snappy_litcopy candidates (k_snappy_head decides): dictionary pages, and data pages that did
     // not compress (a stream of literals only; one literal is read in place instead)
@@ -1411,6 +1436,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_wins = take(m, sizeof(int2) * ctx->wins.size());
     ctx->off_bajobs = take(m, sizeof(BaJob) * ctx->bajobs.size());
     ctx->off_batiles = take(m, sizeof(int2) * ctx->ba_tiles.size());
+    ctx->off_nfbq = take(m, 16 + sizeof(int2) * size_t(ctx->n_null4 + ctx->n_null8), 16);   // k_flat_null's fallback queue
     m = take(m, 256) + 256;   // arena counter lives in the last 256 bytes
     ctx->meta_bytes = m;
     HIPCHK(ctx, ctx->d_meta.ensure(m));

@@ -136,6 +136,39 @@ def test_null_blocks_staggered(oracle, tmp_path, switches, page_null):
             assert_chunk_equal(got[(0, c)], of.decode(0, c), f"column {c} page_null={page_null}")
 
 
+@pytest.mark.parametrize("stagger", ["0", "100"])
+def test_null_fallback_queue(oracle, tmp_path, switches, stagger):
+    """Pages k_flat_null does not take go to its fallback queue and k_flat_fb decodes them (round 5:
+    k_flat_all no longer walks the nullable blocks). PF_NULL_DCAP=16 leaves no room for any block's
+    level bytes, so k_lvl refuses every nullable page (fit word 0) and all of them take that path;
+    INT32 / INT64 / DOUBLE dictionary columns and a PLAIN INT64 one, 30 % nulls, bit-exact."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from pfloor.decoder import GpuDecoder, decode_file
+    rng = np.random.default_rng(11)
+    n = 50_000
+    cols = {}
+    for c, typ in enumerate((np.int32, np.int64, np.float64)):
+        pool = rng.integers(-2**31, 2**31 - 1, 2000).astype(typ)
+        cols[f"c{c}"] = pa.array(pool[rng.integers(0, len(pool), n)], mask=rng.random(n) < 0.3)
+    cols["p"] = pa.array(rng.integers(0, 1 << 40, n), mask=rng.random(n) < 0.3)
+    path = str(tmp_path / "fbq.parquet")
+    pq.write_table(pa.table(cols), path, compression="snappy", row_group_size=n, use_dictionary=["c0", "c1", "c2"])
+    with switches(PF_PAGE_NULL="0", PF_NULL_DCAP="16", PF_DEBUG_NULL_STAGGER=stagger):
+        d = GpuDecoder(0)
+        try:
+            got = decode_file(path, decoder=d)
+            flags = _done(d)
+        finally:
+            d.close()
+    assert got["_status"] == 0, got["_error"]
+    with oracle.open(path) as of:
+        for c in range(4):
+            assert_chunk_equal(got[(0, c)], of.decode(0, c), f"column {c} via k_flat_fb")
+    nullable = [f for f in flags if f[0] & 4 or f[1] != 0]
+    assert not nullable, flags   # no page was taken by k_flat_null / k_page_null
+
+
 @pytest.mark.parametrize("page_null", ["0", "1"])
 def test_null_blocks_concurrent(tmp_path, page_null):
     """Two contexts decoding nullable multi-block pages at once, with k_page_null off (every page
