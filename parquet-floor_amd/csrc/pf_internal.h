@@ -23,6 +23,7 @@ struct PfOpts {
     bool page_null = false;   // PF_PAGE_NULL=1: k_page_null before k_lvl
     bool null_dict_lds = true;   // PF_NULL_DICT_LDS=0: k_flat_null never stages its dictionary
     int null_stagger = 0;     // PF_DEBUG_NULL_STAGGER=k: k_flat_null's blocks > 0 wait k rounds (race tests)
+    bool nest_timeout = false;   // PF_DEBUG_NEST_TIMEOUT=1: every k_nest_lvl hand-over times out (whole-page path; tests)
     uint32_t null_dcap = 0;   // PF_NULL_DCAP=b: k_flat_null's level-byte stage instead of the batch's (16: blocks with
                               // level bytes do not fit, so k_lvl refuses the page and k_flat_fb decodes it; tests)
     bool flat_split = false;  // PF_FLAT_SPLIT=1: k_flat_fixed + k_flat instead of k_flat_all
@@ -210,7 +211,9 @@ __host__ __device__ inline uint32_t lvl_table_cap(int32_t num_values) {
 
 // One PLAIN BYTE_ARRAY length walk (a BYTE_ARRAY dictionary page, or the values section of a
 // PLAIN BYTE_ARRAY data page), done tile-parallel by the k_ba_* kernels (pf_pages.hip).
-enum : int32_t { BA_OK = 0, BA_FALLBACK = 1, BA_SKIP = 2 };
+// BA_RELINK: the fused tile pass (k_ba_tile) rejected the job -- a value longer than its halo, or
+// filters it could not separate -- and k_ba_fallback re-links it over the whole job before any walk
+enum : int32_t { BA_OK = 0, BA_FALLBACK = 1, BA_SKIP = 2, BA_RELINK = 3 };
 struct BaJob {
     const uint8_t* p;         // stream (data pages: set by k_count)
     uint32_t* pos;            // out: chars start of value k

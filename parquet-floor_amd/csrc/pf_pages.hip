@@ -18,9 +18,6 @@
 //   k_decode      : per data page: levels -> validity / list offsets / levels; values -> slots
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
-#include <type_traits>
-
 #include "pf_device.h"
 #include "pf_snappy_par.h"
 
@@ -509,8 +506,9 @@ __global__ __launch_bounds__(NT) void k_ba_link(BaJob* __restrict__ jobs, const 
 // and checks the chain locally: every accepted value of the tile must end exactly at the next accepted
 // position (and the job's first accepted position is 0); with the count check of k_ba_scan that is
 // k_ba_verify's test. A value longer than BA_HALO - 4 bytes is not linked here: its page fails the count
-// or the chain check and takes the exact fallback walk, like any page the filters cannot separate, so
-// the emitted positions are always the verified true chain.
+// or the chain check (BA_RELINK) and k_ba_fallback re-links it over the whole job (ba_relink_wg, any
+// value length) before it would take the exact walk, so the emitted positions are always the verified
+// true chain.
 constexpr int BA_HALO = 128;
 constexpr uint32_t BA_XW = (2 * BA_HALO) / 32;                       // halo words before the tile
 constexpr uint32_t BA_NW = BA_XW + BA_TILE / 32 + BA_HALO / 32;        // words of the window
@@ -646,7 +644,7 @@ __global__ __launch_bounds__(NT) void k_ba_tile(BaJob* __restrict__ jobs, const 
     uint32_t tot;
     block_excl_scan<NT>(__popc(acc), tmp, tot);
     if (threadIdx.x == 0) J.tile_cnt[jt.y] = tot;
-    if (__syncthreads_or(bad) && threadIdx.x == 0) atomicExch(&J.state, int32_t(BA_FALLBACK));
+    if (__syncthreads_or(bad) && threadIdx.x == 0) atomicExch(&J.state, int32_t(BA_RELINK));
 }
 
 __global__ __launch_bounds__(NT) void k_ba_count(BaJob* __restrict__ jobs, const int2* __restrict__ tiles) {
@@ -665,7 +663,7 @@ __global__ __launch_bounds__(NT) void k_ba_count(BaJob* __restrict__ jobs, const
     if (threadIdx.x == 0) J.tile_cnt[jt.y] = tot;
 }
 
-__global__ __launch_bounds__(NT) void k_ba_scan(BaJob* __restrict__ jobs) {
+__global__ __launch_bounds__(NT) void k_ba_scan(BaJob* __restrict__ jobs, int32_t fail_state) {
     __shared__ uint32_t tmp[NT / 64];
     BaJob& J = jobs[blockIdx.x];
     if (J.state != BA_OK) return;
@@ -679,7 +677,7 @@ __global__ __launch_bounds__(NT) void k_ba_scan(BaJob* __restrict__ jobs) {
         run += tot;
     }
     if (threadIdx.x == 0 && int64_t(run) != J.count) {
-        J.state = BA_FALLBACK;
+        J.state = fail_state;   // (fused: BA_RELINK; round-3 kernels: BA_FALLBACK)
         PSTAMP(14, 1);
         PSTAMP(15, run > uint64_t(J.count) ? run - uint64_t(J.count) : 0);
     }
@@ -740,13 +738,102 @@ __global__ __launch_bounds__(NT) void k_ba_verify(BaJob* __restrict__ jobs, cons
     if (__syncthreads_or(bad) && threadIdx.x == 0) { atomicExch(&J.state, int32_t(BA_FALLBACK)); PSTAMP(6, 1); }
 }
 
+// A job k_ba_tile rejected (BA_RELINK), in one workgroup: k_ba_link's rule over the job's whole
+// candidate bitmap (k_ba_tile wrote it; successors at any distance, so values of any length), then
+// k_ba_count / k_ba_scan / k_ba_emit / k_ba_verify's count, emit and chain check over the job's words
+// in order. Returns -1 on every thread when the chain does not verify (the exact walk takes the job);
+// otherwise the job's chars on the thread holding its last value and 0 on the others.
+// Link words are read back with agent-scope loads (their bits were set by global atomics).
+__device__ int64_t ba_relink_wg(BaJob& J, uint32_t* tmp) {
+    const uint32_t n = J.n;
+    const int64_t count = J.count;
+    if (n == 0 || count <= 0) return -1;
+    const uint32_t nw = (n + 31u) / 32u;
+    const uint8_t* p = J.p;
+    const uint32_t* cand = J.cand;
+    uint32_t* l1 = J.link1;
+    uint32_t* l2 = J.link2;
+    auto ld = [](const uint32_t* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    for (uint32_t w = threadIdx.x; w < nw; w += NT) { l1[w] = w == 0 ? 1u : 0u; l2[w] = w == 0 ? 1u : 0u; }
+    __syncthreads();
+    for (int level = 1; level <= 2; level++) {   // link1: successors of candidates; link2: of link1 members
+        uint32_t* to = level == 1 ? l1 : l2;
+        for (uint32_t w = threadIdx.x; w < nw; w += NT) {
+            uint32_t m = cand[w];
+            if (level == 2) m &= ld(l1 + w);
+            while (m) {
+                const uint32_t q = w * 32u + uint32_t(__ffs(m) - 1);
+                m &= m - 1;
+                const uint64_t sv = uint64_t(q) + 4 + ld32le(p, q, n);
+                if (sv < n && ((cand[sv >> 5] >> (sv & 31u)) & 1u)) atomicOr(&to[sv >> 5], 1u << (sv & 31u));
+            }
+        }
+        __syncthreads();
+    }
+    // accepted = cand & link2: emit by rank, then check the chain (value k + 1 starts where k ends)
+    int64_t run = 0;
+    for (uint32_t b = 0; b < nw; b += NT) {
+        const uint32_t w = b + threadIdx.x;
+        uint32_t m = w < nw ? cand[w] & ld(l2 + w) : 0u;
+        uint32_t tot;
+        int64_t k = run + block_excl_scan<NT>(__popc(m), tmp, tot);
+        while (m) {
+            const uint32_t q = w * 32u + uint32_t(__ffs(m) - 1);
+            m &= m - 1;
+            if (k < count) {
+                J.pos[k] = q + 4;
+                if (J.len) J.len[k] = ld32le(p, q, n);
+            }
+            k++;
+        }
+        run += tot;
+    }
+    if (run != count) return -1;   // (uniform: every thread ran the same scans)
+    __syncthreads();
+    int bad = 0;
+    int64_t chars = 0;
+    run = 0;
+    for (uint32_t b = 0; b < nw; b += NT) {
+        const uint32_t w = b + threadIdx.x;
+        uint32_t m = w < nw ? cand[w] & ld(l2 + w) : 0u;
+        uint32_t tot;
+        int64_t k = run + block_excl_scan<NT>(__popc(m), tmp, tot);
+        while (m) {
+            const uint32_t q = w * 32u + uint32_t(__ffs(m) - 1);
+            m &= m - 1;
+            const uint64_t nq = uint64_t(q) + 4 + ld32le(p, q, n);
+            if (k == 0 && q != 0) bad = 1;
+            if (k + 1 < count) bad |= ld(J.pos + k + 1) != nq + 4;
+            else chars = int64_t(nq) - 4 * count;   // (k + 1 == count: run == count)
+            k++;
+        }
+        run += tot;
+    }
+    if (__syncthreads_or(bad)) return -1;
+    return chars;   // (the thread that holds the last value; 0 on the others)
+}
+
 // Grid-stride over the jobs with a small grid: nearly every walk was accepted by the checks above,
 // and a block per job (21 KB of LDS each) would wait for CUs held by other streams' kernels.
 __global__ __launch_bounds__(NT) void k_ba_fallback(BaJob* __restrict__ jobs, int n_jobs, DevChunkResult* res) {
     __shared__ BinWalkLds W;
+    __shared__ long long s_chars;
     for (int j = blockIdx.x; j < n_jobs; j += gridDim.x) {
         BaJob& J = jobs[j];
-        if (J.state != BA_FALLBACK) continue;
+        if (J.state == BA_RELINK) {
+            if (threadIdx.x == 0) s_chars = 0;
+            __syncthreads();
+            const int64_t c = ba_relink_wg(J, W.scan);   // (c < 0 on every thread or on none)
+            if (c > 0) atomicAdd(reinterpret_cast<unsigned long long*>(&s_chars), (unsigned long long)c);
+            __syncthreads();
+            if (c >= 0) {
+                if (threadIdx.x == 0 && J.chars_out) *J.chars_out = s_chars;
+                __syncthreads();
+                continue;
+            }
+        } else if (J.state != BA_FALLBACK) {
+            continue;
+        }
         const int64_t t = binary_walk_wg(J.p, J.n, J.count, J.pos, J.len, W);
         if (threadIdx.x == 0) {
             if (t < 0) set_status(res, J.chunk, ST_CORRUPT, J.page);
@@ -2103,8 +2190,10 @@ __global__ __launch_bounds__(64) void k_snappy_head(SnappyJob* __restrict__ jobs
         if (p == n && o == J.dst_len && cnt > 0) {
             J.lit = cnt;
             fb[j] = FB_LITCOPY;
+            return;
         }
-        return;
+        // not a literal-only stream after all (a copy token, or more than LC_MAX literals): a data
+        // page still gets the VALUES setup below (the partial table is overwritten by k_snappy_index)
     }
     if (pg.flags & PG_DICT) return;
     if (one) {
@@ -2779,7 +2868,7 @@ __global__ __launch_bounds__(NT, PF_FLAT_OCC) void k_flat_all(const DevChunk* __
 // k_flat_fb: the blocks k_flat_null did not take (its fallback queue, filled earlier in stream order),
 // grid-stride over a small grid (the queue is nearly always empty: the page had no block table, or
 // k_page_null took it). Same bodies as k_flat_all.
-__global__ __launch_bounds__(NT) void k_flat_fb(const DevChunk* __restrict__ chunks, DevPage* pages,
+__global__ __launch_bounds__(NT, PF_FLAT_OCC) void k_flat_fb(const DevChunk* __restrict__ chunks, DevPage* pages,
                                                 const int* __restrict__ fbq, DevChunkResult* res) {
     __shared__ union FlatAllLds {
         FixedLds f;
@@ -2866,7 +2955,7 @@ __global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chun
                                                DevChunkResult* res, uint32_t dcap, uint32_t icap) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[LVL_STAGE + 48];
     __shared__ uint32_t scan_tmp[LT_NT / 64];
-    __shared__ uint32_t s_ns8, s_ok, s_nr;
+    __shared__ uint32_t s_ns8;
     // next-header positions of every byte position (0xffff: not a header, or its run passes the
     // section end; dn: the chain ends there), then the page's dictionary-id runs (k_runs) for the
     // block table
@@ -3222,11 +3311,14 @@ __device__ __forceinline__ void null_fallback(int* fbq, int2 pbk) {
     if (threadIdx.x == 0) reinterpret_cast<int2*>(fbq + 4)[atomicAdd(fbq, 1)] = pbk;
 }
 
+template <int W> struct WidthType { using type = uint64_t; };
+template <> struct WidthType<4> { using type = uint32_t; };
+
 template <int W>
 __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ chunks, DevPage* pages,
                                                    const int2* __restrict__ blocks, DevChunkResult* res, NullCaps nc,
                                                    int stagger, int* fbq) {
-    using VT = typename std::conditional<W == 4, uint32_t, uint64_t>::type;
+    using VT = typename WidthType<W>::type;
     __shared__ __attribute__((aligned(16))) NullLds S;
     extern __shared__ __attribute__((aligned(16))) uint64_t DYN[];
     uint32_t* const s_dst = reinterpret_cast<uint32_t*>(DYN);
@@ -3918,7 +4010,7 @@ constexpr uint64_t NL_CMAX = (1ull << 40) - 1;   // count field saturates (the e
 constexpr uint32_t NL_JNONE = 0xFFFu, NL_JCMAX = 0xFFFFFu;   // J: no exit inside the window; saturated entries
 static_assert(NEST_WIN <= 2048, "J packs window-relative exits in 12 bits");
 __global__ __launch_bounds__(NL_NT) void k_nest_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
-                                                    DevChunkResult* res) {
+                                                    DevChunkResult* res, uint32_t spin_cap) {
     __shared__ __attribute__((aligned(16))) uint32_t st[(NEST_WIN + 64) / 4];
     __shared__ uint64_t X[NEST_WIN];   // per position: entries to the exit << 24 | exit (window-relative, NL_END, NL_FAR)
     // the same after 5 rounds, packed in 32 bits: jumps over >= 32 runs (or to the exit), for the checkpoint
@@ -3992,10 +4084,13 @@ __global__ __launch_bounds__(NL_NT) void k_nest_lvl(const DevChunk* __restrict__
         bool ok = true;
         if (w > 0) {
             const WinPub& pv = pub[w - 1];
-            uint32_t spins = 0;   // (bounded: a hand-over that never comes fails the chunk instead of hanging)
-            while (__hip_atomic_load(&pv.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 && ++spins < (1u << 22))
+            // bounded (spin_cap: 2^22; the diagnostics option nest_timeout makes it 0, so every hand-over
+            // "times out"): a hand-over that never comes sends the page to the whole-page path (below)
+            // instead of hanging
+            uint32_t spins = 0;
+            while (__hip_atomic_load(&pv.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 && ++spins < spin_cap)
                 __builtin_amdgcn_s_sleep(2);
-            ok = spins < (1u << 22);
+            ok = spins < spin_cap;
             tp = __hip_atomic_load(&pv.p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             te = __hip_atomic_load(&pv.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             tst = __hip_atomic_load(&pv.st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -4257,10 +4352,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PF_DSEG_WAVE
 
 // ---- launchers -------------------------------------------------------------------------------
 void launch_nest_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int max_nwin, DevChunkResult* d_res,
-                     hipStream_t st) {
+                     hipStream_t st, bool force_timeout) {
     // windows in blockIdx.x: a window waits on the one before it, which the dispatcher starts first
     if (n > 0 && max_nwin > 0)
-        hipLaunchKernelGGL(k_nest_lvl, dim3(max_nwin, 2, n), dim3(NL_NT), 0, st, d_chunks, d_pages, d_list, d_res);
+        hipLaunchKernelGGL(k_nest_lvl, dim3(max_nwin, 2, n), dim3(NL_NT), 0, st, d_chunks, d_pages, d_list, d_res,
+                           force_timeout ? 0u : (1u << 22));
 }
 void launch_nest_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, const int2* d_segs, int n_segs,
                        DevChunkResult* d_res, hipStream_t st) {
@@ -4295,7 +4391,7 @@ void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevC
     } else {
         hipLaunchKernelGGL(k_ba_tile, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
     }
-    hipLaunchKernelGGL(k_ba_scan, dim3(n_jobs), dim3(NT), 0, st, d_jobs);
+    hipLaunchKernelGGL(k_ba_scan, dim3(n_jobs), dim3(NT), 0, st, d_jobs, fused ? int32_t(BA_RELINK) : int32_t(BA_FALLBACK));
     hipLaunchKernelGGL(k_ba_emit, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
     if (!fused) hipLaunchKernelGGL(k_ba_verify, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
     hipLaunchKernelGGL(k_ba_fallback, dim3(std::min(n_jobs, 64)), dim3(NT), 0, st, d_jobs, n_jobs, d_res);
@@ -4432,7 +4528,7 @@ void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
     if (n4 > 0) hipLaunchKernelGGL(k_flat_null<4>, dim3(n4), dim3(NTN), dyn, st, d_chunks, d_pages, blocks + n, d_res, nc, stagger, d_fbq);
     if (n8 > 0)
         hipLaunchKernelGGL(k_flat_null<8>, dim3(n8), dim3(NTN), dyn, st, d_chunks, d_pages, blocks + n + n4, d_res, nc, stagger, d_fbq);
-    if (n4 + n8 > 0) hipLaunchKernelGGL(k_flat_fb, dim3(std::min(n4 + n8, 1024)), dim3(NT), 0, st, d_chunks, d_pages, d_fbq, d_res);
+    if (n4 + n8 > 0) hipLaunchKernelGGL(k_flat_fb, dim3(n4 + n8 < 1024 ? n4 + n8 : 1024), dim3(NT), 0, st, d_chunks, d_pages, d_fbq, d_res);
     if (n <= 0) return;
     if (split) {   // A/B: the two kernels in stream order
         hipLaunchKernelGGL(k_flat_fixed, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);

@@ -41,7 +41,7 @@ void launch_flat(const DevChunk*, DevPage*, const int*, int, int, int, int*, Dev
 void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool, NullCaps);
 void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t, int);
-void launch_nest_lvl(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
+void launch_nest_lvl(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t, bool);
 void launch_nest_count(const DevChunk*, DevPage*, const int*, int, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_nest_decode(const DevChunk*, DevPage*, const int2*, int, DevChunkResult*, hipStream_t);
 void launch_page_scan(const ScanChunk*, int, pf_page_desc*, ScanCrc*, ScanResult*, hipStream_t);
@@ -301,7 +301,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     if (!(skip & 8u)) launch_lvl(d_chunks, d_pages, d_lvl, int(ctx->l_lvl.size()), d_res, st, ctx->opts.page_null, ncaps);
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
     EVREC(ctx, ctx->ev[6], st);
-    launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, ctx->max_nwin, d_res, st);
+    launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, ctx->max_nwin, d_res, st, ctx->opts.nest_timeout);
     if (!(skip & 16u)) launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_res, d_bajobs, st,
                                        ctx->opts.count_grid);
     launch_nest_count(d_chunks, d_pages, d_nest, n_nest, d_nseg, n_nseg, d_res, st);
@@ -823,6 +823,7 @@ void opts_from_env(pf::PfOpts& o) {
     o.ba_fused = on("PF_BA_FUSED", o.ba_fused);
     o.page_null = on("PF_PAGE_NULL", o.page_null);
     o.null_dict_lds = on("PF_NULL_DICT_LDS", o.null_dict_lds);
+    o.nest_timeout = on("PF_DEBUG_NEST_TIMEOUT", o.nest_timeout);
     o.null_dcap = uint32_t(std::max(0, num("PF_NULL_DCAP", 0))) & ~15u;
     o.null_stagger = num("PF_DEBUG_NULL_STAGGER", o.null_stagger);
     o.flat_split = on("PF_FLAT_SPLIT", o.flat_split);

@@ -187,3 +187,24 @@ def test_nested_leaf_types_in_segments(decoder, oracle, switches, tmp_path, seg)
                 g = got[(rg, c)]
                 assert g["status"] == 0, (rg, c, got["_error"])
                 assert_chunk_equal(g, of.decode(rg, c), f"types rg{rg} c{c} seg={seg}")
+
+
+@pytest.mark.parametrize("v2", [False, True])
+def test_nest_handover_timeout_whole_page(oracle, switches, tmp_path, v2):
+    """A k_nest_lvl hand-over that never comes (a scheduling stall) sends the page to the whole-page
+    path (seg_ok = 2: k_count / k_decode decode it) instead of failing the chunk.
+    PF_DEBUG_NEST_TIMEOUT=1 makes every hand-over time out: the pages with more than one level
+    window take that path, and every chunk is bit-exact vs the oracle."""
+    from pfloor.decoder import GpuDecoder, decode_file
+    from test_dbp_config import _paths
+    path = _nested_file(tmp_path, v2)
+    with switches(PF_DEBUG_NEST_TIMEOUT="1"), GpuDecoder(0) as d:
+        got = decode_file(path, decoder=d)
+        paths = _paths(d)
+    assert any(p[2] == 2 for p in paths), paths
+    with oracle.open(path) as of:
+        for rg in range(of.num_row_groups):
+            for c in range(of.num_columns):
+                g = got[(rg, c)]
+                assert g["status"] == 0, (rg, c, got["_error"])
+                assert_chunk_equal(g, of.decode(rg, c), f"nest timeout rg{rg} c{c} v2={v2}")
