@@ -66,9 +66,9 @@ STAGE_KERNELS = {
     "snappy_exec": r"k_snappy_(exec2|exec5|serial)$",
     "delta": r"k_(dbp_pos|dbp_blk|dbp_scan|delta)$",
     "levels": r"k_(runs|lvl|dlen)$",
-    "count": r"k_(nest_lvl|count|count_flat|count_seg|nest_scan|nest_ids|nest_chars|ba_[a-z]+)$",
+    "count": r"k_(nest_lvl|count|count_flat|count_dict|count_seg|nest_scan|nest_ids|nest_chars|ba_[a-z]+)$",
     "scan": r"k_scan$",
-    "flat": r"k_flat(_all|_fixed|_null)?$",
+    "flat": r"k_flat(_all|_fixed|_null|_fb)?$",
     "decode": r"k_(decode|decode_seg|dba_chars)$",
 }
 STAGE_LABEL = {"snappy_exec": "Snappy executor stage: k_snappy_exec%s (+ redo, serial fallback)" % _EXEC,
@@ -394,7 +394,7 @@ def measure_pmc(args, kernel_re):
         per_launch = []
         with open(files[0]) as f:
             for row in csv.DictReader(f):
-                per_launch.append((int(row.get("Dispatch_Id", 0) or 0), row["Kernel_Name"].split("(")[0].replace("pf::", ""),
+                per_launch.append((int(row.get("Dispatch_Id", 0) or 0), row["Kernel_Name"].split("(")[0].replace("pf::", "").replace("void ", ""),
                                    float(row["Counter_Value"]) * 1024.0))   # KB -> bytes
         res[cnt] = sorted(per_launch)
     shutil.rmtree(out, ignore_errors=True)
@@ -930,9 +930,14 @@ def main():
         wl = (f"wide: {w['rows']} rows x {pf.num_columns} nullable INT32/FLOAT columns, 30% nulls, {args.pool}-value dictionaries, "
               "Snappy, device-resident")
         scaling = "strong"
+    step_frac = round(b_alg_step / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
     out = {
         "metric": METRIC,
         "value": round(value, 3), "unit": "decoded GB/s",
+        # headline efficiency: the whole step's algorithmic HBM bytes / step time /
+        # HBM peak, with the dominant kernel's own fraction beside it (details: pipeline_roofline, roofline)
+        "step_frac": step_frac,
+        "dominant_kernel_frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
         "rows_per_s": round(float(tot[1]) * args.steps / dt, 1),
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "warmup_policy": {"passes_run": warm_passes, "seconds": round(warm_s, 3),
@@ -965,7 +970,7 @@ def main():
                      "stage_ms_overlapped": round(stage_ms.get(dom, 0.0), 4)},
         "pipeline_roofline": {"b_alg_per_step_rank0": b_alg_step, "ms_per_step": round(ms_per_step, 4),
                               "achieved": round(b_alg_step / (ms_per_step * 1e-3) / 1e9, 2),
-                              "frac": round(b_alg_step / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
+                              "frac": step_frac},
     }
     if traffic_detail:
         out["pmc_traffic_per_launch"] = traffic_detail

@@ -1795,18 +1795,95 @@ __global__ __launch_bounds__(128) void k_runs(const DevChunk* __restrict__ chunk
     if (tid == 0) { T[0] = uint32_t(nr); T[1] = s_cov; T[2] = 1u; T[3] = s_allp ? 1u : 0u; }
 }
 
+// Dictionary-string pages k_count_flat takes: flat, levels all present (k_runs: T[3]), a run table.
+__device__ __forceinline__ bool count_dict_page(const DevPage& pg, const DevChunk& ck, const Sections& s) {
+    const uint32_t* T = pg.runtab;
+    return T != nullptr && T[3] == 1u && T[0] <= uint32_t(RUN_CAP) && T[1] >= uint32_t(pg.num_values) && ck.dict_len &&
+           s.val_n > 0 && flat_block_chars(pg) != nullptr;
+}
+constexpr uint64_t BC_BAD = ~0ull;   // a block's chars word when one of its ids is out of the dictionary
+
+// k_count_dict (round 5): the chars of one 4096-entry block of a flat dictionary BYTE_ARRAY page per
+// workgroup -- the block's ids from the page's run table (k_runs), their dictionary lengths summed --
+// into the page's per-block chars word bc[block]; k_count_flat scans those words into the blocks'
+// chars bases and the page's chars. (Round 4 summed a page's blocks one after another in
+// k_count_flat's one workgroup per page: SF1's pages of ~1M entries were 256 dependent rounds.)
+__global__ __launch_bounds__(NT) void k_count_dict(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                   const int2* __restrict__ blocks, DevChunkResult* res) {
+    __shared__ Run R[RUN_CAP];
+    __shared__ uint32_t s_len[DSTR_CAP];   // lengths of small dictionaries
+    __shared__ unsigned long long s_acc;
+    const int2 pb = blocks[blockIdx.x];
+    DevPage& pg = pages[pb.x];
+    const DevChunk& ck = chunks[pg.chunk];
+    const int tid = threadIdx.x;
+    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.ptype != 6 || !is_dict_enc(pg.encoding)) return;
+    Sections s;
+    if (!page_sections(pg, ck, s) || !count_dict_page(pg, ck, s)) return;
+    const uint32_t ne = uint32_t(pg.num_values);
+    const uint32_t b0 = uint32_t(pb.y) * FBLK;
+    if (pb.y > 0 && b0 >= ne) return;
+    const uint32_t b1 = min(ne, b0 + FBLK);
+    const uint32_t* T = pg.runtab;
+    const uint32_t nr = T[0], cov = T[1];
+    for (uint32_t i = tid; i < nr; i += NT) {
+        const uint32_t f = T[4 + 2 * i];
+        const uint32_t nf = i + 1 < nr ? (T[4 + 2 * (i + 1)] & 0x7fffffffu) : cov;
+        Run r;
+        r.first = f & 0x7fffffffu;
+        r.count = nf - r.first;
+        r.data = T[5 + 2 * i];
+        r.packed = f >> 31;
+        R[i] = r;
+    }
+    const bool lstage = ck.dict_n > 0 && ck.dict_n <= int64_t(DSTR_CAP);
+    if (lstage)
+        for (uint32_t i = tid; i < uint32_t(ck.dict_n); i += NT) s_len[i] = gptr(ck.dict_len)[i];
+    if (tid == 0) s_acc = 0;
+    __syncthreads();
+    const uint8_t* ids = s.val + 1;
+    const uint64_t ids_n = s.val_n - 1;
+    const int id_bw = int(s.val[0]);
+    constexpr int EPB = int(FBLK) / NT;   // entries of the block per thread
+    int bad = 0;
+    uint64_t acc = 0;
+    // ids of the thread's EPB entries first (their loads in flight together), then the lengths
+    uint32_t idk[EPB];
+    int r = -1;
+    #pragma unroll
+    for (int k = 0; k < EPB; k++) {
+        const uint32_t e = b0 + uint32_t(k) * NT + uint32_t(tid);
+        idk[k] = 0xffffffffu;
+        if (e >= b1) continue;
+        if (r < 0) r = run_find(R, int(nr), e);
+        while (e >= R[r].first + R[r].count) r++;
+        const Run& Rr = R[r];
+        uint32_t id = Rr.data;
+        if (Rr.packed) {
+            const uint64_t bit = uint64_t(Rr.data) + uint64_t(e - Rr.first) * uint64_t(id_bw);
+            id = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
+                                          : bits_le(ids, ids_n, bit, id_bw);
+        }
+        if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
+        idk[k] = id;
+    }
+    #pragma unroll
+    for (int k = 0; k < EPB; k++)
+        if (idk[k] != 0xffffffffu) acc += lstage ? s_len[idk[k]] : gptr(ck.dict_len)[idk[k]];
+    if (acc) atomicAdd(&s_acc, (unsigned long long)acc);
+    bad = __syncthreads_or(bad);
+    if (tid == 0) flat_block_chars(pg)[pb.y] = bad ? BC_BAD : uint64_t(s_acc);
+}
+
 // k_count for flat BYTE_ARRAY pages whose levels are all present: slots = rows = values =
-// entries; dictionary strings sum their chars over the run table (k_runs) FBLK entries at a time,
-// which also gives k_flat's per-block chars bases; PLAIN pages hand their value chain to the k_ba
-// walk. Every thread's loads are independent (no run-header walk). Marks the page counted
+// entries; dictionary strings scan k_count_dict's per-block chars (k_flat's per-block chars bases,
+// the page's chars); PLAIN pages hand their value chain to the k_ba walk. Marks the page counted
 // (pg.counted) so k_count skips it; pages it leaves alone (nulls, corrupt) go through k_count.
 __global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ chunks, DevPage* pages,
                                                    const int* __restrict__ page_list, DevChunkResult* res,
                                                    BaJob* bajobs) {
-    __shared__ Run R[RUN_CAP];
-    __shared__ uint32_t s_len[DSTR_CAP];   // lengths of small dictionaries
     __shared__ int s_ok;
-    __shared__ unsigned long long s_acc;
+    __shared__ unsigned long long s_scan[NT / 64];
     const int pi = page_list[blockIdx.x];
     DevPage& pg = pages[pi];
     const DevChunk& ck = chunks[pg.chunk];
@@ -1819,62 +1896,19 @@ __global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ 
     const uint32_t* T = pg.runtab;
     uint64_t total = 0;
     if (dict) {
-        if (!(T != nullptr && T[3] == 1u && T[0] <= uint32_t(RUN_CAP) && T[1] >= ne) || !ck.dict_len || s.val_n == 0)
-            return;
-        const uint32_t nr = T[0], cov = T[1];
-        for (uint32_t i = tid; i < nr; i += NT) {
-            const uint32_t f = T[4 + 2 * i];
-            const uint32_t nf = i + 1 < nr ? (T[4 + 2 * (i + 1)] & 0x7fffffffu) : cov;
-            Run r;
-            r.first = f & 0x7fffffffu;
-            r.count = nf - r.first;
-            r.data = T[5 + 2 * i];
-            r.packed = f >> 31;
-            R[i] = r;
-        }
-        const uint8_t* ids = s.val + 1;
-        const uint64_t ids_n = s.val_n - 1;
-        const int id_bw = int(s.val[0]);
+        if (!count_dict_page(pg, ck, s)) return;
+        // k_count_dict's block sums -> exclusive bases in place (a page of 1M entries: 256 words)
         uint64_t* bc = flat_block_chars(pg);
+        const uint32_t nb = (ne + FBLK - 1) / FBLK;
         int bad = 0;
-        const bool lstage = ck.dict_n > 0 && ck.dict_n <= int64_t(DSTR_CAP);
-        if (lstage)
-            for (uint32_t i = tid; i < uint32_t(ck.dict_n); i += NT) s_len[i] = gptr(ck.dict_len)[i];
-        __syncthreads();
-        constexpr int EPB = int(FBLK) / NT;   // entries of a block per thread
-        for (uint32_t b0 = 0; b0 < ne; b0 += FBLK) {
-            const uint32_t b1 = min(ne, b0 + FBLK);
-            if (tid == 0) s_acc = 0;
-            __syncthreads();
-            uint64_t acc = 0;
-            // ids of the thread's EPB entries first (their loads in flight together), then the lengths
-            uint32_t idk[EPB];
-            int r = -1;
-            #pragma unroll
-            for (int k = 0; k < EPB; k++) {
-                const uint32_t e = b0 + uint32_t(k) * NT + uint32_t(tid);
-                idk[k] = 0xffffffffu;
-                if (e >= b1) continue;
-                if (r < 0) r = run_find(R, int(nr), e);
-                while (e >= R[r].first + R[r].count) r++;
-                const Run& Rr = R[r];
-                uint32_t id = Rr.data;
-                if (Rr.packed) {
-                    const uint64_t bit = uint64_t(Rr.data) + uint64_t(e - Rr.first) * uint64_t(id_bw);
-                    id = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
-                                                  : bits_le(ids, ids_n, bit, id_bw);
-                }
-                if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
-                idk[k] = id;
-            }
-            #pragma unroll
-            for (int k = 0; k < EPB; k++)
-                if (idk[k] != 0xffffffffu) acc += lstage ? s_len[idk[k]] : gptr(ck.dict_len)[idk[k]];
-            atomicAdd(&s_acc, (unsigned long long)acc);
-            __syncthreads();
-            if (tid == 0 && bc) bc[b0 / FBLK] = total;
-            total += s_acc;
-            __syncthreads();
+        for (uint32_t b = 0; b < nb; b += NT) {
+            const uint32_t i = b + uint32_t(tid);
+            uint64_t v = i < nb ? bc[i] : 0ull;
+            if (v == BC_BAD) { bad = 1; v = 0; }
+            uint64_t tot;
+            const uint64_t ex = block_excl_scan64<NT>(v, s_scan, tot);
+            if (i < nb) bc[i] = total + ex;
+            total += tot;
         }
         if (__syncthreads_or(bad)) return;   // k_count reports the bad id
     } else {
@@ -4370,9 +4404,11 @@ void launch_nest_decode(const DevChunk* d_chunks, DevPage* d_pages, const int2* 
                         hipStream_t st) {
     if (n_segs > 0) hipLaunchKernelGGL(k_decode_seg, dim3(n_segs), dim3(NT), 0, st, d_chunks, d_pages, d_segs, d_res);
 }
-void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
-                  BaJob* d_bajobs, hipStream_t st, int idle_grid) {
+void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, const int2* d_dblk, int n_dblk,
+                  DevChunkResult* d_res, BaJob* d_bajobs, hipStream_t st, int idle_grid) {
+    // d_dblk: (page, block) pairs of the flat dictionary BYTE_ARRAY pages (k_count_dict, before k_count_flat)
     if (n <= 0) return;
+    if (n_dblk > 0) hipLaunchKernelGGL(k_count_dict, dim3(n_dblk), dim3(NT), 0, st, d_chunks, d_pages, d_dblk, d_res);
     hipLaunchKernelGGL(k_count_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res, d_bajobs);
     hipLaunchKernelGGL(k_count, dim3(std::min(n, idle_grid)), dim3(NT), 0, st, d_chunks, d_pages, d_list, n, d_res, d_bajobs);
 }

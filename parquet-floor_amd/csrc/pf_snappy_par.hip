@@ -845,7 +845,11 @@ __device__ void repair_window(const SnappyJob* __restrict__ jobs, const int2 jw,
     const uint64_t n = job.src_len;
     const uint64_t wend = min(uint64_t(W0) + SNAP_WIN, n);
     const uint64_t stop = sw.flags == WM_FULL ? wend : uint64_t(sw.exit);
-    const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
+    // WM_MERGE reads the window only up to its merge point's lane region (+ a token's bytes and the
+    // parse's 64-position lookahead): usually the first 256 bytes, not the whole 8 KiB (round 5)
+    const uint32_t need = sw.flags == WM_FULL ? SNAP_WSTAGE
+                                              : min(SNAP_WSTAGE, ((sw.exit - W0) / SNAP_RB + 1) * SNAP_RB + 128u);
+    const uint32_t woff = snap_stage(stage, job.src, n, W0, need, lane);
     reinterpret_cast<uint4*>(sbits)[lane] = make_uint4(0, 0, 0, 0);
     slo[lane] = 0;
     __syncthreads();

@@ -11,7 +11,7 @@ disp = collections.defaultdict(set)
 for d in sys.argv[1:]:
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("pf::", "")
+            k = r["Kernel_Name"].split("(")[0].replace("pf::", "").replace("void ", "")
             acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[(k, r["Counter_Name"])].add((f, r["Dispatch_Id"]))
 for k, c in sorted(acc.items()):

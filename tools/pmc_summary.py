@@ -13,7 +13,7 @@ seen = collections.Counter()
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     with open(f"{d}/{c}/run_counter_collection.csv") as f:
         for r in csv.DictReader(f):
-            name = r["Kernel_Name"].split("(")[0].replace("pf::", "")
+            name = r["Kernel_Name"].split("(")[0].replace("pf::", "").replace("void ", "")
             if name == "k_snappy_exec":   # launched twice per step: pieces, then the whole-page redo
                 seen[c] += 1
                 if seen[c] % 2 == 0:

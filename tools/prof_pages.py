@@ -11,7 +11,7 @@ pages = [ln.split() for ln in open(probe_list) if ln.startswith("PAGE ")]
 per = collections.defaultdict(list)
 with open(trace) as f:
     for r in csv.DictReader(f):
-        name = r["Kernel_Name"].split("(")[0].replace("pf::", "")
+        name = r["Kernel_Name"].split("(")[0].replace("pf::", "").replace("void ", "")
         if name.startswith("k_snappy"):
             per[name].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 agg = collections.defaultdict(lambda: collections.defaultdict(list))

@@ -7,7 +7,7 @@ import sys
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
 for r in csv.DictReader(open(sys.argv[1])):
-    k = r["Kernel_Name"].split("(")[0].replace("pf::", "")
+    k = r["Kernel_Name"].split("(")[0].replace("pf::", "").replace("void ", "")
     acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
     disp[k].add(r["Dispatch_Id"])
 for k, c in sorted(acc.items()):

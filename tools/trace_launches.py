@@ -11,7 +11,7 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Time
 passes = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 per = collections.defaultdict(list)
 for r in rows:
-    n = r["Kernel_Name"].split("(")[0].replace("pf::", "")
+    n = r["Kernel_Name"].split("(")[0].replace("pf::", "").replace("void ", "")
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     if n.startswith("k_snappy_exec") and d < 100:
         n += "_redo"
