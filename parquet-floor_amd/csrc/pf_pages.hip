@@ -2280,7 +2280,7 @@ struct FixedLds {
 };
 
 template <class Lds>
-__device__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg, const Sections& s, bool dict,
+__device__ __forceinline__ int flat_present_fixed(Lds& S, const DevChunk& ck, const DevPage& pg, const Sections& s, bool dict,
                                   bool boolean, int enc, int w, const uint8_t* ids, uint64_t ids_n, int id_bw,
                                   uint64_t slot_base, uint32_t e_begin, uint32_t e_end, bool direct = false) {
     const int tid = threadIdx.x;
@@ -2550,10 +2550,24 @@ __device__ __forceinline__ bool flat_fixed_block(FixedLds& S, const DevChunk* __
     return true;
 }
 
-__global__ __launch_bounds__(NT, 4) void k_flat_fixed(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                                   const int2* __restrict__ blocks, DevChunkResult* res) {
+// Fallback queue (device, zeroed with the batch metadata): word 0 counts the (page, block) pairs that
+// start at word 4; k_flat_null and k_flat_fixed append the blocks they do not take, k_flat_fb decodes them.
+__device__ __forceinline__ void null_fallback(int* fbq, int2 pbk) {
+    if (threadIdx.x == 0) reinterpret_cast<int2*>(fbq + 4)[atomicAdd(fbq, 1)] = pbk;
+}
+
+// k_flat_fixed (round 5): the blocks of flat fixed-width pages, in a list of their own. Its register
+// budget is the fixed-width body's (73 VGPRs, 21 KiB LDS: six workgroups per CU, against four of
+// k_flat_all's 127-VGPR union of both bodies); blocks it does not take (a page with nulls that
+// k_flat_null did not take, levels that are not RLE, ...) go to the fallback queue for k_flat_fb.
+#ifndef PF_FIXED_OCC
+#define PF_FIXED_OCC 6
+#endif
+__global__ __launch_bounds__(NT, PF_FIXED_OCC) void k_flat_fixed(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                              const int2* __restrict__ blocks, DevChunkResult* res, int* fbq) {
     __shared__ FixedLds S;
-    flat_fixed_block(S, chunks, pages, blocks[blockIdx.x], res);
+    const int2 pbk = blocks[blockIdx.x];
+    if (!flat_fixed_block(S, chunks, pages, pbk, res)) null_fallback(fbq, pbk);
 }
 
 // One workgroup per (page, FBLK block of entries). Pages whose levels are all present (max_def
@@ -2874,11 +2888,6 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
     }
 }
 
-__global__ __launch_bounds__(NT) void k_flat(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                             const int2* __restrict__ blocks, DevChunkResult* res) {
-    __shared__ FlatLds S;
-    flat_block(S, chunks, pages, blocks[blockIdx.x], res);
-}
 
 // k_flat_fixed and k_flat in one launch over the same (page, block) list: a block decodes its page
 // with the fixed-width body when that applies, else with the general body. One stage instead of
@@ -3339,11 +3348,6 @@ __device__ __forceinline__ int rl_find(const uint2* runs, int nr, uint32_t i) { 
 // fitting one, <= NULL_DICT_LDS; 0 when it has none), gathered from LDS (north_star K3: "dictionary
 // staged in LDS when it fits"); larger ones are gathered from L2 / HBM. Config 4 (1-bit levels,
 // 17-bit ids): ~16.6 KiB a workgroup, eight resident per CU (the VGPR limit) instead of five.
-// Fallback queue (device, zeroed with the batch metadata): word 0 counts the (page, block) pairs that
-// start at word 4; k_flat_null appends the blocks of pages it does not take, k_flat_fb decodes them.
-__device__ __forceinline__ void null_fallback(int* fbq, int2 pbk) {
-    if (threadIdx.x == 0) reinterpret_cast<int2*>(fbq + 4)[atomicAdd(fbq, 1)] = pbk;
-}
 
 template <int W> struct WidthType { using type = uint64_t; };
 template <> struct WidthType<4> { using type = uint32_t; };
@@ -4553,25 +4557,24 @@ void launch_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, i
     if (page_null) hipLaunchKernelGGL(k_page_null, dim3(n), dim3(PN_NT), 0, st, d_chunks, d_pages, d_list, d_res);
     hipLaunchKernelGGL(k_lvl, dim3(n), dim3(LT_NT), 0, st, d_chunks, d_pages, d_list, d_res, nc.dcap, nc.icap);
 }
-void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int n4, int n8, int* d_fbq,
-                 DevChunkResult* d_res, hipStream_t st, NullCaps nc, int stagger, bool split) {
-    // d_list: n (page, block) pairs of k_flat_all, then n4 / n8 pairs of nullable 4 / 8-byte pages
-    // (k_flat_null<4> / <8>; they mark their pages DONE_NULL and queue the blocks they do not take in
-    // d_fbq for k_flat_fb). nc: k_flat_null's LDS stages (dictionary: nc.dlds bytes); stagger (diagnostics build,
-    // tests): blocks > 0 of a page wait that many sleep rounds (~3 us each) for block 0
+void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int nfix, int n, int n4, int n8, int* d_fbq,
+                 DevChunkResult* d_res, hipStream_t st, NullCaps nc, int stagger) {
+    // d_list: nfix (page, block) pairs of flat fixed-width pages (k_flat_fixed), then n of every other
+    // flat page (k_flat_all), then n4 / n8 of nullable 4 / 8-byte pages (k_flat_null<4> / <8>; they mark
+    // their pages DONE_NULL). Blocks k_flat_null and k_flat_fixed do not take are queued in d_fbq for
+    // k_flat_fb. nc: k_flat_null's LDS stages (dictionary: nc.dlds bytes); stagger (diagnostics build,
+    // tests): k_flat_null's blocks > 0 of a page wait that many sleep rounds (~3 us each) for block 0
     const int2* blocks = reinterpret_cast<const int2*>(d_list);
     const size_t dyn = size_t(nc.dcap) + 32u + nc.icap + 32u + nc.dlds;
-    if (n4 > 0) hipLaunchKernelGGL(k_flat_null<4>, dim3(n4), dim3(NTN), dyn, st, d_chunks, d_pages, blocks + n, d_res, nc, stagger, d_fbq);
+    if (n4 > 0)
+        hipLaunchKernelGGL(k_flat_null<4>, dim3(n4), dim3(NTN), dyn, st, d_chunks, d_pages, blocks + nfix + n, d_res, nc, stagger, d_fbq);
     if (n8 > 0)
-        hipLaunchKernelGGL(k_flat_null<8>, dim3(n8), dim3(NTN), dyn, st, d_chunks, d_pages, blocks + n + n4, d_res, nc, stagger, d_fbq);
-    if (n4 + n8 > 0) hipLaunchKernelGGL(k_flat_fb, dim3(n4 + n8 < 1024 ? n4 + n8 : 1024), dim3(NT), 0, st, d_chunks, d_pages, d_fbq, d_res);
-    if (n <= 0) return;
-    if (split) {   // A/B: the two kernels in stream order
-        hipLaunchKernelGGL(k_flat_fixed, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
-        hipLaunchKernelGGL(k_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
-    } else {
-        hipLaunchKernelGGL(k_flat_all, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res);
-    }
+        hipLaunchKernelGGL(k_flat_null<8>, dim3(n8), dim3(NTN), dyn, st, d_chunks, d_pages, blocks + nfix + n + n4, d_res, nc, stagger,
+                           d_fbq);
+    if (nfix > 0) hipLaunchKernelGGL(k_flat_fixed, dim3(nfix), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res, d_fbq);
+    if (n > 0) hipLaunchKernelGGL(k_flat_all, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks + nfix, d_res);
+    const int nq = nfix + n4 + n8;
+    if (nq > 0) hipLaunchKernelGGL(k_flat_fb, dim3(nq < 1024 ? nq : 1024), dim3(NT), 0, st, d_chunks, d_pages, d_fbq, d_res);
 }
 void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int n_first,
                    DevChunkResult* d_res, hipStream_t st, int idle_grid) {

@@ -37,7 +37,7 @@ void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hi
 void launch_dba_chars(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_count(const DevChunk*, DevPage*, const int*, int, const int2*, int, DevChunkResult*, BaJob*, hipStream_t, int);
 void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
-void launch_flat(const DevChunk*, DevPage*, const int*, int, int, int, int*, DevChunkResult*, hipStream_t, NullCaps, int, bool);
+void launch_flat(const DevChunk*, DevPage*, const int*, int, int, int, int, int*, DevChunkResult*, hipStream_t, NullCaps, int);
 void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool, NullCaps);
 void launch_runs(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_decode(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t, int);
@@ -183,7 +183,8 @@ struct pf_ctx {
     std::vector<pf_column_info> info;
     size_t bits_bytes = 0;
     int n_decode_first = 0;                // l_decode: pages that will need k_decode come first
-    int n_flat_all = 0, n_null4 = 0, n_null8 = 0;   // l_flat: (page, block) pairs of k_flat_all, k_flat_null<4>, <8>
+    int n_flat_fixed = 0, n_flat_all = 0, n_null4 = 0, n_null8 = 0;   // l_flat: (page, block) pairs of k_flat_fixed,
+                                                                     // k_flat_all, k_flat_null<4>, <8>
     size_t off_npub = 0, npub_bytes = 0;   // k_nest_lvl / k_dbp_pos window hand-overs (scratch), zeroed before the batch
     int max_nwin = 0, max_dbp_nwin = 0;
     size_t out_bytes = 0;                  // values / offsets / levels arena extent of the last decode
@@ -315,8 +316,8 @@ int enqueue_kernels(pf_ctx* ctx) {
                 ctx->d_chars.cap, used, st);
     EVREC(ctx, ctx->ev[8], st);
     if (!(skip & 32u))
-        launch_flat(d_chunks, d_pages, d_flat, ctx->n_flat_all, ctx->n_null4, ctx->n_null8, reinterpret_cast<int*>(meta + ctx->off_nfbq),
-                    d_res, st, ncaps, ctx->opts.null_stagger, ctx->opts.flat_split);
+        launch_flat(d_chunks, d_pages, d_flat, ctx->n_flat_fixed, ctx->n_flat_all, ctx->n_null4, ctx->n_null8,
+                    reinterpret_cast<int*>(meta + ctx->off_nfbq), d_res, st, ncaps, ctx->opts.null_stagger);
     EVREC(ctx, ctx->ev[9], st);
     if (!(skip & 64u)) launch_decode(d_chunks, d_pages, d_decode, int(ctx->l_decode.size()), ctx->n_decode_first, d_res, st,
                                        ctx->opts.decode_grid);
@@ -828,7 +829,6 @@ void opts_from_env(pf::PfOpts& o) {
     o.nest_timeout = on("PF_DEBUG_NEST_TIMEOUT", o.nest_timeout);
     o.null_dcap = uint32_t(std::max(0, num("PF_NULL_DCAP", 0))) & ~15u;
     o.null_stagger = num("PF_DEBUG_NULL_STAGGER", o.null_stagger);
-    o.flat_split = on("PF_FLAT_SPLIT", o.flat_split);
     o.piece_order = on("PF_PIECE_ORDER", o.piece_order);
     if (const char* e = std::getenv("PF_DEBUG_SKIP")) {
         const char* names[] = {"parse", "exec", "ba", "levels", "count", "flat", "decode"};
@@ -1335,11 +1335,12 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     // gathered through one XCD's L2 instead of all eight (config 4: 400 KB dictionaries); such chunks
     // go to the least loaded label, all other blocks then fill the labels evenly. Labels are
     // interleaved into the grid; short ones are padded with (-1, 0).
-    // Three such grids, one after the other in l_flat: k_flat_all's, then the blocks of nullable 4- and
-    // 8-byte pages (k_flat_null<4> / <8>, which queue what they do not take for k_flat_fb).
+    // Four such grids, one after the other in l_flat: fixed-width pages (k_flat_fixed), the other flat
+    // pages (k_flat_all), then the blocks of nullable 4- and 8-byte pages (k_flat_null<4> / <8>);
+    // k_flat_fixed and k_flat_null queue what they do not take for k_flat_fb.
     constexpr uint32_t STICKY_DICT = 64u << 10;
-    std::vector<int> spread[3];
-    std::vector<std::vector<int>> sticky[3];
+    std::vector<int> spread[4];
+    std::vector<std::vector<int>> sticky[4];
     for (auto& v : sticky) v.resize(static_cast<size_t>(n_chunks));
     std::vector<int> decode_first;
     for (size_t i = 0; i < ctx->pages.size(); i++) {
@@ -1364,7 +1365,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             const bool dict_enc = pg.encoding == PF_ENC_PLAIN_DICTIONARY || pg.encoding == PF_ENC_RLE_DICTIONARY;
             const bool big_dict = ck.dict_page >= 0 && ctx->pages[size_t(ck.dict_page)].body_len > STICKY_DICT && dict_enc;
             const int grid = (pg.lvltab != nullptr && ck.ptype != PF_BYTE_ARRAY && (dict_enc || pg.encoding == PF_ENC_PLAIN))
-                                 ? (ck.width == 4 ? 1 : (ck.width == 8 ? 2 : 0)) : 0;
+                                 ? (ck.width == 4 ? 2 : (ck.width == 8 ? 3 : 1))
+                                 : (ck.ptype != PF_BYTE_ARRAY ? 0 : 1);
             std::vector<int>& q = big_dict ? sticky[grid][size_t(pg.chunk)] : spread[grid];
             for (int b = 0; b < nb; b++) { q.push_back(int(i)); q.push_back(b | (sh << 28)); }
         }
@@ -1379,8 +1381,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     }
     ctx->n_decode_first = int(decode_first.size());
     ctx->l_decode.insert(ctx->l_decode.begin(), decode_first.begin(), decode_first.end());
-    int n_grid[3] = {};
-    for (int gi = 0; gi < 3; gi++) {
+    int n_grid[4] = {};
+    for (int gi = 0; gi < 4; gi++) {
         std::vector<int> xq[8];
         size_t load[8] = {};
         std::vector<int> order(static_cast<size_t>(n_chunks));
@@ -1409,9 +1411,10 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             }
         n_grid[gi] = int(8 * longest);
     }
-    ctx->n_flat_all = n_grid[0];
-    ctx->n_null4 = n_grid[1];
-    ctx->n_null8 = n_grid[2];
+    ctx->n_flat_fixed = n_grid[0];
+    ctx->n_flat_all = n_grid[1];
+    ctx->n_null4 = n_grid[2];
+    ctx->n_null8 = n_grid[3];
     mark();
     // k_snappy_litcopy candidates (k_snappy_head decides): dictionary pages, and data pages that did
     // not compress (a stream of literals only; one literal is read in place instead)
@@ -1444,7 +1447,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_wins = take(m, sizeof(int2) * ctx->wins.size());
     ctx->off_bajobs = take(m, sizeof(BaJob) * ctx->bajobs.size());
     ctx->off_batiles = take(m, sizeof(int2) * ctx->ba_tiles.size());
-    ctx->off_nfbq = take(m, 16 + sizeof(int2) * size_t(ctx->n_null4 + ctx->n_null8), 16);   // k_flat_null's fallback queue
+    ctx->off_nfbq = take(m, 16 + sizeof(int2) * size_t(ctx->n_flat_fixed + ctx->n_null4 + ctx->n_null8), 16);   // fallback queue
     m = take(m, 256) + 256;   // arena counter lives in the last 256 bytes
     ctx->meta_bytes = m;
     HIPCHK(ctx, ctx->d_meta.ensure(m));
