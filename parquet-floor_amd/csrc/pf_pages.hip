@@ -2908,9 +2908,9 @@ __global__ __launch_bounds__(NT, PF_FLAT_OCC) void k_flat_all(const DevChunk* __
     flat_block(S.g, chunks, pages, pbk, res);
 }
 
-// k_flat_fb: the blocks k_flat_null did not take (its fallback queue, filled earlier in stream order),
-// grid-stride over a small grid (the queue is nearly always empty: the page had no block table, or
-// k_page_null took it). Same bodies as k_flat_all.
+// k_flat_fb: the blocks k_flat_null and k_flat_fixed did not take (the fallback queue, filled earlier
+// in stream order), grid-stride over 32 workgroups (the queue is nearly always empty: a page with no
+// block table, one k_page_null took, levels that are not RLE). Same bodies as k_flat_all.
 __global__ __launch_bounds__(NT, PF_FLAT_OCC) void k_flat_fb(const DevChunk* __restrict__ chunks, DevPage* pages,
                                                 const int* __restrict__ fbq, DevChunkResult* res) {
     __shared__ union FlatAllLds {
@@ -4574,7 +4574,9 @@ void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
     if (nfix > 0) hipLaunchKernelGGL(k_flat_fixed, dim3(nfix), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res, d_fbq);
     if (n > 0) hipLaunchKernelGGL(k_flat_all, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks + nfix, d_res);
     const int nq = nfix + n4 + n8;
-    if (nq > 0) hipLaunchKernelGGL(k_flat_fb, dim3(nq < 1024 ? nq : 1024), dim3(NT), 0, st, d_chunks, d_pages, d_fbq, d_res);
+    // (the queue is nearly always empty, and each of k_flat_fb's workgroups needs a CU with room for
+    // k_flat_all-sized workgroups: a grid of min(nq, 1024) waited ~0.1 ms a launch under load on SF1)
+    if (nq > 0) hipLaunchKernelGGL(k_flat_fb, dim3(nq < 32 ? nq : 32), dim3(NT), 0, st, d_chunks, d_pages, d_fbq, d_res);
 }
 void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int n_first,
                    DevChunkResult* d_res, hipStream_t st, int idle_grid) {
