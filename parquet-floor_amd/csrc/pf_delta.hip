@@ -286,16 +286,7 @@ __global__ __launch_bounds__(DP_NT) void k_dbp_pos(const DevChunk* __restrict__ 
         uint64_t tp = H.pos0, tb = 0;
         uint32_t tst = 0;
         bool ok = true;
-        if (w > 0) {
-            const WinPub& pv = pub[w - 1];
-            uint32_t spins = 0;
-            while (__hip_atomic_load(&pv.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 && ++spins < (1u << 22))
-                __builtin_amdgcn_s_sleep(2);
-            ok = spins < (1u << 22);
-            tp = __hip_atomic_load(&pv.p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            tb = __hip_atomic_load(&pv.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            tst = __hip_atomic_load(&pv.st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (w > 0) ok = winpub_get(pub[w - 1], 1u << 22, tp, tb, tst);   // (bounded: no hang on a stall)
         s_hand[0] = tp; s_hand[1] = tb; s_hand[2] = uint64_t(tst) | (ok ? 0u : 2u);
         uint64_t xp = tp, xb = tb;
         uint32_t xst = tst;
@@ -316,11 +307,7 @@ __global__ __launch_bounds__(DP_NT) void k_dbp_pos(const DevChunk* __restrict__ 
             }
         }
         if (!ok) dbp_fail(pg);
-        WinPub& me = pub[w];
-        __hip_atomic_store(&me.p, xp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&me.e, xb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&me.st, xst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&me.flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        winpub_put(pub[w], xp, xb, xst);
     }
     __syncthreads();
     if (s_hand[2] & 2u) return;

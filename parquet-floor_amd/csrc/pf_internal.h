@@ -146,15 +146,35 @@ struct DevPage {
     uint32_t dbp_pad;
 };
 
-// k_nest_lvl: a window's hand-over to the next window of its stream: the position of the first run
-// header at or past the window's end, the entries before it, and whether the chain ended (st = 1).
+// k_nest_lvl / k_dbp_pos: a window's hand-over to the next window of its stream -- the position of
+// the first run header (block header) at or past the window's end, the entries (blocks) before it,
+// whether the chain ended (st = 1) -- packed in one 64-bit word (0 until published) that is stored and
+// polled with relaxed agent-scope atomics (round 5: three stores and a release flag made every
+// hand-over write back the XCD's L2 and every acquire invalidate the reader's).
 struct WinPub {
-    uint32_t flag;            // 0 until published
-    uint32_t st;
-    uint64_t p;
-    uint64_t e;
-    uint64_t pad;
+    uint64_t w;
 };
+#ifdef __HIPCC__
+__device__ __forceinline__ void winpub_put(WinPub& me, uint64_t p, uint64_t e, uint32_t st) {
+    // st + 1 in the low two bits (never 0); a position or count past 31 bits publishes 3 (overflow)
+    const bool ovf = p > 0x7fffffffull || e > 0x7fffffffull || st > 1u;
+    const uint64_t w = (uint64_t(p & 0x7fffffffu) << 33) | (uint64_t(e & 0x7fffffffu) << 2) | uint64_t(ovf ? 3u : st + 1u);
+    __hip_atomic_store(&me.w, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Waits up to spin_cap polls; false: no hand-over came (or it overflowed), the caller gives the page up.
+__device__ __forceinline__ bool winpub_get(const WinPub& pv, uint32_t spin_cap, uint64_t& p, uint64_t& e, uint32_t& st) {
+    if (spin_cap == 0) return false;   // (diagnostics: every hand-over times out)
+    uint64_t w;
+    uint32_t spins = 0;
+    while ((w = __hip_atomic_load(&pv.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0 && ++spins < spin_cap)
+        __builtin_amdgcn_s_sleep(2);
+    if (w == 0 || (w & 3u) == 3u) return false;
+    p = w >> 33;
+    e = (w >> 2) & 0x7fffffffull;
+    st = uint32_t(w & 3u) - 1u;
+    return true;
+}
+#endif
 #ifndef PF_NEST_WIN
 #define PF_NEST_WIN 2048
 #endif

@@ -4120,19 +4120,10 @@ __global__ __launch_bounds__(NL_NT) void k_nest_lvl(const DevChunk* __restrict__
         uint64_t tp = 0, te = 0;
         uint32_t tst = 0;
         bool ok = true;
-        if (w > 0) {
-            const WinPub& pv = pub[w - 1];
-            // bounded (spin_cap: 2^22; the diagnostics option nest_timeout makes it 0, so every hand-over
-            // "times out"): a hand-over that never comes sends the page to the whole-page path (below)
-            // instead of hanging
-            uint32_t spins = 0;
-            while (__hip_atomic_load(&pv.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 && ++spins < spin_cap)
-                __builtin_amdgcn_s_sleep(2);
-            ok = spins < spin_cap;
-            tp = __hip_atomic_load(&pv.p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            te = __hip_atomic_load(&pv.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            tst = __hip_atomic_load(&pv.st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        // bounded (spin_cap: 2^22; the diagnostics option nest_timeout makes it 0, so every hand-over
+        // "times out"): a hand-over that never comes sends the page to the whole-page path (below)
+        // instead of hanging
+        if (w > 0) ok = winpub_get(pub[w - 1], spin_cap, tp, te, tst);
         s_hand[0] = tp; s_hand[1] = te; s_hand[2] = uint64_t(tst) | (ok ? 0u : 2u);
         uint64_t xp = tp, xe = te;
         uint32_t xst = tst;
@@ -4153,14 +4144,10 @@ __global__ __launch_bounds__(NL_NT) void k_nest_lvl(const DevChunk* __restrict__
                 else xp = w0 + e;
             }
         }
-        WinPub& me = pub[w];
         // a hand-over that never came (a scheduling stall, not the data): the page leaves the segment
         // path and k_count / k_decode decode it whole, as k_dbp_pos does with dbp_ok = 2
         if (!ok) __hip_atomic_fetch_max(&pg.seg_ok, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&me.p, xp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&me.e, xe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&me.st, xst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&me.flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        winpub_put(pub[w], xp, xe, xst);
     }
     __syncthreads();
     if (s_hand[2] & 2u) return;
