@@ -11,7 +11,7 @@ from pfloor import _native, datagen  # noqa: E402
 from pfloor.decoder import ParquetFile, decode_file  # noqa: E402
 
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1048576
-path = f"/tmp/probe_lineitem_{rows}.parquet"
+path = os.path.join(ROOT, "gpurun_out", f"probe_lineitem_{rows}.parquet")
 if not os.path.exists(path):
     pq.write_table(datagen.lineitem_table(rows, seed=42), path, compression="snappy", row_group_size=1 << 20)
 L = _native.lib()
@@ -20,7 +20,7 @@ f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
 buf = (C.c_ulonglong * 16)()
 with ParquetFile(path) as pf:
     names = [c.path[0] for c in pf.columns]
-for col in ("l_comment", "l_shipmode", "l_orderkey", "l_shipdate"):
+for col in (sys.argv[2].split(",") if len(sys.argv) > 2 else ("l_comment", "l_shipmode", "l_orderkey", "l_shipdate")):
     c = names.index(col)
     decode_file(path, row_groups=[0], columns=[c])
     f(buf, 16, 1)
