@@ -369,3 +369,43 @@ def test_reader_multi_device_error_at_its_row_group(tmp_path):
             for _ in s:
                 got += 1
     assert got == rows01
+
+
+@pytest.mark.parametrize("kind", ["string", "int64"])
+def test_dictionary_ids_out_of_range(decoder, oracle, tmp_path, kind):
+    """Ids past the dictionary in a flat dictionary data page (0xff bytes written over an uncompressed v2
+    page's bit-packed ids, 10-bit ids into 700 entries): the oracle reports the chunk; the GPU must too,
+    from whichever kernel sees it first (strings: k_count_dict marks its block and k_count reports the
+    page, round 5; fixed width: k_flat_fixed's id check), without a fault; a clean column of the same
+    batch stays bit-exact."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from pfloor.decoder import ParquetFile, decode_file
+    rng = np.random.default_rng(29)
+    n = 60_000
+    vocab = np.array([f"v{i:04d}" * (1 + i % 3) for i in range(700)]) if kind == "string" else \
+        (np.arange(700, dtype=np.int64) * 7919)
+    t = pa.table({"d": pa.array(vocab[rng.integers(0, 700, n)]), "k": pa.array(np.arange(n, dtype=np.int64))})
+    path = str(tmp_path / f"badids_{kind}.parquet")
+    pq.write_table(t, path, compression="NONE", data_page_version="2.0", use_dictionary=["d"], row_group_size=n)
+    data = bytearray(open(path, "rb").read())
+    with ParquetFile(path) as pf:   # (the page descriptors live in the handle: read them inside)
+        start, _ = pf.chunk_range(0, 0)
+        d = pf.chunk_desc(0, 0, 0)
+        dp = [(d.pages[i].offset, d.pages[i].rep_bytes, d.pages[i].def_bytes) for i in range(d.n_pages)
+              if d.pages[i].page_type in (0, 3)]
+    assert dp
+    off, rep_b, def_b = dp[0]
+    vals = start + off + rep_b + def_b   # v2: [rep][def][values]; values: the bit width, then the runs
+    assert data[vals] == 10, data[vals]
+    for i in range(vals + 40, vals + 120):
+        data[i] = 0xFF
+    bad = tmp_path / f"badids_{kind}_bad.parquet"
+    bad.write_bytes(bytes(data))
+    with oracle.open(str(bad)) as of:
+        assert of.decode(0, 0)["status"] != 0
+        good = of.decode(0, 1)
+    got = decode_file(str(bad), decoder=decoder)
+    assert got[(0, 0)]["status"] != 0, "ids past the dictionary not reported"
+    assert got[(0, 1)]["status"] == 0
+    assert_chunk_equal(got[(0, 1)], good, "clean column next to the damaged one")
