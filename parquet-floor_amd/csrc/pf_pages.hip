@@ -1710,7 +1710,7 @@ __device__ __forceinline__ uint32_t run_value(const Run& r, const uint8_t* p, ui
 // Copy the chars of nv values (value v: coff[v] .. next start, from sbase + csrc[v]) to
 // obase[0 .. total): one 16-byte output chunk per thread step; interior chunks are one 16-byte
 // store, the two edge chunks (shared with neighbouring tiles) byte stores.
-__device__ inline void copy_chars(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
+__device__ __forceinline__ void copy_chars(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
                                   const uint8_t* sbase, uint8_t* obase) {
     if (total == 0 || nv == 0) return;
     const uintptr_t a0 = reinterpret_cast<uintptr_t>(obase);
@@ -1941,7 +1941,7 @@ __global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ 
 // One 16-byte output chunk at arena address c (tile chars start at a0, total bytes): chunks inside
 // one value are one 16-byte source read (aligned dwords + v_alignbyte); a chunk spanning values is
 // blended from one aligned window per value piece. v: a value at or before the chunk's first byte.
-__device__ inline void copy_chunk16(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
+__device__ __forceinline__ void copy_chunk16(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
                                     const uint8_t* sbase, const uint8_t* send, uintptr_t a0, uintptr_t c, uint32_t v) {
     const int64_t r0 = int64_t(c) - int64_t(a0);
     uint32_t vb = coff[v];
@@ -2018,8 +2018,8 @@ __device__ inline void copy_chunk16(const uint32_t* coff, const uint32_t* csrc, 
 // copy_chars with a chunk -> value table (no per-chunk binary search) and 16-byte source reads
 // (aligned dwords + v_alignbyte) for chunks inside one value; other chunks blended per value piece.
 // cv: LDS table of CV_CAP u16; send: end of the readable source buffer.
-constexpr uint32_t CV_CAP = 4096;
-__device__ inline void copy_chars_fast(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
+constexpr uint32_t CV_CAP = 2048;   // (round 5: 4096 -> 2048 brought k_flat_all under 32 KiB of LDS, five workgroups per CU)
+__device__ __forceinline__ void copy_chars_fast(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
                                        const uint8_t* sbase, const uint8_t* send, uint8_t* obase, uint16_t* cv) {
     if (total == 0 || nv == 0) return;
     const uintptr_t a0 = reinterpret_cast<uintptr_t>(obase);
@@ -2054,7 +2054,7 @@ __device__ __forceinline__ uint32_t sp_pick(const uint32_t* Z, int d, uint32_t h
     for (uint32_t k = 1; k <= SP_K; k++) r = h >= k ? Z[d + int(k)] : r;
     return r;
 }
-__device__ inline void copy_chars_plain(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
+__device__ __forceinline__ void copy_chars_plain(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
                                         const uint8_t* sbase, const uint8_t* send, uint8_t* obase, uint16_t* cv) {
     if (total == 0 || nv == 0) return;
     const uintptr_t a0 = reinterpret_cast<uintptr_t>(obase);
@@ -2897,7 +2897,7 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
 // two in stream order (the fixed-width columns' blocks no longer wait for the string blocks or the
 // other way round); the LDS of the two bodies is shared (they never run in one block together).
 #ifndef PF_FLAT_OCC
-#define PF_FLAT_OCC 4
+#define PF_FLAT_OCC 5   // round 5 (with CV_CAP 2048 and the chars copies inlined): SF1 2.74 -> 2.69 ms; 4 before
 #endif
 __global__ __launch_bounds__(NT, PF_FLAT_OCC) void k_flat_all(const DevChunk* __restrict__ chunks, DevPage* pages,
                                                  const int2* __restrict__ blocks, DevChunkResult* res) {
