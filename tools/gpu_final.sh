@@ -20,4 +20,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 f=$(find $OUT/prof -name '*kernel_trace.csv' | head -1)
 python3 $GRAFT_REPO_ROOT/tools/trace_launches.py "$f" 3 > $OUT/launches.txt; head -12 $OUT/launches.txt
 find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
-cd $GRAFT_REPO_ROOT && tools/gpu_pool_sweep.sh ${TAG}_pool
+[ -n "$SKIP_POOL" ] || (cd $GRAFT_REPO_ROOT && tools/gpu_pool_sweep.sh ${TAG}_pool)
