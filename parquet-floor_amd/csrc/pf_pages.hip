@@ -2687,6 +2687,12 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
     }
     uint64_t vidx = e_begin;                                // page-relative index of the next present value
     int err = 0;
+#ifdef PF_STAMPS   // tile sub-phases (tools/probe_flat_all.py): 11 levels, 12 values, 13 scan, 14 offsets, 15 chars
+    unsigned long long fs_ = __builtin_amdgcn_s_memtime();
+#define FSTAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) PSTAMP(i, t_ - fs_); fs_ = t_; } while (0)
+#else
+#define FSTAMP(i) ((void)0)
+#endif
 
 
     for (uint32_t e0 = e_begin, want = 0; e0 < e_end; e0 += want) {
@@ -2745,6 +2751,7 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
                 bad = 1;
         }
         if (__syncthreads_or(bad)) { err = 1; break; }
+        FSTAMP(11);
         // ---- values
         uint32_t lsum = 0;
         uint32_t my_src[FEPT], my_len[FEPT];   // indexed by entry k (static after unrolling)
@@ -2830,10 +2837,12 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
                 }
             }
         }
+        FSTAMP(12);
         uint32_t tchars = 0;
         const uint32_t lo = binary ? block_excl_scan<NT>(lsum, S.scan_tmp, tchars) : 0;
         if (binary && char_base + tchars > uint64_t(pg.char_start + pg.n_chars)) bad = 1;   // k_count disagrees
         if (__syncthreads_or(bad)) { err = 1; break; }
+        FSTAMP(13);
         if (binary) {
             uint32_t c = lo, j = 0;
             #pragma unroll
@@ -2858,7 +2867,7 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
         }
         __syncthreads();
 #ifdef PF_STAMPS
-        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) { PSTAMP(4, t_ - ft1); PSTAMP(3, 1); } ft1 = t_; }
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tid == 0) { PSTAMP(4, t_ - ft1); PSTAMP(3, 1); PSTAMP(14, t_ - fs_); } ft1 = t_; fs_ = t_; }
 #endif
         if (binary) {
             const uint8_t* sb = dict ? ck.dict_data : s.val;
@@ -2867,6 +2876,7 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
             else if (!dict) copy_chars_plain(S.coff, S.csrc, tv, tchars, sb, se, ck.chars + char_base, S.cv);
             else copy_chars_fast(S.coff, S.csrc, tv, tchars, sb, se, ck.chars + char_base, S.cv);
         }
+        FSTAMP(15);
         if (ck.max_def > 0 && ck.validity) flush_bits(S.vbits, slot_base + e0, want, ck.validity);
         vidx += tv;
         char_base += tchars;

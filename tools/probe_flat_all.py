@@ -32,3 +32,8 @@ with GpuDecoder(0) as dec:
         n = max(buf[0], 1)
         print(f"{col:16s} blocks {buf[0]:6d} | cycles per block {buf[1] / n:9.0f} | dict {buf[6]} binary {buf[7]} | "
               f"max binary {buf[8]} max fixed {buf[9]}", "status", got["_status"], flush=True)
+        t = max(buf[3], 1)
+        print(f"{'':16s} general body: prologue {buf[2] / n:9.0f} per block | per tile ({buf[3]} tiles): "
+              f"levels+values+offsets {buf[4] / t:9.0f} chars+validity {buf[5] / t:9.0f}", flush=True)
+        print(f"{'':16s} tile sub-phases: levels {buf[11] / t:7.0f} values {buf[12] / t:7.0f} scan {buf[13] / t:7.0f} "
+              f"offsets {buf[14] / t:7.0f} chars {buf[15] / t:7.0f}", flush=True)
