@@ -1707,51 +1707,6 @@ __device__ __forceinline__ uint32_t run_value(const Run& r, const uint8_t* p, ui
     return r.packed ? bits_le(p, n, uint64_t(r.data) + uint64_t(i - r.first) * uint64_t(bw), bw) : r.data;
 }
 
-// Copy the chars of nv values (value v: coff[v] .. next start, from sbase + csrc[v]) to
-// obase[0 .. total): one 16-byte output chunk per thread step; interior chunks are one 16-byte
-// store, the two edge chunks (shared with neighbouring tiles) byte stores.
-__device__ __forceinline__ void copy_chars(const uint32_t* coff, const uint32_t* csrc, uint32_t nv, uint32_t total,
-                                  const uint8_t* sbase, uint8_t* obase) {
-    if (total == 0 || nv == 0) return;
-    const uintptr_t a0 = reinterpret_cast<uintptr_t>(obase);
-    const uintptr_t aend = a0 + total;
-    for (uintptr_t c = (a0 & ~uintptr_t(15)) + 16u * threadIdx.x; c < aend; c += 16u * blockDim.x) {
-        const int64_t r0 = int64_t(c) - int64_t(a0);
-        const uint32_t first = r0 < 0 ? 0u : uint32_t(r0);
-        int lo = 0, hi = int(nv);
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (coff[mid] <= first) lo = mid; else hi = mid;
-        }
-        uint32_t v = uint32_t(lo);
-        uint32_t vend = v + 1 < nv ? coff[v + 1] : total;
-        const uint8_t* sp = sbase + (int64_t(csrc[v]) - int64_t(coff[v]));
-        uint32_t word[4] = {0, 0, 0, 0};
-        #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int64_t r = r0 + k;
-            if (r >= 0 && r < int64_t(total)) {
-                while (uint32_t(r) >= vend) {
-                    v++;
-                    vend = v + 1 < nv ? coff[v + 1] : total;
-                    sp = sbase + (int64_t(csrc[v]) - int64_t(coff[v]));
-                }
-                word[k >> 2] |= uint32_t(sp[r]) << (8 * (k & 3));
-            }
-        }
-        uint8_t* dst = reinterpret_cast<uint8_t*>(c);
-        if (r0 >= 0 && r0 + 16 <= int64_t(total)) {
-            *reinterpret_cast<uint4*>(dst) = make_uint4(word[0], word[1], word[2], word[3]);
-        } else {
-            #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const int64_t r = r0 + k;
-                if (r >= 0 && r < int64_t(total)) dst[k] = uint8_t(word[k >> 2] >> (8 * (k & 3)));
-            }
-        }
-    }
-}
-
 // One 128-thread workgroup per dictionary data page of a flat chunk: walks the page's
 // dictionary-id run headers ONCE (wave 1) and checks whether every definition level is present
 // (wave 0), so that k_flat's blocks of the page load a ready run table instead of each walking
@@ -2015,7 +1970,7 @@ __device__ __forceinline__ void copy_chunk16(const uint32_t* coff, const uint32_
     }
 }
 
-// copy_chars with a chunk -> value table (no per-chunk binary search) and 16-byte source reads
+// Chars copy with a chunk -> value table (no per-chunk binary search) and 16-byte source reads
 // (aligned dwords + v_alignbyte) for chunks inside one value; other chunks blended per value piece.
 // cv: LDS table of CV_CAP u16; send: end of the readable source buffer.
 constexpr uint32_t CV_CAP = 2048;   // (round 5: 4096 -> 2048 brought k_flat_all under 32 KiB of LDS, five workgroups per CU)
@@ -2025,18 +1980,22 @@ __device__ __forceinline__ void copy_chars_fast(const uint32_t* coff, const uint
     const uintptr_t a0 = reinterpret_cast<uintptr_t>(obase);
     const uintptr_t c0 = a0 & ~uintptr_t(15);
     const uint32_t nch = uint32_t(((a0 + total + 15) & ~uintptr_t(15)) - c0) / 16u;
-    if (nch > CV_CAP) { copy_chars(coff, csrc, nv, total, sbase, obase); return; }
-    // value v owns the chunks whose first byte lies inside it
-    if (threadIdx.x == 0) cv[0] = 0;
-    for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {
-        const uint32_t b = coff[v], e = v + 1 < nv ? coff[v + 1] : total;
-        if (e <= b) continue;
-        const uintptr_t ab = a0 + b, ae = a0 + e;
-        for (uintptr_t c = (ab + 15) & ~uintptr_t(15); c < ae; c += 16) cv[(c - c0) >> 4] = uint16_t(v);
+    // value v owns the chunks whose first byte lies inside it (chunk 0 may start before the tile: 0);
+    // tiles of more than CV_CAP chunks in passes of CV_CAP (round 5: the per-chunk search before)
+    for (uint32_t p0 = 0; p0 < nch; p0 += CV_CAP) {
+        const uintptr_t lo = c0 + uintptr_t(p0) * 16u, hi = c0 + uintptr_t(min(nch, p0 + CV_CAP)) * 16u;
+        if (p0 > 0) __syncthreads();   // the previous pass's table reads are done
+        if (threadIdx.x == 0 && p0 == 0) cv[0] = 0;
+        for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {
+            const uint32_t b = coff[v], e = v + 1 < nv ? coff[v + 1] : total;
+            if (e <= b) continue;
+            const uintptr_t ab = max(a0 + b, lo), ae = min(a0 + e, hi);
+            for (uintptr_t c = (ab + 15) & ~uintptr_t(15); c < ae; c += 16) cv[(c - lo) >> 4] = uint16_t(v);
+        }
+        __syncthreads();
+        for (uint32_t ci = threadIdx.x; ci < uint32_t((hi - lo) >> 4); ci += blockDim.x)
+            copy_chunk16(coff, csrc, nv, total, sbase, send, a0, lo + uintptr_t(ci) * 16u, cv[ci]);
     }
-    __syncthreads();
-    for (uint32_t ci = threadIdx.x; ci < nch; ci += blockDim.x)
-        copy_chunk16(coff, csrc, nv, total, sbase, send, a0, c0 + uintptr_t(ci) * 16u, cv[ci]);
 }
 
 // PLAIN BYTE_ARRAY chars (round 4): the tile's values are consecutive in the page body, each after its
@@ -2060,7 +2019,8 @@ __device__ __forceinline__ void copy_chars_plain(const uint32_t* coff, const uin
     const uintptr_t a0 = reinterpret_cast<uintptr_t>(obase);
     const uintptr_t s0 = a0 & ~uintptr_t(63);
     const uint32_t nsp = uint32_t(((a0 + total + 63) & ~uintptr_t(63)) - s0) / 64u;
-    if (nsp > CV_CAP) { copy_chars(coff, csrc, nv, total, sbase, obase); return; }
+    // more spans than the table holds (values averaging over 64 bytes): the chunk copy, in passes
+    if (nsp > CV_CAP) { copy_chars_fast(coff, csrc, nv, total, sbase, send, obase, cv); return; }
     // value v owns the spans whose first byte lies inside it
     if (threadIdx.x == 0) cv[0] = 0;
     for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {

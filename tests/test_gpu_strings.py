@@ -85,3 +85,27 @@ def test_plain_strings_rare_long(decoder, oracle, tmp_path, version):
         with oracle.open(path) as of:
             for c in cols:
                 assert_chunk_equal(got[(0, c)], of.decode(0, c), f"rare long v{version} col {c} of {cols}")
+
+
+@pytest.mark.parametrize("nulls", [False, True])
+def test_dict_strings_multi_pass_tiles(decoder, oracle, tmp_path, nulls):
+    """Dictionary strings averaging ~40 chars: a 2048-value tile holds ~80 KiB of chars, more
+    16-byte chunks than the chunk -> value table (CV_CAP), so the copy runs in several table passes
+    (round 5; the per-chunk search before). Config 1's 8-24-char vocabulary straddles one pass."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from pfloor.decoder import decode_file
+    rng = np.random.default_rng(29 + nulls)
+    n = 50_000
+    alphabet = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz ,.0123456789", np.uint8)
+    vlens = rng.integers(8, 72, 700)
+    vocab = [alphabet[rng.integers(0, len(alphabet), int(k))].tobytes().decode() for k in vlens]
+    vals = [vocab[i] for i in rng.integers(0, len(vocab), n)]
+    mask = (rng.random(n) < 0.15) if nulls else None
+    t = pa.table({"s": pa.array(vals, type=pa.string(), mask=mask)})
+    path = str(tmp_path / f"dict_long_{nulls}.parquet")
+    pq.write_table(t, path, compression="snappy", use_dictionary=True, row_group_size=n)
+    got = decode_file(path, decoder=decoder)
+    assert got["_status"] == 0, got["_error"]
+    with oracle.open(path) as of:
+        assert_chunk_equal(got[(0, 0)], of.decode(0, 0), f"dict long nulls={nulls}")
