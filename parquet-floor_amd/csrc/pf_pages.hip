@@ -1851,7 +1851,6 @@ __global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ 
     if (!page_sections(pg, ck, s)) return;
     const bool dict = is_dict_enc(pg.encoding);
     const uint32_t ne = uint32_t(pg.num_values);
-    const uint32_t* T = pg.runtab;
     uint64_t total = 0;
     if (dict) {
         if (!count_dict_page(pg, ck, s)) return;
