@@ -101,6 +101,22 @@ __global__ __launch_bounds__(256) void k_copy_words(uint64_t* __restrict__ d0, c
     }
 }
 static_assert(sizeof(DevChunkResult) % 8 == 0 && sizeof(DevChunk) % 8 == 0, "k_copy_words moves 8-byte words");
+// The batch's metadata upload (pinned host words -> device) and the zeroing of its validity arena and
+// window hand-over words in one launch (round 5: two hipMemsetAsync fills were two more dependent
+// launches at the head of every batch's chain). z0 / z1: 8-byte aligned, nz0 / nz1 bytes.
+__global__ __launch_bounds__(256) void k_upload(uint64_t* __restrict__ d, const uint64_t* __restrict__ s, uint32_t n,
+                                                uint8_t* __restrict__ z0, uint32_t nz0, uint8_t* __restrict__ z1, uint32_t nz1) {
+    const uint32_t stride = gridDim.x * 256u;
+    const uint32_t w0 = (nz0 + 7u) / 8u, w1 = (nz1 + 7u) / 8u;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n + w0 + w1; i += stride) {
+        if (i < n) { d[i] = s[i]; continue; }
+        const bool first = i < n + w0;
+        uint8_t* z = first ? z0 : z1;
+        const uint32_t w = first ? i - n : i - n - w0, nz = first ? nz0 : nz1;
+        if (8u * w + 8u <= nz) reinterpret_cast<uint64_t*>(z)[w] = 0;
+        else for (uint32_t b = 8u * w; b < nz; b++) z[b] = 0;
+    }
+}
 inline void copy_words(void* d0, const void* s0, size_t b0, void* d1, const void* s1, size_t b1, hipStream_t st) {
     const uint32_t n0 = uint32_t(b0 / 8), n1 = uint32_t(b1 / 8);
     const uint32_t grid = std::max(1u, std::min(1024u, (n0 + n1 + 255u) / 256u));
@@ -267,9 +283,11 @@ int enqueue_kernels(pf_ctx* ctx) {
 #else
     constexpr unsigned skip = 0;
 #endif
-    if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
-    if (ctx->npub_bytes)
-        HIPCHK(ctx, hipMemsetAsync(static_cast<uint8_t*>(ctx->d_scratch.p) + ctx->off_npub, 0, ctx->npub_bytes, st));
+    if (!(ctx->zc && ctx->h_meta.d)) {   // (the zero-copy upload, k_upload, zeroes them)
+        if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
+        if (ctx->npub_bytes)
+            HIPCHK(ctx, hipMemsetAsync(static_cast<uint8_t*>(ctx->d_scratch.p) + ctx->off_npub, 0, ctx->npub_bytes, st));
+    }
     EVREC(ctx, ctx->ev[1], st);
     // single-literal pages in place, PLAIN fixed-width pages straight into the column (pf_pages.hip)
     if (!(skip & 1u)) launch_snappy_head(d_jobs, int(ctx->jobs.size()), d_pages, d_chunks, d_fallback, d_res, st);
@@ -449,8 +467,15 @@ int upload_meta(pf_ctx* ctx) {
             r[c].num_rows = ck.num_entries;
         }
     }
-    if (ctx->zc && ctx->h_meta.d) copy_words(ctx->d_meta.p, ctx->h_meta.d, ctx->meta_bytes, nullptr, nullptr, 0, ctx->stream);
-    else HIPCHK(ctx, hipMemcpyAsync(ctx->d_meta.p, h, ctx->meta_bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (ctx->zc && ctx->h_meta.d) {   // enqueue_kernels follows at once on the same stream
+        const uint32_t n = uint32_t(ctx->meta_bytes / 8), nz0 = uint32_t(ctx->bits_bytes), nz1 = uint32_t(ctx->npub_bytes);
+        const uint32_t grid = std::max(1u, std::min(1024u, (n + (nz0 + 7u) / 8u + (nz1 + 7u) / 8u + 255u) / 256u));
+        hipLaunchKernelGGL(k_upload, dim3(grid), dim3(256), 0, ctx->stream, static_cast<uint64_t*>(ctx->d_meta.p),
+                           static_cast<const uint64_t*>(ctx->h_meta.d), n, static_cast<uint8_t*>(ctx->d_bits.p), nz0,
+                           static_cast<uint8_t*>(ctx->d_scratch.p) + ctx->off_npub, nz1);
+    } else {
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_meta.p, h, ctx->meta_bytes, hipMemcpyHostToDevice, ctx->stream));
+    }
     return PF_OK;
 }
 
