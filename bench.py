@@ -102,8 +102,10 @@ WORKLOADS = {
     # batch 0: the column split (as sf1): 0.84 vs 0.905 ms with one row group per batch (r04)
     "nested": dict(rows=1_000_000, rg_rows=250_000, seed=5, kind="nested", batch=0),
     # (configs[0]) INT64 / DOUBLE / nullable INT32 / dictionary UTF8, uncompressed
-    # (batch 0: 0.278 vs 0.380 ms with one row group per batch, r04)
-    "flat": dict(rows=1_000_000, rg_rows=250_000, seed=1, kind="flat", batch=0),
+    # (batch 0: 0.278 vs 0.380 ms with one row group per batch, r04). string_weight 4: the string
+    # column gets a stream of its own (its chain: value walk, runs, counts, scan, string gather):
+    # 0.142-0.146 vs 0.181 ms at 1 (r05, gpurun_out/sw; 2: 0.182, 8: 0.204; config 5 is best at 1)
+    "flat": dict(rows=1_000_000, rg_rows=250_000, seed=1, kind="flat", batch=0, string_weight=4.0),
 }
 
 
@@ -699,8 +701,9 @@ def main():
                     help="sf1: give each context all row groups of a column subset (default), the same with "
                          "BYTE_ARRAY and fixed-width columns on separate contexts (kinds), or whole row groups")
     ap.add_argument("--string-ctx", type=int, default=2, help="--split kinds: contexts for the BYTE_ARRAY columns")
-    ap.add_argument("--string-weight", type=float, default=1.0,
-                    help="--split columns: LPT cost multiplier of BYTE_ARRAY chunks (their value walk, chars count and copy)")
+    ap.add_argument("--string-weight", type=float, default=None,
+                    help="--split columns: LPT cost multiplier of BYTE_ARRAY chunks (their value walk, chars count and "
+                         "copy); default: the workload's (flat 4, others 1)")
     ap.add_argument("--lpt-cost", choices=("decompressed", "compressed"), default="compressed",
                     help="sf1 --split columns: the per-chunk cost the column slices are dealt by")
     ap.add_argument("--columns", default=None, help=argparse.SUPPRESS)   # analysis only: comma-separated column subset
@@ -718,6 +721,8 @@ def main():
                     help="timed steps decode -> wait per batch on one context per stream (A/B of the pipelined default)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args, _ = ap.parse_known_args()
+    if args.string_weight is None:
+        args.string_weight = WORKLOADS[args.workload].get("string_weight", 1.0)
     if args.pmc_child:
         return pmc_child(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -950,8 +955,9 @@ def main():
                    "compressed_page_bytes_rank0": st_all["compressed"],
                    "parallelism": f"row groups sharded round-robin over {world} GPU(s) (pfloor.shard, no collective), "
                                   f"{S} decode streams per GPU" +
-                                  (", each stream all row groups of a column subset (LPT on compressed bytes)"
-                                   if args.split == "columns" and args.workload == "sf1" and S > 1 else "")},
+                                  (f", each stream a column subset (column slices dealt LPT on {args.lpt_cost} bytes"
+                                   + (f", BYTE_ARRAY chunks weighted x{args.string_weight:g}" if args.string_weight != 1.0 else "")
+                                   + ")" if args.split == "columns" and S > 1 and wl_batch(args) <= 0 else "")},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "stage_ms_source": "context 0's per-stage HIP events, separate untimed passes (all streams decoding, "
                            "not pipelined); the timed steps run with the events off",
