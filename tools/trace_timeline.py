@@ -14,8 +14,9 @@ for s in ([sid] if sid else streams):
     # a decode starts at the fillBuffer (bits memset) or the first k_snappy_index after a gap
     # decodes start at their metadata upload: k_copy_words launches alternate upload / results
     # download (zero-copy default); older traces: the Snappy index / head kernel
+    up = [i for i, r in enumerate(rs) if "k_upload" in r["Kernel_Name"]]   # r05: the upload kernel
     cw = [i for i, r in enumerate(rs) if "k_copy_words" in r["Kernel_Name"]]
-    starts = cw[0::2] if cw else [i for i, r in enumerate(rs) if "k_snappy_index" in r["Kernel_Name"] or
+    starts = up if up else cw[0::2] if cw else [i for i, r in enumerate(rs) if "k_snappy_index" in r["Kernel_Name"] or
                                   "k_snappy_head" in r["Kernel_Name"]]
     if not starts:
         continue
