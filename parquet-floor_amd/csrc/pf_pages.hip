@@ -2233,12 +2233,13 @@ __global__ __launch_bounds__(64) void k_snappy_head(SnappyJob* __restrict__ jobs
 #endif
 constexpr uint32_t DICT_LDS = PF_DICT_LDS;   // bytes of a fixed-width dictionary staged in LDS (k_flat_fixed)
 struct FixedLds {
-    uint64_t dict[DICT_LDS / 8 + 1];
+    uint64_t dict[DICT_LDS / 8 + 2];   // the dictionary, then the block's id bytes when they fit behind it
     Run vrun[RUN_CAP];
     uint32_t coff[FTX / 64];
     RunWalk vst;
     int nvrun, vres, allp;
     uint32_t vcover, vlo;
+    uint32_t ib[2];                   // the block's id byte range [ib[0], ib[1])
 };
 
 template <class Lds>
@@ -2251,6 +2252,49 @@ __device__ __forceinline__ int flat_present_fixed(Lds& S, const DevChunk& ck, co
     // dictionary gather from LDS when the whole dictionary fits (north_star: K3 LDS / global)
     const bool dlds = DICT_LDS > 0 && dict && dalign && (w == 4 || w == 8) && ck.dict_data != nullptr &&
                       ck.dict_n > 0 && uint64_t(ck.dict_n) * uint64_t(w) <= DICT_LDS;
+    // The block's dictionary ids, when the run table covers the block and their bytes fit behind the
+    // dictionary: staged in LDS with the dictionary's loads (round 5), so the tiles read ids from LDS
+    // instead of issuing a round of id loads per tile batch. Page id byte k is staged byte k - idd.
+    const uint32_t dbytes = dlds ? (uint32_t(ck.dict_n) * uint32_t(w) + 15u) & ~15u : 0u;
+    uint8_t* const sid = reinterpret_cast<uint8_t*>(S.dict) + dbytes;
+    int64_t idd = 0;
+    bool ilds = false;
+    if (dict && dalign && (w == 4 || w == 8) && id_bw > 0 && id_bw <= 32 && s.val_n > 0 && S.vres != 2 &&
+        S.vlo <= e_begin && e_end <= S.vcover) {
+        if (tid == 0) { S.ib[0] = 0xffffffffu; S.ib[1] = 0u; }
+        __syncthreads();
+        for (int r = tid; r < S.nvrun; r += NT) {
+            const Run R = S.vrun[r];
+            const uint32_t f = max(R.first, e_begin), l = min(R.first + R.count, e_end);
+            if (!R.packed || f >= l) continue;
+            atomicMin(&S.ib[0], uint32_t((uint64_t(R.data) + uint64_t(f - R.first) * uint64_t(id_bw)) >> 3));
+            atomicMax(&S.ib[1], uint32_t((uint64_t(R.data) + uint64_t(l - R.first) * uint64_t(id_bw) + 7u) >> 3));
+        }
+        __syncthreads();
+        const uint32_t lo = S.ib[0], hi = S.ib[1];
+        if (lo < hi && hi <= ids_n) {
+            const uintptr_t a0 = (reinterpret_cast<uintptr_t>(ids) + lo) & ~uintptr_t(15);
+            const uintptr_t aend = reinterpret_cast<uintptr_t>(ids) + ids_n;     // readable source end
+            const uint32_t nb = (uint32_t(reinterpret_cast<uintptr_t>(ids) + hi - a0) + 8u + 15u) & ~15u;
+            if (dbytes + nb <= uint32_t(sizeof(S.dict))) {
+                ilds = true;
+                idd = int64_t(a0) - int64_t(reinterpret_cast<uintptr_t>(ids));
+                for (uint32_t c = tid; c < nb / 16u; c += NT) {
+                    const uintptr_t a = a0 + 16u * c;
+                    u32x4 x;
+                    if (a + 16u <= aend) {
+                        x = *reinterpret_cast<const PF_GLOBAL u32x4*>(a);
+                    } else {   // the section's last bytes: no read past it
+                        uint32_t q[4] = {0, 0, 0, 0};
+                        for (uint32_t b = 0; b < 16u && a + b < aend; b++)
+                            q[b >> 2] |= uint32_t(*reinterpret_cast<const PF_GLOBAL uint8_t*>(a + b)) << (8 * (b & 3));
+                        x = u32x4{q[0], q[1], q[2], q[3]};
+                    }
+                    reinterpret_cast<u32x4*>(sid)[c] = x;
+                }
+            }
+        }
+    }
     if (dlds) {
         if (w == 8) {
             const uint64_t* g = reinterpret_cast<const uint64_t*>(ck.dict_data);
@@ -2260,8 +2304,8 @@ __device__ __forceinline__ int flat_present_fixed(Lds& S, const DevChunk& ck, co
             uint32_t* d32 = reinterpret_cast<uint32_t*>(S.dict);
             for (uint32_t i = tid; i < uint32_t(ck.dict_n); i += NT) d32[i] = g[i];
         }
-        __syncthreads();
     }
+    if (dlds || ilds) __syncthreads();
     for (uint32_t e0 = e_begin, want = 0; e0 < e_end; e0 += want) {
         want = min(uint32_t(FTX), e_end - e0);
         int bad = 0;
@@ -2307,8 +2351,15 @@ __device__ __forceinline__ int flat_present_fixed(Lds& S, const DevChunk& ck, co
                     id[k] = R.data;
                     if (R.packed) {
                         const uint64_t bit = uint64_t(R.data) + uint64_t(e - R.first) * uint64_t(id_bw);
-                        id[k] = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
-                                                         : bits_le(ids, ids_n, bit, id_bw);
+                        if (ilds) {
+                            const uint32_t rb = uint32_t(int64_t(bit) - 8 * idd);
+                            const uint32_t* q = reinterpret_cast<const uint32_t*>(sid) + (rb >> 5);
+                            const uint64_t x = (uint64_t(q[0]) | (uint64_t(q[1]) << 32)) >> (rb & 31u);
+                            id[k] = uint32_t(x & (id_bw == 32 ? 0xffffffffull : ((1ull << id_bw) - 1ull)));
+                        } else {
+                            id[k] = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
+                                                             : bits_le(ids, ids_n, bit, id_bw);
+                        }
                     }
                 } else if (enc == 0) {
                     if ((uint64_t(e) + 1) * uint64_t(w) > s.val_n) { bad = 1; continue; }
