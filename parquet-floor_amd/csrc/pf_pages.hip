@@ -2232,8 +2232,12 @@ __global__ __launch_bounds__(64) void k_snappy_head(SnappyJob* __restrict__ jobs
 #define PF_DICT_LDS 16384   // 16 KiB: 0.8 % faster SF1 step than 32 KiB (occupancy), 64 KiB 8 % slower (tools/gpu_ab_libs.sh)
 #endif
 constexpr uint32_t DICT_LDS = PF_DICT_LDS;   // bytes of a fixed-width dictionary staged in LDS (k_flat_fixed)
+#ifndef PF_FIX_IDS
+#define PF_FIX_IDS 0   // extra LDS bytes behind the dictionary for a block's ids (6144, which fits the date
+                       // columns' 10 + 12 KB, costs a workgroup per CU: SF1 2.660-2.663 vs 2.632-2.655 ms)
+#endif
 struct FixedLds {
-    uint64_t dict[DICT_LDS / 8 + 2];   // the dictionary, then the block's id bytes when they fit behind it
+    uint64_t dict[(DICT_LDS + PF_FIX_IDS) / 8 + 2];   // the dictionary, then the block's id bytes when they fit
     Run vrun[RUN_CAP];
     uint32_t coff[FTX / 64];
     RunWalk vst;
