@@ -557,20 +557,10 @@ __global__ __launch_bounds__(NT) void k_ba_tile(BaJob* __restrict__ jobs, const 
         #pragma unroll
         for (int i = 0; i < 9; i++) E[i] = __builtin_amdgcn_alignbyte(D[i + 1], D[i], s);
         const int64_t room = int64_t(n) - q0 - 4;
-        // positions whose length's top byte is zero: the only ones that can fit a stream under 16 MiB
-        // (round 5: the 33-position test below ran for every position; text has few such bytes)
-        uint64_t zb = 0;   // bit j: stage byte (a & ~3) + j is zero
-        #pragma unroll
-        for (int i = 0; i < 10; i++) {
-            const uint32_t f = ~(((D[i] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | D[i] | 0x7f7f7f7fu);   // 0x80 per zero byte
-            zb |= uint64_t(((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u)) << (4 * i);
-        }
-        uint64_t cand = room < (int64_t(1) << 24) ? (zb >> (s + 3u)) & ((2ull << 32) - 1ull) : ((2ull << 32) - 1ull);
         uint64_t fit = 0;
-        while (cand) {
-            const int b = __ffsll((unsigned long long)cand) - 1;
-            cand &= cand - 1;
-            const uint32_t l = __builtin_amdgcn_alignbyte(E[(b >> 2) + 1], E[b >> 2], uint32_t(b & 3));
+        #pragma unroll
+        for (int b = 0; b <= 32; b++) {
+            const uint32_t l = (b & 3) == 0 ? E[b >> 2] : __builtin_amdgcn_alignbyte(E[(b >> 2) + 1], E[b >> 2], b & 3);
             fit |= uint64_t(int64_t(l) <= room - b && q0 + b >= 0) << b;
         }
         uint64_t m = 0;
