@@ -95,7 +95,9 @@ METRIC = "decoded GB/s + rows/s (node), lineitem-shape Snappy+dict, 1/2/4/8 GPUs
 
 WORKLOADS = {
     # physical file, logical row groups, row groups per decode batch
-    "sf1": dict(rows=SF1_ROWS, rg_rows=RG_ROWS, seed=SEED, kind="lineitem", batch=0),
+    # slice_mult 2: each column cut into twice as many row-group slices as its LPT share needs
+    # (2.612-2.624 vs 2.634-2.653 ms at 1, 2.658-2.679 at 3; r05, gpurun_out/slices_sf1)
+    "sf1": dict(rows=SF1_ROWS, rg_rows=RG_ROWS, seed=SEED, kind="lineitem", batch=0, slice_mult=2),
     "sf100": dict(rows=8_000_000, rg_rows=4_000_000, seed=43, kind="lineitem", batch=1, logical=150),
     "wide": dict(rows=1_000_000, rg_rows=1_000_000, seed=4, kind="wide", batch=1),
     # (configs[4]) l optional LIST<STRUCT<a INT64 (DELTA_BINARY_PACKED), b UTF8 (dictionary)>>, v2 pages
@@ -230,14 +232,14 @@ def units_for_rank(args, pf, world, rank, S, batch=None):
         # of adding up. A column heavier than a context's fair share is cut into that many slices of
         # its row groups; slices go longest-processing-time first (compressed bytes) to the least
         # loaded context.
-        sw = getattr(args, "string_weight", 1.0)
+        sw = getattr(args, "string_weight", None) or 1.0
         size = {(p, c): chunk_cost(pf, p, c, getattr(args, "lpt_cost", "compressed")) *
                 (sw if pf.columns[c].physical_type == 6 else 1.0) for _, p, _ in units for c in cols}
         cost = {c: sum(size[(p, c)] for _, p, _ in units) for c in cols}
         share = sum(cost.values()) / S
         slices = []
         for c in cols:
-            k = max(1, min(len(units), int(-(-cost[c] // max(1, int(share))))))
+            k = max(1, min(len(units), int(-(-cost[c] // max(1, int(share)))) * (getattr(args, "slice_mult", None) or 1)))
             for j in range(k):
                 us = units[j::k]
                 slices.append((sum(size[(p, c)] for _, p, _ in us), c, [(g, p) for g, p, _ in us]))
@@ -383,7 +385,7 @@ def measure_pmc(args, kernel_re):
         cmd = [prof, "--pmc", cnt, "--kernel-include-regex", kernel_re, "--output-format", "csv", "-d", d, "-o", "run",
                "--", sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
                "--data-dir", args.data_dir, "--streams", str(args.streams), "--split", args.split, "--pool", str(args.pool),
-               "--string-ctx", str(args.string_ctx), "--lpt-cost", args.lpt_cost, "--string-weight", str(args.string_weight)] + \
+               "--string-ctx", str(args.string_ctx), "--lpt-cost", args.lpt_cost, "--string-weight", str(args.string_weight), "--slice-mult", str(args.slice_mult)] + \
               (["--rg-batch", str(args.rg_batch)] if args.rg_batch is not None else [])
         t0 = time.time()
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
@@ -704,6 +706,8 @@ def main():
     ap.add_argument("--string-weight", type=float, default=None,
                     help="--split columns: LPT cost multiplier of BYTE_ARRAY chunks (their value walk, chars count and "
                          "copy); default: the workload's (flat 4, others 1)")
+    ap.add_argument("--slice-mult", type=int, default=None,
+                    help="--split columns: row-group slices per column x this (default: the workload's; sf1 2, others 1)")
     ap.add_argument("--lpt-cost", choices=("decompressed", "compressed"), default="compressed",
                     help="sf1 --split columns: the per-chunk cost the column slices are dealt by")
     ap.add_argument("--columns", default=None, help=argparse.SUPPRESS)   # analysis only: comma-separated column subset
@@ -723,6 +727,8 @@ def main():
     args, _ = ap.parse_known_args()
     if args.string_weight is None:
         args.string_weight = WORKLOADS[args.workload].get("string_weight", 1.0)
+    if args.slice_mult is None:
+        args.slice_mult = WORKLOADS[args.workload].get("slice_mult", 1)
     if args.pmc_child:
         return pmc_child(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -957,6 +963,7 @@ def main():
                                   f"{S} decode streams per GPU" +
                                   (f", each stream a column subset (column slices dealt LPT on {args.lpt_cost} bytes"
                                    + (f", BYTE_ARRAY chunks weighted x{args.string_weight:g}" if args.string_weight != 1.0 else "")
+                                   + (f", x{args.slice_mult} row-group slices per column" if args.slice_mult != 1 else "")
                                    + ")" if args.split == "columns" and S > 1 and wl_batch(args) <= 0 else "")},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "stage_ms_source": "context 0's per-stage HIP events, separate untimed passes (all streams decoding, "
