@@ -113,3 +113,44 @@ def test_bench_work_plan_shards_row_groups():
     plan, _, _ = bench.units_for_rank(a, FakePF(1, 500), 1, 0, 4)
     cols = sorted(c for ctx in plan for b in ctx for u in b for c in u[2])
     assert cols == list(range(500)) and len(plan) == 4
+
+
+def test_bench_column_split_plan_covers_every_chunk_once():
+    """bench.py's column-split plan (SF1's, config 1's): column slices dealt LPT to the streams, with
+    the per-workload BYTE_ARRAY weight and row-group slice multiplier. Every (row group, column) chunk
+    is decoded by exactly one stream, for multipliers 1-3 and 1/2 ranks."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import argparse
+    import random
+    import bench
+
+    class Col:
+        def __init__(self, pt):
+            self.physical_type = pt
+
+    class FakePF:
+        def __init__(self, nrg, ncol, seed):
+            rng = random.Random(seed)
+            self.num_row_groups, self.num_columns = nrg, ncol
+            self.columns = [Col(6 if c % 5 == 4 else 2) for c in range(ncol)]
+            self.size = {(p, c): rng.randint(1, 40) << 20 for p in range(nrg) for c in range(ncol)}
+
+        def chunk_range(self, p, c):
+            return (0, self.size[(p, c)])
+
+    for wl in ("sf1", "flat"):
+        for mult in (1, 2, 3):
+            for world in (1, 2):
+                seen = []
+                for rank in range(world):
+                    a = argparse.Namespace(workload=wl, split="columns", slice_mult=mult, string_weight=None,
+                                           lpt_cost="compressed")
+                    plan, n_log, mine = bench.units_for_rank(a, FakePF(6, 16, 7), world, rank, 4)
+                    assert len(plan) <= 4
+                    for ctx in plan:
+                        for batch in ctx:
+                            for g, p, cols in batch:
+                                assert g in mine and p == g % 6
+                                seen += [(g, c) for c in cols]
+                assert sorted(seen) == sorted((g, c) for g in range(n_log) for c in range(16)), (wl, mult, world)
