@@ -2299,14 +2299,27 @@ __device__ __forceinline__ int flat_present_fixed(Lds& S, const DevChunk& ck, co
             }
         }
     }
-    if (dlds) {
+    if (dlds) {   // eight loads a thread in flight per round (a 2,526-entry date dictionary: 2 rounds, not 10)
+        const uint32_t dn = uint32_t(ck.dict_n);
         if (w == 8) {
-            const uint64_t* g = reinterpret_cast<const uint64_t*>(ck.dict_data);
-            for (uint32_t i = tid; i < uint32_t(ck.dict_n); i += NT) S.dict[i] = g[i];
+            const PF_GLOBAL uint64_t* g = (const PF_GLOBAL uint64_t*)(ck.dict_data);
+            for (uint32_t i0 = tid; i0 < dn; i0 += 8u * NT) {
+                uint64_t v[8];
+                #pragma unroll
+                for (uint32_t k = 0; k < 8; k++) v[k] = i0 + k * NT < dn ? g[i0 + k * NT] : 0ull;
+                #pragma unroll
+                for (uint32_t k = 0; k < 8; k++) if (i0 + k * NT < dn) S.dict[i0 + k * NT] = v[k];
+            }
         } else {
-            const uint32_t* g = reinterpret_cast<const uint32_t*>(ck.dict_data);
+            const PF_GLOBAL uint32_t* g = (const PF_GLOBAL uint32_t*)(ck.dict_data);
             uint32_t* d32 = reinterpret_cast<uint32_t*>(S.dict);
-            for (uint32_t i = tid; i < uint32_t(ck.dict_n); i += NT) d32[i] = g[i];
+            for (uint32_t i0 = tid; i0 < dn; i0 += 8u * NT) {
+                uint32_t v[8];
+                #pragma unroll
+                for (uint32_t k = 0; k < 8; k++) v[k] = i0 + k * NT < dn ? g[i0 + k * NT] : 0u;
+                #pragma unroll
+                for (uint32_t k = 0; k < 8; k++) if (i0 + k * NT < dn) d32[i0 + k * NT] = v[k];
+            }
         }
     }
     if (dlds || ilds) __syncthreads();
