@@ -4435,12 +4435,14 @@ void launch_nest_decode(const DevChunk* d_chunks, DevPage* d_pages, const int2* 
                         hipStream_t st) {
     if (n_segs > 0) hipLaunchKernelGGL(k_decode_seg, dim3(n_segs), dim3(NT), 0, st, d_chunks, d_pages, d_segs, d_res);
 }
-void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, const int2* d_dblk, int n_dblk,
+void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int n_flat, const int2* d_dblk, int n_dblk,
                   DevChunkResult* d_res, BaJob* d_bajobs, hipStream_t st, int idle_grid) {
-    // d_dblk: (page, block) pairs of the flat dictionary BYTE_ARRAY pages (k_count_dict, before k_count_flat)
+    // d_list: the n_flat flat BYTE_ARRAY pages (k_count_flat's grid; none: no launch) first, then the
+    // other pages that need counts. d_dblk: (page, block) pairs of the flat dictionary BYTE_ARRAY
+    // pages (k_count_dict, before k_count_flat)
     if (n <= 0) return;
     if (n_dblk > 0) hipLaunchKernelGGL(k_count_dict, dim3(n_dblk), dim3(NT), 0, st, d_chunks, d_pages, d_dblk, d_res);
-    hipLaunchKernelGGL(k_count_flat, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res, d_bajobs);
+    if (n_flat > 0) hipLaunchKernelGGL(k_count_flat, dim3(n_flat), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res, d_bajobs);
     hipLaunchKernelGGL(k_count, dim3(std::min(n, idle_grid)), dim3(NT), 0, st, d_chunks, d_pages, d_list, n, d_res, d_bajobs);
 }
 // PLAIN BYTE_ARRAY walks of jobs [0, n_jobs) over tiles [0, n_tiles).

@@ -35,7 +35,7 @@ void launch_snappy_litcopy(const SnappyJob*, const int*, int, const int*, hipStr
 void launch_delta(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
 void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_dba_chars(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
-void launch_count(const DevChunk*, DevPage*, const int*, int, const int2*, int, DevChunkResult*, BaJob*, hipStream_t, int);
+void launch_count(const DevChunk*, DevPage*, const int*, int, int, const int2*, int, DevChunkResult*, BaJob*, hipStream_t, int);
 void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
 void launch_flat(const DevChunk*, DevPage*, const int*, int, int, int, int, int*, DevChunkResult*, hipStream_t, NullCaps, int);
 void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool, NullCaps);
@@ -199,6 +199,7 @@ struct pf_ctx {
     std::vector<pf_column_info> info;
     size_t bits_bytes = 0;
     int n_decode_first = 0;                // l_decode: pages that will need k_decode come first
+    int n_count_flat = 0;                  // l_count: flat BYTE_ARRAY pages (k_count_flat's grid) come first
     int n_flat_fixed = 0, n_flat_all = 0, n_null4 = 0, n_null8 = 0;   // l_flat: (page, block) pairs of k_flat_fixed,
                                                                      // k_flat_all, k_flat_null<4>, <8>
     size_t off_npub = 0, npub_bytes = 0;   // k_nest_lvl / k_dbp_pos window hand-overs (scratch), zeroed before the batch
@@ -323,7 +324,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
     EVREC(ctx, ctx->ev[6], st);
     launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, ctx->max_nwin, d_res, st, ctx->opts.nest_timeout);
-    if (!(skip & 16u)) launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), d_cdict, int(ctx->l_cdict.size() / 2),
+    if (!(skip & 16u)) launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), ctx->n_count_flat, d_cdict, int(ctx->l_cdict.size() / 2),
                                        d_res, d_bajobs, st, ctx->opts.count_grid);
     launch_nest_count(d_chunks, d_pages, d_nest, n_nest, d_nseg, n_nseg, d_res, st);
     if (!(skip & 4u))
@@ -1367,13 +1368,13 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     std::vector<int> spread[4];
     std::vector<std::vector<int>> sticky[4];
     for (auto& v : sticky) v.resize(static_cast<size_t>(n_chunks));
-    std::vector<int> decode_first;
+    std::vector<int> decode_first, count_rest;
     for (size_t i = 0; i < ctx->pages.size(); i++) {
         const DevPage& pg = ctx->pages[i];
         if (pg.flags & PG_DICT) continue;
         const DevChunk& ck = ctx->chunks[pg.chunk];
         if (pg.encoding == PF_ENC_DELTA_BINARY_PACKED && pg.aux && ck.ptype != PF_BYTE_ARRAY) ctx->l_delta.push_back(int(i));
-        if (ck.needs_count) ctx->l_count.push_back(int(i));
+        if (ck.needs_count) (ck.ptype == PF_BYTE_ARRAY && ck.max_rep == 0 ? ctx->l_count : count_rest).push_back(int(i));
         if (ck.ptype == PF_BYTE_ARRAY && ck.max_rep == 0 && pg.runtab != nullptr &&
             (pg.encoding == PF_ENC_PLAIN_DICTIONARY || pg.encoding == PF_ENC_RLE_DICTIONARY)) {
             const int nb = std::max(1, int((int64_t(pg.num_values) + FLAT_BLK - 1) / FLAT_BLK));
@@ -1405,6 +1406,8 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             ctx->l_decode.push_back(int(i));
     }
     ctx->n_decode_first = int(decode_first.size());
+    ctx->n_count_flat = int(ctx->l_count.size());
+    ctx->l_count.insert(ctx->l_count.end(), count_rest.begin(), count_rest.end());
     ctx->l_decode.insert(ctx->l_decode.begin(), decode_first.begin(), decode_first.end());
     int n_grid[4] = {};
     for (int gi = 0; gi < 4; gi++) {
