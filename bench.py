@@ -189,7 +189,7 @@ def units_for_rank(args, pf, world, rank, S, batch=None):
     units = [(g, g % n_phys, cols) for g in mine]
     if args.workload == "wide" and units:   # one row group: split its columns over the contexts
         g, p, _ = units[0]
-        k = max(1, min(S, len(cols)))
+        k = max(1, min(S * (getattr(args, "wide_groups", None) or 1), len(cols)))   # column groups (batches)
         units = [(g, p, cols[i::k]) for i in range(k)] + units[1:]
     elif getattr(args, "split", "rowgroups") == "kinds" and units and S > 2 and batch is None and \
             wl_batch(args) <= 0:
@@ -706,6 +706,7 @@ def main():
     ap.add_argument("--string-weight", type=float, default=None,
                     help="--split columns: LPT cost multiplier of BYTE_ARRAY chunks (their value walk, chars count and "
                          "copy); default: the workload's (flat 4, others 1)")
+    ap.add_argument("--wide-groups", type=int, default=None, help=argparse.SUPPRESS)   # analysis: wide column batches per stream
     ap.add_argument("--slice-mult", type=int, default=None,
                     help="--split columns: row-group slices per column x this (default: the workload's; sf1 2, others 1)")
     ap.add_argument("--lpt-cost", choices=("decompressed", "compressed"), default="compressed",
