@@ -1495,6 +1495,9 @@ struct X5Lds {
     uint32_t SB[2][X5_W], WP[2][X5_W];   // token starts of the batch's output, tokens in earlier words
     uint32_t REC[2][4];                  // kind, output start, output bytes, long literal input position
     uint16_t jv[256];
+#if defined(PF_X5_PAD) && PF_X5_PAD > 0
+    uint8_t pad[PF_X5_PAD];   // diagnostics: fewer executor workgroups per CU (room for other streams' kernels)
+#endif
 };
 
 // One piece (mode 0: pieces[item]) or one whole-page redo (mode 1: job item) by the workgroup's two waves.
