@@ -3034,7 +3034,11 @@ constexpr uint32_t LVL_JUMP = 8;          // runs per step of k_lvl's chain walk
 constexpr uint32_t LVL_S8 = LVL_NXT / LVL_JUMP;   // walk steps (a run is at least one byte)
 constexpr uint32_t LVL_PPT = LVL_NXT / LT_NT;     // section positions per thread in the table passes
 static_assert(LVL_PPT == 16, "k_lvl's mark words: two threads per 32 positions");
-__global__ __launch_bounds__(LT_NT) void k_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
+#ifndef PF_LVL_OCC
+#define PF_LVL_OCC 1   // k_lvl workgroups per CU the register budget must allow (1: the compiler's choice, 114 VGPRs;
+                       // 5: 96 VGPRs + 80 B scratch, config 4 3.70-3.75 vs 3.68-3.74 ms, not kept)
+#endif
+__global__ __launch_bounds__(LT_NT, PF_LVL_OCC) void k_lvl(const DevChunk* __restrict__ chunks, DevPage* pages, const int* __restrict__ list,
                                                DevChunkResult* res, uint32_t dcap, uint32_t icap) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[LVL_STAGE + 48];
     __shared__ uint32_t scan_tmp[LT_NT / 64];
