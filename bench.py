@@ -160,14 +160,16 @@ def logical_row_groups(args, n_phys, world):
     return w.get("logical", n_phys)
 
 
-def chunk_cost(pf, p, c, kind):
+def chunk_cost(pf, p, c, kind, row_cost=0.0):
     """LPT cost of one column chunk: its compressed bytes, or the decompressed bytes of its pages
     (what the Snappy executor and the value kernels walk: dense integer columns cost more per
-    compressed byte than text)."""
+    compressed byte than text), plus row_cost bytes per row (the flat stage's blocks scale with rows:
+    a 1-bit dictionary column is a few hundred KB but as many blocks as any other column)."""
+    extra = row_cost * pf.row_group_rows(p) if row_cost else 0.0
     if kind == "compressed":
-        return pf.chunk_range(p, c)[1]
+        return pf.chunk_range(p, c)[1] + extra
     d = pf.chunk_desc(p, c, 0)
-    return sum(d.pages[i].uncompressed_size for i in range(d.n_pages))
+    return sum(d.pages[i].uncompressed_size for i in range(d.n_pages)) + extra
 
 
 def wl_batch(args):
@@ -233,7 +235,7 @@ def units_for_rank(args, pf, world, rank, S, batch=None):
         # its row groups; slices go longest-processing-time first (compressed bytes) to the least
         # loaded context.
         sw = getattr(args, "string_weight", None) or 1.0
-        size = {(p, c): chunk_cost(pf, p, c, getattr(args, "lpt_cost", "compressed")) *
+        size = {(p, c): chunk_cost(pf, p, c, getattr(args, "lpt_cost", "compressed"), getattr(args, "row_cost", None) or 0.0) *
                 (sw if pf.columns[c].physical_type == 6 else 1.0) for _, p, _ in units for c in cols}
         cost = {c: sum(size[(p, c)] for _, p, _ in units) for c in cols}
         share = sum(cost.values()) / S
@@ -707,6 +709,7 @@ def main():
                     help="--split columns: LPT cost multiplier of BYTE_ARRAY chunks (their value walk, chars count and "
                          "copy); default: the workload's (flat 4, others 1)")
     ap.add_argument("--wide-groups", type=int, default=None, help=argparse.SUPPRESS)   # analysis: wide column batches per stream
+    ap.add_argument("--row-cost", type=float, default=None, help=argparse.SUPPRESS)   # analysis: LPT bytes per row of a chunk
     ap.add_argument("--slice-mult", type=int, default=None,
                     help="--split columns: row-group slices per column x this (default: the workload's; sf1 2, others 1)")
     ap.add_argument("--lpt-cost", choices=("decompressed", "compressed"), default="compressed",
