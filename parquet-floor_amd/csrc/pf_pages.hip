@@ -2089,7 +2089,7 @@ __device__ __forceinline__ void copy_chars_plain(const uint32_t* coff, const uin
 }
 
 #ifndef PF_SHORT_AVG
-#define PF_SHORT_AVG 16
+#define PF_SHORT_AVG 32   // r05: SF1 2.624-2.626 vs 2.630-2.643 ms at 16 (24: 2.610-2.631), configs 1 / 5 unchanged
 #endif
 constexpr uint32_t SHORT_AVG = PF_SHORT_AVG;   // tiles averaging at most this many chars per value: copy_chars_short
 // Short values (dictionary strings such as flags and modes: 1-16 chars): one value per thread,
