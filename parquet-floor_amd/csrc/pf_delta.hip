@@ -307,7 +307,7 @@ __global__ __launch_bounds__(DP_NT) void k_dbp_pos(const DevChunk* __restrict__ 
             }
         }
         if (!ok) dbp_fail(pg);
-        winpub_put(pub[w], xp, xb, xst);
+        winpub_put(pub[w], ok ? xp : ~0ull, xb, xst);   // (failed: the overflow word, later windows fail at once)
     }
     __syncthreads();
     if (s_hand[2] & 2u) return;

@@ -98,6 +98,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, unsigned long 
         if (w < wid) base += t;
         tot += t;
     }
+    __syncthreads();   // every wave has read lds_wave before a caller's next pass overwrites it
     total = tot;
     return base + x - v;
 }

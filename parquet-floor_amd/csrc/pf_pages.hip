@@ -519,7 +519,10 @@ __global__ __launch_bounds__(NT) void k_ba_tile(BaJob* __restrict__ jobs, const 
     __shared__ uint32_t tmp[NT / 64];
     const int2 jt = tiles[blockIdx.x];
     BaJob& J = jobs[jt.x];
-    if (J.state != BA_OK) return;
+    // a job another tile already rejected (BA_RELINK) still needs this tile's candidate words:
+    // ba_relink_wg re-links the job from the whole candidate bitmap
+    const int32_t st0 = J.state;
+    if (st0 == BA_SKIP || st0 == BA_FALLBACK) return;
     const uint32_t n = J.n;
     const uint32_t t0 = uint32_t(jt.y) * BA_TILE;
     if (t0 >= n) {
@@ -3658,6 +3661,7 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
 #undef NSTAMP
 }
 
+#ifdef PF_DIAG   // diagnostics build only (VERDICT r05 hygiene)
 // k_page_null: one 512-thread workgroup per nullable flat page (fixed width 4 / 8, dictionary or
 // PLAIN), for pages whose level section (<= LVL_STAGE bytes), level runs (<= PN_RUNS) and
 // dictionary-id bytes (<= PN_IST) fit its LDS. It runs before k_lvl in the levels stage and does
@@ -3920,6 +3924,7 @@ __global__ __launch_bounds__(PN_NT) void k_page_null(const DevChunk* __restrict_
         atomicOr(&pg.done, DONE_NULL | DONE_PAGE);
     }
 }
+#endif  // PF_DIAG
 
 // ---- nested pages in segments (k_nest_*) --------------------------------------------------------
 // A nested page's levels are walked run by run from its first entry, so k_count / k_decode take it in
@@ -4191,7 +4196,8 @@ __global__ __launch_bounds__(NL_NT) void k_nest_lvl(const DevChunk* __restrict__
         // a hand-over that never came (a scheduling stall, not the data): the page leaves the segment
         // path and k_count / k_decode decode it whole, as k_dbp_pos does with dbp_ok = 2
         if (!ok) __hip_atomic_fetch_max(&pg.seg_ok, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        winpub_put(pub[w], xp, xe, xst);
+        // a failed hand-over is published as the overflow word, so every later window fails at once
+        winpub_put(pub[w], ok ? xp : ~0ull, xe, xst);
     }
     __syncthreads();
     if (s_hand[2] & 2u) return;
@@ -4469,6 +4475,7 @@ void launch_ba(BaJob* d_jobs, int n_jobs, const int2* d_tiles, int n_tiles, DevC
     if (!fused) hipLaunchKernelGGL(k_ba_verify, dim3(n_tiles), dim3(NT), 0, st, d_jobs, d_tiles);
     hipLaunchKernelGGL(k_ba_fallback, dim3(std::min(n_jobs, 64)), dim3(NT), 0, st, d_jobs, n_jobs, d_res);
 }
+#ifdef PF_DIAG   // diagnostics build only (VERDICT r05 hygiene)
 // Diagnostics (tests/test_gpu_runs.py): walk_runs (one lane) and wave_walk_runs (one wave) over the
 // same stream; out = {ret, nruns, covered, pos, first, runs[cap] x 4} for each.
 __global__ __launch_bounds__(64) void k_debug_walk(const uint8_t* p, uint64_t n, int bw, uint32_t lo, uint32_t limit, int cap,
@@ -4518,6 +4525,7 @@ extern "C" int pf_debug_walk_runs(const uint8_t* stream, uint64_t n, int bw, uin
     (void)hipFree(o);
     return rc;
 }
+#endif  // PF_DIAG
 
 // Dictionary pages that are one Snappy literal (k_snappy_head: FB_LITCOPY): the literal's bytes to
 // the page's 16-byte aligned scratch body, 16 bytes per thread per step (aligned dword loads +
@@ -4587,7 +4595,11 @@ void launch_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, i
     if (n <= 0) return;
     // page_null (diagnostics option): k_page_null first (one 512-thread workgroup and ~57 KiB of LDS per
     // page; under the bench's four streams its workgroups wait for whole CUs: config 4 5.57 ms with it, 4.47 without)
+#ifdef PF_DIAG
     if (page_null) hipLaunchKernelGGL(k_page_null, dim3(n), dim3(PN_NT), 0, st, d_chunks, d_pages, d_list, d_res);
+#else
+    (void)page_null;
+#endif
     hipLaunchKernelGGL(k_lvl, dim3(n), dim3(LT_NT), 0, st, d_chunks, d_pages, d_list, d_res, nc.dcap, nc.icap);
 }
 void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int nfix, int n, int n4, int n8, int* d_fbq,

@@ -188,6 +188,7 @@ struct pf_ctx {
     int n_ba_dict = 0, n_ba_dict_tiles = 0;
     bool ba_short_dict = true, ba_short_data = true;   // every walk job's values average <= BA_SHORT bytes: k_ba_tile
     uint32_t null_dict_lds = 0;            // bytes of the largest nullable-page dictionary that fits k_flat_null's LDS stage
+    bool meta_by_kernel = false;   // this batch's metadata went up by k_upload (which also zeroes bits / npub)
     uint32_t null_dcap = 16, null_icap = 16;   // k_flat_null's level / id byte stages (NullCaps)
     int max_snap_win = 1;                  // index windows of the batch's largest Snappy job (k_snappy_chain's tables)
     uint32_t n_splits = 0;
@@ -284,7 +285,7 @@ int enqueue_kernels(pf_ctx* ctx) {
 #else
     constexpr unsigned skip = 0;
 #endif
-    if (!(ctx->zc && ctx->h_meta.d)) {   // (the zero-copy upload, k_upload, zeroes them)
+    if (!ctx->meta_by_kernel) {   // (the zero-copy upload, k_upload, zeroes them)
         if (ctx->bits_bytes) HIPCHK(ctx, hipMemsetAsync(ctx->d_bits.p, 0, ctx->bits_bytes, st));
         if (ctx->npub_bytes)
             HIPCHK(ctx, hipMemsetAsync(static_cast<uint8_t*>(ctx->d_scratch.p) + ctx->off_npub, 0, ctx->npub_bytes, st));
@@ -468,12 +469,16 @@ int upload_meta(pf_ctx* ctx) {
             r[c].num_rows = ck.num_entries;
         }
     }
-    if (ctx->zc && ctx->h_meta.d) {   // enqueue_kernels follows at once on the same stream
+    // k_upload counts in 32 bits: an arena of 4 GiB or more takes the copy path (its zero fills below)
+    const bool small = ctx->meta_bytes / 8 < (1ull << 31) && ctx->bits_bytes < (1ull << 31) && ctx->npub_bytes < (1ull << 31);
+    ctx->meta_by_kernel = ctx->zc && ctx->h_meta.d && small;
+    if (ctx->meta_by_kernel) {   // enqueue_kernels follows at once on the same stream
         const uint32_t n = uint32_t(ctx->meta_bytes / 8), nz0 = uint32_t(ctx->bits_bytes), nz1 = uint32_t(ctx->npub_bytes);
         const uint32_t grid = std::max(1u, std::min(1024u, (n + (nz0 + 7u) / 8u + (nz1 + 7u) / 8u + 255u) / 256u));
         hipLaunchKernelGGL(k_upload, dim3(grid), dim3(256), 0, ctx->stream, static_cast<uint64_t*>(ctx->d_meta.p),
                            static_cast<const uint64_t*>(ctx->h_meta.d), n, static_cast<uint8_t*>(ctx->d_bits.p), nz0,
                            static_cast<uint8_t*>(ctx->d_scratch.p) + ctx->off_npub, nz1);
+        HIPCHK(ctx, hipGetLastError());
     } else {
         HIPCHK(ctx, hipMemcpyAsync(ctx->d_meta.p, h, ctx->meta_bytes, hipMemcpyHostToDevice, ctx->stream));
     }
@@ -1282,8 +1287,12 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
                 // level / id byte stages: FBLK values of the level width / the dictionary's id width
                 // (bit width of its largest index, as writers choose it) + run headers
                 auto bits = [](uint64_t v) { int b = 0; while (v) { b++; v >>= 1; } return b; };
+                // hybrid worst case: bit-packed, FLAT_BLK * b / 8 bytes + headers; or RLE runs of
+                // 8 repeats, a header byte + ceil(b / 8) value bytes per 8 entries (1-bit levels: 1 KiB)
                 auto cap = [](int b, uint32_t most) {
-                    return uint32_t(std::min<uint64_t>(most, align_up(uint64_t(FLAT_BLK) * uint64_t(b) / 8 + NL_SLACK, 16)));
+                    const uint64_t bp = uint64_t(FLAT_BLK) * uint64_t(b) / 8;
+                    const uint64_t rle = uint64_t(FLAT_BLK) / 8 * (1 + (uint64_t(b) + 7) / 8);
+                    return uint32_t(std::min<uint64_t>(most, align_up(std::max(bp, rle) + NL_SLACK, 16)));
                 };
                 ctx->null_dcap = std::max(ctx->null_dcap, cap(bits(uint64_t(std::max(lc.max_def, 0))), NL_DST));
                 if (lc.dict_page >= 0)

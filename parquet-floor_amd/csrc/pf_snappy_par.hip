@@ -1036,7 +1036,7 @@ constexpr uint32_t XSTAGE = XCHUNK + 64 + 16;
 #ifndef PF_XBATCH
 #define PF_XBATCH 1024
 #endif
-constexpr uint32_t XBATCH = PF_XBATCH;   // output bytes of one parallel step (ring: XBATCH + XSLOT <= XRING)
+[[maybe_unused]] constexpr uint32_t XBATCH = PF_XBATCH;   // output bytes of one parallel step (ring: XBATCH + XSLOT <= XRING)
 constexpr uint32_t XLIT = 1024;      // long literals are copied in pieces of this many bytes
 constexpr uint32_t FBUF_W = 17;      // dwords per far copy's source slot (64 bytes + misalignment)
 #ifndef PF_XFAR
@@ -1165,11 +1165,12 @@ __device__ __forceinline__ void wait_vmem_last_slot() {   // all but the last fl
 // Self-overlapping copies read source byte (j mod offset), so a run never chains through itself.
 // Dependent copies therefore cost a few register rounds per 64 bytes instead of one serial
 // read-then-write per token.
-constexpr uint32_t X2_STAGE_OFF = XRING;                            // [ring | stage | far slots] in one LDS array,
+[[maybe_unused]] constexpr uint32_t X2_STAGE_OFF = XRING;                            // [ring | stage | far slots] in one LDS array,
 constexpr uint32_t X2_FBUF_OFF = XRING + ((XSTAGE + 15u) & ~15u);   // so one byte address selects any source
-constexpr uint32_t X2_LDS = X2_FBUF_OFF + XFAR * FBUF_W * 4;
+[[maybe_unused]] constexpr uint32_t X2_LDS = X2_FBUF_OFF + XFAR * FBUF_W * 4;
 enum : uint32_t { X2_LDSADDR = 0, X2_COPY = 1 };
 
+#ifdef PF_DIAG   // diagnostics build only (VERDICT r05 hygiene)
 __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
                                                      const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
     __shared__ __attribute__((aligned(16))) uint8_t L[X2_LDS];
@@ -1452,6 +1453,7 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
         put16(od, a, *reinterpret_cast<const u32x4*>(ring + (a & XRMASK)));
     for (uint32_t a = F + ((op - F) & ~15u) + uint32_t(lane); a < op; a += 64) put1(od, a, ring[a & XRMASK]);
 }
+#endif  // PF_DIAG
 
 // ======================================================================== executor v5
 //
@@ -1879,11 +1881,16 @@ void launch_snappy_exec(const SnappyJob* d_jobs, int n_jobs, const int2* d_piece
     if (n_jobs <= 0) return;
     // exec (PfOpts; the diagnostics build's PF_EXEC): 5 = producer / consumer waves (default), 2 = one wave
     // per piece. The whole-page redo is always the same kernel's mode 1.
+#ifdef PF_DIAG
     if (exec == 2) {
         hipLaunchKernelGGL(k_snappy_exec2, dim3(n_pieces), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
         // whole-page redo of pages whose pieces were not independent
         hipLaunchKernelGGL(k_snappy_exec2, dim3(n_jobs), dim3(64), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
-    } else {
+    } else
+#else
+    (void)exec;
+#endif
+    {
         hipLaunchKernelGGL(k_snappy_exec5, dim3(n_pieces), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 0);
         hipLaunchKernelGGL(k_snappy_exec5, dim3(n_jobs), dim3(128), 0, s, d_jobs, d_pieces, (const uint32_t*)d_splits, d_fb, 1);
     }

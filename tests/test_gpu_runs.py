@@ -46,7 +46,11 @@ def _stream(rng, bw, kind):
 @pytest.mark.parametrize("kind", ["uniform", "mixed", "truncated", "corrupt"])
 def test_wave_walk_matches_lane_walk(kind):
     from pfloor import _native
-    L = _native.lib()
+    with _native.diagnostics() as L:   # (pf_debug_walk_runs is built into the diagnostics library only)
+        _walk_cases(L, kind)
+
+
+def _walk_cases(L, kind):
     f = L.pf_debug_walk_runs
     f.argtypes = [C.c_char_p, C.c_uint64, C.c_int, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32,
                   C.POINTER(C.c_uint32)]

@@ -109,3 +109,31 @@ def test_dict_strings_multi_pass_tiles(decoder, oracle, tmp_path, nulls):
     assert got["_status"] == 0, got["_error"]
     with oracle.open(path) as of:
         assert_chunk_equal(got[(0, 0)], of.decode(0, 0), f"dict long nulls={nulls}")
+
+
+def test_dict_strings_page_over_256_blocks(decoder, oracle, tmp_path):
+    """One dictionary string page of 1.5M values: more than 256 blocks of 4096 entries, so
+    k_count_flat scans the block chars in several passes of block_excl_scan64 (the
+    scan's LDS totals must not be overwritten by a fast wave of the next pass). A required and a
+    nullable column, each one data page, bit-exact vs the oracle."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from pfloor.decoder import decode_file
+    rng = np.random.default_rng(41)
+    n = 1_500_000
+    vocab = np.array(["v%05d" % i + "x" * (i % 7) for i in range(40)], dtype=object)
+    mask = rng.random(n) < 0.1
+    t = pa.table({"s": pa.array(vocab[rng.integers(0, 40, n)], type=pa.string()),
+                  "m": pa.array(vocab[rng.integers(0, 40, n)], type=pa.string(), mask=mask)})
+    path = str(tmp_path / "dict_big_page.parquet")
+    pq.write_table(t, path, compression="snappy", use_dictionary=True, row_group_size=n,
+                   data_page_size=64 << 20, max_rows_per_page=n)
+    with oracle.open(path) as of:
+        for c in range(2):
+            pages = of.chunk_pages(0, c)[2]
+            assert max(p["num_values"] for p in pages) == n
+    got = decode_file(path, decoder=decoder)
+    assert got["_status"] == 0, got["_error"]
+    with oracle.open(path) as of:
+        for c in range(2):
+            assert_chunk_equal(got[(0, c)], of.decode(0, c), f"dict big page col {c}")
