@@ -1473,46 +1473,87 @@ __global__ __launch_bounds__(64) void k_snappy_exec2(const SnappyJob* __restrict
 // that guarantees the bytes (and their cache line) are in HBM, and a far copy above it cuts the batch
 // (one empty batch when it is the first token, which only follows a long literal).
 #ifndef PF_X5_BATCH
-#define PF_X5_BATCH 768
+#define PF_X5_BATCH 764
 #endif
 constexpr uint32_t X5_BATCH = PF_X5_BATCH;                     // output bytes of one batch (ring: + XSLOT + far margin)
 constexpr uint32_t X5_STG = (XSTAGE + 15u) & ~15u;     // one staged input chunk
-constexpr uint32_t X5_FSL = XFAR * FBUF_W * 4u;        // far-copy source slots of one batch
+constexpr uint32_t X5_FSLOT = 80u;                     // a far copy's source: 5 aligned 16-byte chunks (<= 64 B + shift < 16)
+constexpr uint32_t X5_FSL = XFAR * X5_FSLOT;           // far-copy source slots of one batch
 constexpr uint32_t X5_STAGE0 = XRING;                  // [ring | stage x2 | far slots x2]: one byte address
 constexpr uint32_t X5_FBUF0 = XRING + 2u * X5_STG;     // selects any byte source
 constexpr uint32_t X5_LDS = X5_FBUF0 + 2u * X5_FSL;
-constexpr uint32_t X5_W = X5_BATCH / 32u;              // token-start words of a batch
+constexpr uint32_t X5_W = 768u / 32u;                  // token-start words of a batch (+ its alignment bytes)
 constexpr uint32_t X5_LINE = 128u;                     // a far source's cache line must be wholly landed
+constexpr uint32_t X5_FREAD = 5u * 16u;                // bytes a far load reads from its 16-byte aligned base
+constexpr uint32_t X5_DS = 65u;                        // descriptor table: entry t at [t], its second word at [t + X5_DS]
+static_assert(X5_BATCH + 3u <= 768u, "a batch and its alignment bytes are at most three 256-byte windows");
+static_assert((X5_FBUF0 & 15u) == 0u && (X5_FSLOT & 15u) == 0u, "far slots are 16-byte aligned");
 enum : uint32_t { R5_NORMAL = 0, R5_LONG = 1, R5_NOP = 2, R5_END = 3, R5_BAD = 4 };
+// Descriptor word 0: the token's first output byte relative to the batch's 4-byte aligned base S
+// (bits 0-14), bit 15 a copy whose source is read through the ring / the window, bits 16-31 its offset.
+// Word 1: a literal or far copy: the LDS address of its byte at base position x is word1 + x; a ring
+// copy: rcp(offset) as a float (byte x's source is x - offset * (1 + floor((x - start) / offset)), the
+// same byte an overlapping copy reads as (x - start) mod offset). Entry 0 is a dummy literal for the
+// batch's alignment bytes (token t of the batch is entry t + 1).
+constexpr uint32_t X5_CP = 0x8000u;
 
 // Workgroup barrier for LDS hand-over only (no wait on outstanding global stores).
 __device__ __forceinline__ void x5_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 // Compiler ordering point for one wave's LDS accesses (the hardware runs them in order).
 __device__ __forceinline__ void x5_order() { asm volatile("" ::: "memory"); }
 
+// Two 16-bit jump words at once: each half of w still pending (bit 15) takes the half of g
+// (v_pk_ashrrev_i16 makes the per-half mask, v_bfi_b32 merges; the compiler otherwise splits the halves).
+__device__ __forceinline__ uint32_t x5_pick(uint32_t w, uint32_t g) {
+    uint32_t m, r;
+    asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(m) : "v"(w));   // (the shift in both halves)
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(g), "v"(w));
+    return r;
+}
+
 struct X5Lds {
     __attribute__((aligned(16))) uint8_t L[X5_LDS];
     uint16_t tokpos[XCHUNK / 2];
-    uint32_t D0[2][64], D1[2][64];     // packed token descriptors (exec2's d0 / d1)
-    uint32_t SB[2][X5_W], WP[2][X5_W];   // token starts of the batch's output, tokens in earlier words
+    uint32_t D[2][2 * X5_DS];            // token descriptors (entry 0: the dummy literal)
+    uint32_t SB[2][X5_W], WP[2][X5_W];   // token starts from the batch's aligned base, tokens in earlier words
     uint32_t REC[2][4];                  // kind, output start, output bytes, long literal input position
-    uint16_t jv[256];
+    __attribute__((aligned(8))) uint16_t jv[256];
 #if defined(PF_X5_PAD) && PF_X5_PAD > 0
     uint8_t pad[PF_X5_PAD];   // diagnostics: fewer executor workgroups per CU (room for other streams' kernels)
 #endif
 };
+
+// 16 input bytes from gin[src] (src + 15 < the stream's end) as four dwords: 16-byte aligned loads only
+// (the second chunk only when src is not aligned), so no load passes the chunk holding the last byte.
+__device__ __forceinline__ u32x4 x5_load16(const PF_GLOBAL uint8_t* gin, uint32_t src) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(gin) + src;
+    const PF_GLOBAL u32x4* p = (const PF_GLOBAL u32x4*)(a & ~uintptr_t(15));
+    const uint32_t sh = uint32_t(a & 15u);
+    const u32x4 A = p[0];
+    u32x4 B = A;
+    if (sh) B = p[1];
+    const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    const uint32_t k = sh >> 2, s = sh & 3u;
+    u32x4 r;
+    #pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t lo = k == 0 ? w[i] : (k == 1 ? w[i + 1] : (k == 2 ? w[i + 2] : w[i + 3]));
+        const uint32_t hi = k == 0 ? w[i + 1] : (k == 1 ? w[i + 2] : (k == 2 ? w[i + 3] : w[i + 4]));
+        r[i] = __builtin_amdgcn_alignbyte(hi, lo, s);
+    }
+    return r;
+}
 
 // One piece (mode 0: pieces[item]) or one whole-page redo (mode 1: job item) by the workgroup's two waves.
 __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
                                             const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode, int item) {
     uint8_t* const L = S.L;
     uint16_t* const tokpos = S.tokpos;
-    auto& D0 = S.D0;
-    auto& D1 = S.D1;
+    auto& D = S.D;
     auto& SB = S.SB;
     auto& WP = S.WP;
     auto& REC = S.REC;
-    uint16_t* const jv = S.jv;
+    uint8_t* const jvb = reinterpret_cast<uint8_t*>(S.jv);
     uint8_t* const ring = L;
     const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
     const int lane = int(threadIdx.x) & 63;
@@ -1562,6 +1603,10 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
     const PF_GLOBAL uint8_t* gin = gptr(in);
     PF_GLOBAL uint8_t* gdst = gptr(job.dst);
     const OutDst od{gdst, mode == 0 ? gptr(job.ddst) : nullptr, job.dlo, job.dgran};
+    if (threadIdx.x < 2) {   // the dummy entry of both descriptor buffers (a literal reading ring bytes)
+        D[threadIdx.x][0] = 0u;
+        D[threadIdx.x][X5_DS] = 0u;
+    }
     // producer state
     uint32_t op = out_start, sb = 0, T = 0, I = 0, woff = 0, cb = 1;
     uint32_t ops_m1 = out_start, k_m1 = R5_NOP, k_m2 = R5_NOP, nops = 0;
@@ -1640,7 +1685,8 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                     const uint32_t a = otok - off;          // copy source start
                     const bool farc = take && kd != 0 && a + min(ol, off) <= op &&
                                       int32_t(a - (op + X5_BATCH - XRING)) < 0;
-                    const bool fnr = farc && a + ol + X5_LINE > LF;   // source not yet landed in HBM
+                    // source not yet landed in HBM: every cache line its 80-byte aligned read touches must be
+                    const bool fnr = farc && a + X5_FREAD + X5_LINE > LF;
                     const unsigned long long farm = __ballot(farc);
                     const uint32_t frank = uint32_t(__popcll(farm & lane_mask_lt(uint32_t(lane))));
                     const unsigned long long cutm =
@@ -1672,36 +1718,46 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                         if (od.dd != nullptr && __any(far && a < od.dlo && a + ol > od.dlo)) ok = false;
                         X5T(1);   // token decode, chain checks, cuts
                         if (ok) {
-                            uint32_t* fl = reinterpret_cast<uint32_t*>(L + X5_FBUF0 + b * X5_FSL) + frank * FBUF_W;
-                            if (far) {
-                                const PF_GLOBAL uint8_t* fb0 = od.dd != nullptr && a >= od.dlo ? od.dd + a : gdst + a;
-                                const uintptr_t fa = reinterpret_cast<uintptr_t>(fb0);
-                                const PF_GLOBAL uint32_t* fsrc = (const PF_GLOBAL uint32_t*)(fa & ~uintptr_t(3));
-                                const uint32_t nwd = (uint32_t(fa & 3u) + ol + 3u) >> 2;
-                                uint32_t fw[FBUF_W];
-                                #pragma unroll
-                                for (int u = 0; u < int(FBUF_W); u++) fw[u] = uint32_t(u) < nwd ? fsrc[u] : 0u;
-                                #pragma unroll
-                                for (int u = 0; u < int(FBUF_W); u++)
-                                    if (uint32_t(u) < nwd) fl[u] = fw[u];
+                            const PF_GLOBAL uint8_t* fb0 = od.dd != nullptr && a >= od.dlo ? od.dd + a : gdst + a;
+                            const uint32_t fsh = uint32_t(reinterpret_cast<uintptr_t>(fb0) & 15u);
+                            // far-copy sources: five aligned 16-byte chunks each (the arenas keep >= 80 bytes of
+                            // slack), loaded straight into the slots by LDS-DMA -- lane l loads chunk l % 5 of far
+                            // copy l / 5, so the lane-linear destination is the slot layout -- and waited for only
+                            // before the barrier, after the descriptors (no data registers, latency behind them)
+                            const uint32_t nfar = uint32_t(__popcll(farm & lane_mask_lt(cut)));
+                            if (nfar) {
+                                uint64_t* fa = reinterpret_cast<uint64_t*>(L + X5_FBUF0 + b * X5_FSL);   // (overwritten by the loads)
+                                if (far) fa[frank] = reinterpret_cast<uintptr_t>(fb0) & ~uintptr_t(15);
+                                x5_order();
+                                const uint32_t l0 = uint32_t(lane), f0 = (l0 * 205u) >> 10;   // l / 5 for l < 80
+                                const uint64_t s0a = fa[f0] + 16u * (l0 - 5u * f0);
+                                uint64_t s1a = 0;
+                                if (nfar > 12u) {
+                                    const uint32_t l1 = l0 + 64u, f1 = (l1 * 205u) >> 10;
+                                    s1a = fa[min(f1, XFAR - 1u)] + 16u * (l1 - 5u * f1);
+                                }
+                                uint8_t* slots = L + X5_FBUF0 + b * X5_FSL;
+                                if (l0 < 5u * nfar)
+                                    __builtin_amdgcn_global_load_lds((const PF_GLOBAL void*)s0a, (__attribute__((address_space(3))) void*)slots, 16, 0, 0);
+                                if (nfar > 12u && l0 + 64u < 5u * nfar)
+                                    __builtin_amdgcn_global_load_lds((const PF_GLOBAL void*)s1a,
+                                                                     (__attribute__((address_space(3))) void*)(slots + 1024), 16, 0, 0);
                             }
-                            X5T(2);   // far-copy source loads
-                            const uint32_t rel = otok - op;
+                            X5T(2);   // far-copy source loads (issued)
+                            const uint32_t relS = otok - (op & ~3u);   // from the batch's aligned base
                             uint32_t d0 = 0, d1 = 0;
                             if (inb) {
                                 const bool near = cp && !far;
-                                d0 = rel | ((near ? X2_COPY : X2_LDSADDR) << 11) | ((near && off < ol) ? (1u << 12) : 0u) |
-                                     (min(off, 0xffffu) << 16);
-                                const uint32_t fsh = od.dd != nullptr && a >= od.dlo
-                                                         ? uint32_t((reinterpret_cast<uintptr_t>(od.dd) + a) & 3u) : (a & 3u);
-                                d1 = lit ? X5_STAGE0 + cb * X5_STG + woff + (srcv - I)
-                                         : (far ? X5_FBUF0 + b * X5_FSL + frank * (FBUF_W * 4) + fsh : a);
+                                d0 = relS | (near ? (X5_CP | (off << 16)) : 0u);
+                                d1 = near ? __float_as_uint(__builtin_amdgcn_rcpf(float(off)))
+                                          : (lit ? X5_STAGE0 + cb * X5_STG + woff + (srcv - I) - relS
+                                                 : X5_FBUF0 + b * X5_FSL + frank * X5_FSLOT + fsh - relS);
                             }
-                            D0[b][lane] = d0;
-                            D1[b][lane] = d1;
+                            D[b][1 + lane] = d0;
+                            D[b][1 + X5_DS + lane] = d1;
                             if (lane < int(X5_W)) SB[b][lane] = 0;
                             x5_order();
-                            if (inb) atomicOr(&SB[b][rel >> 5], 1u << (rel & 31u));
+                            if (inb) atomicOr(&SB[b][relS >> 5], 1u << (relS & 31u));
                             x5_order();
                             const uint32_t c = lane < int(X5_W) ? __popc(SB[b][lane]) : 0u;
                             const uint32_t e2 = dpp_incl_scan(c) - c;
@@ -1725,7 +1781,8 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                 REC[b][2] = b_tot;
                 REC[b][3] = b_s0;
             }
-            X5T(3);   // descriptors, token-start words
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // far-copy slots landed in LDS
+            X5T(3);   // descriptors, token-start words, far-copy loads landed
             k_m2 = k_m1;
             k_m1 = kind;
             ops_m1 = b_op;
@@ -1736,61 +1793,74 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
             const uint32_t s0 = __builtin_amdgcn_readfirstlane(REC[pb][1]);
             const uint32_t btot = __builtin_amdgcn_readfirstlane(REC[pb][2]);
             if (kind == R5_NORMAL) {
+                // 256-byte windows from the aligned base Sb = s0 & ~3, four consecutive bytes a lane; the
+                // al = s0 & 3 bytes before s0 belong to the previous batch (read, never written)
+                const uint32_t al = s0 & 3u;
+                const uint32_t Sb = s0 - al;
+                const uint32_t btS = btot + al;
                 const uint32_t* sbw = SB[pb];
                 const uint32_t* wpw = WP[pb];
-                const uint32_t* d0w = D0[pb];
-                const uint32_t* d1w = D1[pb];
-                for (uint32_t w0 = 0; w0 < btot; w0 += 256) {
-                    const uint32_t s1 = s0 + w0;
-                    uint32_t W[4], xw[4], ti[4], i0[4], i1[4], addr[4];
-                    bool act[4], pend[4];
+                const uint32_t* Dp = D[pb];
+                for (uint32_t w0 = 0; w0 < btS; w0 += 256) {
+                    const uint32_t x0 = w0 + 4u * uint32_t(lane);
+                    const uint32_t ws = w0 == 0 ? al : w0;   // sources at or past ws are resolved in the window
+                    const uint32_t wd = x0 >> 5, sh = x0 & 31u;
+                    const uint32_t sbv = sbw[wd];
+                    const uint32_t t0 = wpw[wd] + __popc(sbv & ((2u << sh) - 1u));   // entry of byte x0
+                    const uint32_t nb = sbv >> sh;
+                    uint32_t tk[4];
+                    tk[0] = t0;
+                    tk[1] = t0 + ((nb >> 1) & 1u);
+                    tk[2] = tk[1] + ((nb >> 2) & 1u);
+                    tk[3] = tk[2] + ((nb >> 3) & 1u);
+                    uint32_t d0[4], d1[4];
                     #pragma unroll
                     for (int u = 0; u < 4; u++) {
-                        const uint32_t x = w0 + 64u * uint32_t(u) + uint32_t(lane);
-                        act[u] = x < btot;
-                        xw[u] = act[u] ? x : btot - 1u;
+                        d0[u] = Dp[tk[u]];
+                        d1[u] = Dp[tk[u] + X5_DS];
                     }
+                    uint32_t addr[4], pw[4];
+                    bool pend[4];
                     #pragma unroll
                     for (int u = 0; u < 4; u++) {
-                        const uint32_t wd = xw[u] >> 5;
-                        ti[u] = wpw[wd] + __popc(sbw[wd] & ((2u << (xw[u] & 31u)) - 1u)) - 1u;
+                        const uint32_t x = x0 + uint32_t(u);
+                        const uint32_t jj = x - (d0[u] & 0x7fffu);
+                        const bool cp = (d0[u] & X5_CP) != 0u;
+                        const uint32_t q = uint32_t((float(jj) + 0.5f) * __uint_as_float(d1[u]));
+                        const uint32_t y = x - (d0[u] >> 16) * (q + 1u);   // a copy's source (from Sb; may wrap)
+                        pend[u] = cp && int32_t(y) >= int32_t(ws);
+                        addr[u] = cp ? ((Sb + y) & XRMASK) : (d1[u] + x);
+                        pw[u] = 0x8000u | ((y - w0) << 1);
                     }
-                    #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        i0[u] = d0w[ti[u]];
-                        i1[u] = d1w[ti[u]];
-                    }
-                    #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t jj = xw[u] - (i0[u] & 0x7ffu);
-                        const bool copy = ((i0[u] >> 11) & 1u) == X2_COPY;
-                        const uint32_t offv = max(i0[u] >> 16, 1u);
-                        const uint32_t r = (i0[u] & (1u << 12)) ? mod_small(jj & 63u, offv) : jj;
-                        const uint32_t y = i1[u] + r;                 // copy: absolute output position of the source byte
-                        pend[u] = act[u] && copy && y >= s1;          // produced in this window
-                        addr[u] = copy ? (y & XRMASK) : (i1[u] + jj);
-                        W[u] = 0x100u | ((y - s1) & 0xffu);
-                    }
-                    // the four source reads issued together (every addr is inside L): left to itself the
-                    // compiler sank each read into its lane's branch with a wait of its own
+                    // the four source reads issued together (every addr is inside the workgroup's LDS)
                     uint32_t vv[4];
                     #pragma unroll
                     for (int u = 0; u < 4; u++) vv[u] = uint32_t(L[addr[u]]);
                     asm volatile("" : "+v"(vv[0]), "+v"(vv[1]), "+v"(vv[2]), "+v"(vv[3]));
-                    #pragma unroll
-                    for (int u = 0; u < 4; u++) W[u] = pend[u] ? W[u] : (act[u] ? vv[u] : 0u);
-                    while (__any(((W[0] | W[1] | W[2] | W[3]) & 0x100u) != 0u)) {
-                        #pragma unroll
-                        for (int u = 0; u < 4; u++) jv[64u * uint32_t(u) + uint32_t(lane)] = uint16_t(W[u]);
-                        uint32_t G[4];
-                        #pragma unroll
-                        for (int u = 0; u < 4; u++) G[u] = jv[W[u] & 0xffu];
-                        #pragma unroll
-                        for (int u = 0; u < 4; u++) W[u] = (W[u] & 0x100u) ? G[u] : W[u];
+                    // jump words, two per dword: (value << 1), or 0x8000 | (window position << 1) while pending
+                    uint32_t Wa = (pend[0] ? pw[0] : (vv[0] << 1)) | ((pend[1] ? pw[1] : (vv[1] << 1)) << 16);
+                    uint32_t Wb = (pend[2] ? pw[2] : (vv[2] << 1)) | ((pend[3] ? pw[3] : (vv[3] << 1)) << 16);
+                    while (__any(((Wa | Wb) & 0x80008000u) != 0u)) {
+                        *reinterpret_cast<uint2*>(jvb + 8u * uint32_t(lane)) = make_uint2(Wa, Wb);
+                        const uint32_t g0 = *reinterpret_cast<const uint16_t*>(jvb + (Wa & 0x1feu));
+                        const uint32_t g1 = *reinterpret_cast<const uint16_t*>(jvb + ((Wa >> 16) & 0x1feu));
+                        const uint32_t g2 = *reinterpret_cast<const uint16_t*>(jvb + (Wb & 0x1feu));
+                        const uint32_t g3 = *reinterpret_cast<const uint16_t*>(jvb + ((Wb >> 16) & 0x1feu));
+                        const uint32_t ga = __builtin_amdgcn_perm(g1, g0, 0x05040100u), gb = __builtin_amdgcn_perm(g3, g2, 0x05040100u);
+                        Wa = x5_pick(Wa, ga);
+                        Wb = x5_pick(Wb, gb);
                     }
-                    #pragma unroll
-                    for (int u = 0; u < 4; u++)
-                        if (act[u]) ring[(s1 + 64u * uint32_t(u) + uint32_t(lane)) & XRMASK] = uint8_t(W[u]);
+                    const uint32_t o4 = __builtin_amdgcn_perm(Wb >> 1, Wa >> 1, 0x06040200u);
+                    if (x0 < btS) {
+                        const uint32_t ra = (Sb + x0) & XRMASK;
+                        if (x0 >= al) {   // (a dword past the batch end writes <= 3 bytes the next batch rewrites)
+                            *reinterpret_cast<uint32_t*>(ring + ra) = o4;
+                        } else {          // the batch's first dword: only bytes from s0 on
+                            #pragma unroll
+                            for (uint32_t u = 1; u < 4; u++)
+                                if (u >= al) ring[ra + u] = uint8_t(o4 >> (8u * u));
+                        }
+                    }
                 }
                 X5T(6);   // windows
                 flush_slots(ring, od, F, s0 + btot, lane);
@@ -1799,21 +1869,22 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                 asm volatile("s_waitcnt vmcnt(1)" ::: "memory");   // all but the newest store have landed
                 X5T(8);   // store drain
             } else if (kind == R5_LONG) {
+                // bytes [s0, s0 + btot) = input [sl, sl + btot): whole 16-byte ring blocks from 16-byte loads,
+                // the partial first / last block byte by byte
                 const uint32_t sl = __builtin_amdgcn_readfirstlane(REC[pb][3]);
-                for (uint32_t d0 = 0; d0 < btot; d0 += XLIT) {
-                    const uint32_t c = min(btot - d0, XLIT);
-                    const uint32_t b0 = uint32_t(lane) * 16u;
-                    if (b0 < c) {
-                        uint8_t by[16];
-                        #pragma unroll
-                        for (int u = 0; u < 16; u++) by[u] = b0 + u < c ? gin[sl + d0 + b0 + u] : uint8_t(0);
-                        #pragma unroll
-                        for (int u = 0; u < 16; u++)
-                            if (b0 + u < c) ring[(s0 + d0 + b0 + u) & XRMASK] = by[u];
+                const uint32_t e = s0 + btot;
+                for (uint32_t base = s0 & ~15u; base < e; base += XLIT) {
+                    const uint32_t p = base + 16u * uint32_t(lane);   // this lane's block
+                    if (p < e) {
+                        if (p >= s0 && p + 16u <= e) {
+                            *reinterpret_cast<u32x4*>(ring + (p & XRMASK)) = x5_load16(gin, sl + (p - s0));
+                        } else {
+                            for (uint32_t q = max(p, s0); q < min(p + 16u, e); q++) ring[q & XRMASK] = gin[sl + (q - s0)];
+                        }
                     }
-                    flush_slots(ring, od, F, s0 + d0 + c, lane);
+                    flush_slots(ring, od, F, min(base + XLIT, e), lane);
                 }
-                cop = s0 + btot;
+                cop = e;
                 wait_vmem();
             } else {
                 wait_vmem();

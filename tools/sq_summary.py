@@ -16,4 +16,6 @@ for k, c in sorted(acc.items()):
     print(f"{k:22s} dispatches={len(disp[k])} waves/dispatch={w / len(disp[k]):.0f} cycles/wave={cyc / w:.0f} "
           f"parked={c['SQ_WAIT_ANY'] / max(cyc, 1):.2f} stall={c['SQ_WAIT_INST_ANY'] / max(cyc, 1):.2f} "
           f"active={c['SQ_ACTIVE_INST_ANY'] / max(cyc, 1):.2f} valu={c['SQ_INSTS_VALU'] / w:.0f} "
-          f"lds={c['SQ_INSTS_LDS'] / w:.0f} salu={c['SQ_INSTS_SALU'] / w:.0f}")
+          f"lds={c['SQ_INSTS_LDS'] / w:.0f} salu={c['SQ_INSTS_SALU'] / w:.0f} "
+          f"| per dispatch: valu={c['SQ_INSTS_VALU'] / len(disp[k]) / 1e6:.2f}M lds={c['SQ_INSTS_LDS'] / len(disp[k]) / 1e6:.2f}M "
+          f"salu={c['SQ_INSTS_SALU'] / len(disp[k]) / 1e6:.2f}M")
