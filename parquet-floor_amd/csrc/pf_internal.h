@@ -32,6 +32,7 @@ struct PfOpts {
     int force_redo = 0;       // PF_DEBUG_FORCE_REDO=k: every k-th Snappy job rejected by the block executor
     bool exec_stream = false; // PF_EXEC_STREAM=1: the executor on a low-priority stream of its own
     bool zc = true;           // PF_ZC=0: SDMA copies for the batch tables instead of k_copy_words
+    bool dl_kernel = true;    // PF_DL_KERNEL=0: pf_copy_batch_async by SDMA copies instead of k_download
     bool debug_plan = false;  // PF_DEBUG_PLAN=1: host planning phase times on stderr
     int64_t nest_seg = 0;     // PF_NEST_SEG=n: nested segment length, forced (0: default, not forced)
     bool nest_seg_set = false;

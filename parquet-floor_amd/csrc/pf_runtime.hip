@@ -126,6 +126,32 @@ inline void copy_words(void* d0, const void* s0, size_t b0, void* d1, const void
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// A decoded batch into pinned host memory by a kernel writing through the pages' device address
+// (round 6): the SDMA engines move one direction at a time on this link -- an SDMA H2D and an SDMA D2H
+// together make 57 GB/s, an SDMA H2D beside this kernel's D2H 86 GB/s (profiles/r06_e2e/duplex.txt) --
+// so the next batch's H2D (pf_decode_row_group's SDMA copy) runs under this batch's download. Up to
+// three ranges (the output arenas), 16-byte chunks grid-stride, the ranges' last < 16 bytes by block 0.
+struct DlRange {
+    uint8_t* d;
+    const uint8_t* s;
+    uint64_t n;
+};
+__global__ __launch_bounds__(256) void k_download(DlRange r0, DlRange r1, DlRange r2) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const uint64_t c0 = r0.n >> 4, c1 = r1.n >> 4, c2 = r2.n >> 4;
+    const uint64_t stride = uint64_t(gridDim.x) * 256u;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x; i < c0 + c1 + c2; i += stride) {
+        const DlRange& r = i < c0 ? r0 : (i < c0 + c1 ? r1 : r2);
+        const uint64_t j = i < c0 ? i : (i < c0 + c1 ? i - c0 : i - c0 - c1);
+        reinterpret_cast<u4*>(r.d)[j] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(r.s) + j);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 48) {
+        const DlRange& r = threadIdx.x < 16 ? r0 : (threadIdx.x < 32 ? r1 : r2);
+        const uint64_t b = (r.n & ~uint64_t(15)) + (threadIdx.x & 15u);
+        if (b < r.n) r.d[b] = r.s[b];
+    }
+}
+
 constexpr int N_EVENTS = 11;  // h2d, snappy parse, snappy exec, dict, delta, levels, count, scan, flat, decode
 constexpr uint32_t BA_TILE_BYTES = 8192;   // pf_pages.hip BA_TILE
 constexpr int64_t FLAT_BLK = 4096;         // pf_pages.hip FBLK   // h2d, snappy, dict, delta, count, scan, flat, decode
@@ -870,6 +896,7 @@ void opts_from_env(pf::PfOpts& o) {
     o.force_redo = num("PF_DEBUG_FORCE_REDO", o.force_redo);
     o.exec_stream = on("PF_EXEC_STREAM", o.exec_stream);
     o.zc = on("PF_ZC", o.zc);
+    o.dl_kernel = on("PF_DL_KERNEL", o.dl_kernel);
     o.debug_plan = on("PF_DEBUG_PLAN", o.debug_plan);
     if (const char* e = std::getenv("PF_NEST_SEG")) {
         o.nest_seg = std::atoll(e);
@@ -1690,9 +1717,26 @@ int pf_copy_batch_async(pf_ctx* ctx, void* host, size_t cap) {
     if (b.total > cap) return fail(ctx, PF_ERR_CAPACITY, "batch buffer too small (pf_batch_bytes)");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     uint8_t* h = static_cast<uint8_t*>(host);
-    if (b.out) HIPCHK(ctx, hipMemcpyAsync(h, ctx->d_out.p, b.out, hipMemcpyDeviceToHost, ctx->stream));
-    if (b.bits) HIPCHK(ctx, hipMemcpyAsync(h + b.bits_off, ctx->d_bits.p, b.bits, hipMemcpyDeviceToHost, ctx->stream));
-    if (b.chars) HIPCHK(ctx, hipMemcpyAsync(h + b.chars_off, ctx->d_chars.p, b.chars, hipMemcpyDeviceToHost, ctx->stream));
+    // pinned pages with a device address: k_download; otherwise (or PF_DL_KERNEL=0) SDMA copies
+    void* hd = nullptr;
+    if (ctx->opts.dl_kernel && (b.out || b.bits || b.chars)) {
+        if (hipHostGetDevicePointer(&hd, host, 0) != hipSuccess || !hd || (reinterpret_cast<uintptr_t>(hd) & 15u) != 0) {
+            (void)hipGetLastError();   // (not a mapped pinned buffer: the copy path)
+            hd = nullptr;
+        }
+    }
+    if (hd) {
+        uint8_t* hdev = static_cast<uint8_t*>(hd);
+        const DlRange r0{hdev, static_cast<const uint8_t*>(ctx->d_out.p), b.out};
+        const DlRange r1{hdev + b.bits_off, static_cast<const uint8_t*>(ctx->d_bits.p), b.bits};
+        const DlRange r2{hdev + b.chars_off, static_cast<const uint8_t*>(ctx->d_chars.p), b.chars};
+        hipLaunchKernelGGL(k_download, dim3(256), dim3(256), 0, ctx->stream, r0, r1, r2);
+        HIPCHK(ctx, hipGetLastError());
+    } else {
+        if (b.out) HIPCHK(ctx, hipMemcpyAsync(h, ctx->d_out.p, b.out, hipMemcpyDeviceToHost, ctx->stream));
+        if (b.bits) HIPCHK(ctx, hipMemcpyAsync(h + b.bits_off, ctx->d_bits.p, b.bits, hipMemcpyDeviceToHost, ctx->stream));
+        if (b.chars) HIPCHK(ctx, hipMemcpyAsync(h + b.chars_off, ctx->d_chars.p, b.chars, hipMemcpyDeviceToHost, ctx->stream));
+    }
     HIPCHK(ctx, hipEventRecord(ctx->ev_copy, ctx->stream));
     ctx->copies_pending = true;
     return PF_OK;

@@ -1040,7 +1040,7 @@ constexpr uint32_t XSTAGE = XCHUNK + 64 + 16;
 constexpr uint32_t XLIT = 1024;      // long literals are copied in pieces of this many bytes
 constexpr uint32_t FBUF_W = 17;      // dwords per far copy's source slot (64 bytes + misalignment)
 #ifndef PF_XFAR
-#define PF_XFAR 16
+#define PF_XFAR 24
 #endif
 constexpr uint32_t XFAR = PF_XFAR;   // far copies per step (the step is cut before the next one)
 
@@ -1485,7 +1485,11 @@ constexpr uint32_t X5_LDS = X5_FBUF0 + 2u * X5_FSL;
 constexpr uint32_t X5_W = 768u / 32u;                  // token-start words of a batch (+ its alignment bytes)
 constexpr uint32_t X5_LINE = 128u;                     // a far source's cache line must be wholly landed
 constexpr uint32_t X5_FREAD = 5u * 16u;                // bytes a far load reads from its 16-byte aligned base
-constexpr uint32_t X5_DS = 65u;                        // descriptor table: entry t at [t], its second word at [t + X5_DS]
+#ifndef PF_X5_TPL
+#define PF_X5_TPL 2
+#endif
+constexpr int X5_TPL = PF_X5_TPL;                      // tokens a producer lane decodes per batch
+constexpr uint32_t X5_DS = 64u * X5_TPL + 1u;          // descriptor table: entry t at [t], its second word at [t + X5_DS]
 static_assert(X5_BATCH + 3u <= 768u, "a batch and its alignment bytes are at most three 256-byte windows");
 static_assert((X5_FBUF0 & 15u) == 0u && (X5_FSLOT & 15u) == 0u, "far slots are 16-byte aligned");
 enum : uint32_t { R5_NORMAL = 0, R5_LONG = 1, R5_NOP = 2, R5_END = 3, R5_BAD = 4 };
@@ -1660,47 +1664,75 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
             }
             X5T(0);   // chunk staging + token enumeration
             if (ok) {
+                // X5_TPL tokens a lane: token sb + 64 h + lane in half h (batches of up to 64 X5_TPL tokens)
                 const uint8_t* stg = L + X5_STAGE0 + cb * X5_STG;
-                const uint32_t t = sb + uint32_t(lane);
-                const bool v = t < T;
-                const uint32_t pos = v ? uint32_t(tokpos[t]) : 0u;
-                const SnapTok tk = snap_tok(lds_read8(stg, woff + pos));
-                const uint32_t ol = v ? tk.ol : 0u;
-                const uint32_t start = I + pos;
-                const uint32_t endp = tk.tl > uint64_t(0xffffffffu - start) ? 0xffffffffu : start + uint32_t(tk.tl);
-                const uint32_t prev = dpp_prev(endp);
-                const uint32_t inc = dpp_incl_scan(ol);
-                const uint32_t otok = op + inc - ol;
-                const bool take = v && otok < out_end;
-                const int nt = __popcll(__ballot(take));
-                const bool wrong = take && ((lane == 0 ? start != ip : start != prev) || endp > n || op + inc > out_end ||
-                                            inc < ol);
+                uint32_t pos[X5_TPL], ol[X5_TPL], start[X5_TPL], endp[X5_TPL], inc[X5_TPL], otok[X5_TPL];
+                bool v[X5_TPL], take[X5_TPL];
+                SnapTok tk[X5_TPL];
+                #pragma unroll
+                for (int h = 0; h < X5_TPL; h++) {
+                    const uint32_t t = sb + 64u * uint32_t(h) + uint32_t(lane);
+                    v[h] = t < T;
+                    pos[h] = v[h] ? uint32_t(tokpos[t]) : 0u;
+                }
+                #pragma unroll
+                for (int h = 0; h < X5_TPL; h++) tk[h] = snap_tok(lds_read8(stg, woff + pos[h]));
+                int nt = 0;
+                bool wrong = false;
+                uint32_t prevlast = ip, incbase = 0;
+                #pragma unroll
+                for (int h = 0; h < X5_TPL; h++) {
+                    ol[h] = v[h] ? tk[h].ol : 0u;
+                    start[h] = I + pos[h];
+                    endp[h] = tk[h].tl > uint64_t(0xffffffffu - start[h]) ? 0xffffffffu : start[h] + uint32_t(tk[h].tl);
+                    const uint32_t pdpp = dpp_prev(endp[h]);   // (every lane runs the DPP move)
+                    const uint32_t prev = lane == 0 ? prevlast : pdpp;
+                    inc[h] = incbase + dpp_incl_scan(ol[h]);
+                    otok[h] = op + inc[h] - ol[h];
+                    take[h] = v[h] && otok[h] < out_end;
+                    nt += __popcll(__ballot(take[h]));
+                    wrong = wrong || (take[h] && (start[h] != prev || endp[h] > n || op + inc[h] > out_end || inc[h] < ol[h] ||
+                                                  inc[h] < incbase));
+                    prevlast = __builtin_amdgcn_readlane(endp[h], 63);
+                    incbase = __builtin_amdgcn_readlane(inc[h], 63);
+                }
                 if (__any(wrong) || nt == 0) {
                     ok = false;
                 } else {
-                    const uint32_t kd = tk.kind;
-                    const uint32_t off = tk.arg;
-                    const uint32_t srcv = start + tk.arg;   // literal data position
-                    const bool lstaged = srcv + ol <= I + XCHUNK + 64;
-                    const uint32_t a = otok - off;          // copy source start
-                    const bool farc = take && kd != 0 && a + min(ol, off) <= op &&
-                                      int32_t(a - (op + X5_BATCH - XRING)) < 0;
-                    // source not yet landed in HBM: every cache line its 80-byte aligned read touches must be
-                    const bool fnr = farc && a + X5_FREAD + X5_LINE > LF;
-                    const unsigned long long farm = __ballot(farc);
-                    const uint32_t frank = uint32_t(__popcll(farm & lane_mask_lt(uint32_t(lane))));
-                    const unsigned long long cutm =
-                        __ballot(take && (ol > 64u || inc > X5_BATCH || (kd == 0 && !lstaged) || (farc && frank >= XFAR) || fnr));
-                    const uint32_t cut = cutm ? uint32_t(__ffsll(cutm) - 1) : uint32_t(nt);
+                    uint32_t kd[X5_TPL], off[X5_TPL], srcv[X5_TPL], a[X5_TPL], frank[X5_TPL];
+                    bool farc[X5_TPL], fnr[X5_TPL], lstaged[X5_TPL];
+                    unsigned long long farm[X5_TPL], cutm[X5_TPL];
+                    uint32_t fbase = 0;
+                    #pragma unroll
+                    for (int h = 0; h < X5_TPL; h++) {
+                        kd[h] = tk[h].kind;
+                        off[h] = tk[h].arg;
+                        srcv[h] = start[h] + tk[h].arg;   // literal data position
+                        lstaged[h] = srcv[h] + ol[h] <= I + XCHUNK + 64;
+                        a[h] = otok[h] - off[h];          // copy source start
+                        farc[h] = take[h] && kd[h] != 0 && a[h] + min(ol[h], off[h]) <= op &&
+                                  int32_t(a[h] - (op + X5_BATCH - XRING)) < 0;
+                        // source not yet landed in HBM: every cache line its 80-byte aligned read touches must be
+                        fnr[h] = farc[h] && a[h] + X5_FREAD + X5_LINE > LF;
+                        farm[h] = __ballot(farc[h]);
+                        frank[h] = fbase + uint32_t(__popcll(farm[h] & lane_mask_lt(uint32_t(lane))));
+                        fbase += uint32_t(__popcll(farm[h]));
+                        cutm[h] = __ballot(take[h] && (ol[h] > 64u || inc[h] > X5_BATCH || (kd[h] == 0 && !lstaged[h]) ||
+                                                       (farc[h] && frank[h] >= XFAR) || fnr[h]));
+                    }
+                    uint32_t cut = uint32_t(nt);
+                    #pragma unroll
+                    for (int h = X5_TPL - 1; h >= 0; h--)
+                        if (cutm[h]) cut = 64u * uint32_t(h) + uint32_t(__ffsll(cutm[h]) - 1);
                     uint32_t used = 0;
                     if (cut == 0) {
-                        if (__builtin_amdgcn_readfirstlane(kd) == 0) {   // one long literal: the consumer copies it
+                        if (__builtin_amdgcn_readfirstlane(kd[0]) == 0) {   // one long literal: the consumer copies it
                             kind = R5_LONG;
-                            b_tot = __builtin_amdgcn_readfirstlane(ol);
-                            b_s0 = __builtin_amdgcn_readfirstlane(srcv);
+                            b_tot = __builtin_amdgcn_readfirstlane(ol[0]);
+                            b_s0 = __builtin_amdgcn_readfirstlane(srcv[0]);
                             used = 1;
                             nops = 0;
-                        } else if (__builtin_amdgcn_readfirstlane(uint32_t(fnr)) && nops < 3) {
+                        } else if (__builtin_amdgcn_readfirstlane(uint32_t(fnr[0])) && nops < 3) {
                             kind = R5_NOP;   // wait one batch for the source's stores to land
                             nops++;
                         } else {
@@ -1708,28 +1740,43 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                         }
                     } else {
                         used = cut;
-                        const uint32_t btot = __builtin_amdgcn_readlane(inc, cut - 1);
-                        const bool inb = take && uint32_t(lane) < cut;
-                        const bool lit = inb && kd == 0;
-                        const bool cp = inb && kd != 0;
-                        const bool far = cp && farc;
-                        if (__any(cp && (off == 0 || off > otok - out_start))) ok = false;
-                        // a far source straddling the direct split (level bytes | values) is not one window
-                        if (od.dd != nullptr && __any(far && a < od.dlo && a + ol > od.dlo)) ok = false;
+                        const uint32_t ch = (cut - 1u) >> 6;   // the half holding the batch's last token
+                        uint32_t btot = 0;
+                        #pragma unroll
+                        for (int h = 0; h < X5_TPL; h++)
+                            if (ch == uint32_t(h)) btot = __builtin_amdgcn_readlane(inc[h], (cut - 1u) & 63u);
+                        bool inb[X5_TPL], lit[X5_TPL], cp[X5_TPL], far[X5_TPL];
+                        bool bad = false;
+                        #pragma unroll
+                        for (int h = 0; h < X5_TPL; h++) {
+                            inb[h] = take[h] && 64u * uint32_t(h) + uint32_t(lane) < cut;
+                            lit[h] = inb[h] && kd[h] == 0;
+                            cp[h] = inb[h] && kd[h] != 0;
+                            far[h] = cp[h] && farc[h];
+                            bad = bad || (cp[h] && (off[h] == 0 || off[h] > otok[h] - out_start));
+                            // a far source straddling the direct split (level bytes | values) is not one window
+                            bad = bad || (od.dd != nullptr && far[h] && a[h] < od.dlo && a[h] + ol[h] > od.dlo);
+                        }
+                        if (__any(bad)) ok = false;
                         X5T(1);   // token decode, chain checks, cuts
                         if (ok) {
-                            const PF_GLOBAL uint8_t* fb0 = od.dd != nullptr && a >= od.dlo ? od.dd + a : gdst + a;
-                            const uint32_t fsh = uint32_t(reinterpret_cast<uintptr_t>(fb0) & 15u);
+                            uint32_t fsh[X5_TPL];
+                            uint32_t nfar = 0;
+                            uint64_t* fa = reinterpret_cast<uint64_t*>(L + X5_FBUF0 + b * X5_FSL);   // (overwritten by the loads)
+                            #pragma unroll
+                            for (int h = 0; h < X5_TPL; h++) {
+                                const PF_GLOBAL uint8_t* fb0 = od.dd != nullptr && a[h] >= od.dlo ? od.dd + a[h] : gdst + a[h];
+                                fsh[h] = uint32_t(reinterpret_cast<uintptr_t>(fb0) & 15u);
+                                if (far[h]) fa[frank[h]] = reinterpret_cast<uintptr_t>(fb0) & ~uintptr_t(15);
+                                nfar += uint32_t(__popcll(farm[h] & lane_mask_lt(cut > 64u * uint32_t(h) ? cut - 64u * uint32_t(h) : 0u)));
+                            }
                             // far-copy sources: five aligned 16-byte chunks each (the arenas keep >= 80 bytes of
                             // slack), loaded straight into the slots by LDS-DMA -- lane l loads chunk l % 5 of far
                             // copy l / 5, so the lane-linear destination is the slot layout -- and waited for only
                             // before the barrier, after the descriptors (no data registers, latency behind them)
-                            const uint32_t nfar = uint32_t(__popcll(farm & lane_mask_lt(cut)));
                             if (nfar) {
-                                uint64_t* fa = reinterpret_cast<uint64_t*>(L + X5_FBUF0 + b * X5_FSL);   // (overwritten by the loads)
-                                if (far) fa[frank] = reinterpret_cast<uintptr_t>(fb0) & ~uintptr_t(15);
                                 x5_order();
-                                const uint32_t l0 = uint32_t(lane), f0 = (l0 * 205u) >> 10;   // l / 5 for l < 80
+                                const uint32_t l0 = uint32_t(lane), f0 = (l0 * 205u) >> 10;   // l / 5 for l < 128
                                 const uint64_t s0a = fa[f0] + 16u * (l0 - 5u * f0);
                                 uint64_t s1a = 0;
                                 if (nfar > 12u) {
@@ -1744,20 +1791,23 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                                                                      (__attribute__((address_space(3))) void*)(slots + 1024), 16, 0, 0);
                             }
                             X5T(2);   // far-copy source loads (issued)
-                            const uint32_t relS = otok - (op & ~3u);   // from the batch's aligned base
-                            uint32_t d0 = 0, d1 = 0;
-                            if (inb) {
-                                const bool near = cp && !far;
-                                d0 = relS | (near ? (X5_CP | (off << 16)) : 0u);
-                                d1 = near ? __float_as_uint(__builtin_amdgcn_rcpf(float(off)))
-                                          : (lit ? X5_STAGE0 + cb * X5_STG + woff + (srcv - I) - relS
-                                                 : X5_FBUF0 + b * X5_FSL + frank * X5_FSLOT + fsh - relS);
-                            }
-                            D[b][1 + lane] = d0;
-                            D[b][1 + X5_DS + lane] = d1;
                             if (lane < int(X5_W)) SB[b][lane] = 0;
-                            x5_order();
-                            if (inb) atomicOr(&SB[b][relS >> 5], 1u << (relS & 31u));
+                            #pragma unroll
+                            for (int h = 0; h < X5_TPL; h++) {
+                                const uint32_t relS = otok[h] - (op & ~3u);   // from the batch's aligned base
+                                uint32_t d0 = 0, d1 = 0;
+                                if (inb[h]) {
+                                    const bool near = cp[h] && !far[h];
+                                    d0 = relS | (near ? (X5_CP | (off[h] << 16)) : 0u);
+                                    d1 = near ? __float_as_uint(__builtin_amdgcn_rcpf(float(off[h])))
+                                              : (lit[h] ? X5_STAGE0 + cb * X5_STG + woff + (srcv[h] - I) - relS
+                                                        : X5_FBUF0 + b * X5_FSL + frank[h] * X5_FSLOT + fsh[h] - relS);
+                                }
+                                D[b][1 + 64 * h + lane] = d0;
+                                D[b][1 + X5_DS + 64 * h + lane] = d1;
+                                x5_order();
+                                if (inb[h]) atomicOr(&SB[b][relS >> 5], 1u << (relS & 31u));
+                            }
                             x5_order();
                             const uint32_t c = lane < int(X5_W) ? __popc(SB[b][lane]) : 0u;
                             const uint32_t e2 = dpp_incl_scan(c) - c;
@@ -1769,7 +1819,10 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                     }
                     if (ok && used) {
                         op += b_tot;
-                        ip = __builtin_amdgcn_readlane(endp, int(used) - 1);
+                        const uint32_t uh = (used - 1u) >> 6;
+                        #pragma unroll
+                        for (int h = 0; h < X5_TPL; h++)
+                            if (uh == uint32_t(h)) ip = __builtin_amdgcn_readlane(endp[h], (used - 1u) & 63u);
                         sb += used;
                     }
                 }
