@@ -91,6 +91,7 @@ STAGE_BYTES_DEF = {
 }
 ROOF_PASSES = 3         # isolated decodes of context 0's first batch for the roofline kernel time
 E2E_PASSES = 2
+E2E_STREAM_PASSES = 6   # E2E streamed: the file decoded this many times back to back (a reader over several files)
 METRIC = "decoded GB/s + rows/s (node), lineitem-shape Snappy+dict, 1/2/4/8 GPUs"
 
 WORKLOADS = {
@@ -723,6 +724,12 @@ def main():
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-write", action="store_true", help="skip the write-path leg")
     ap.add_argument("--e2e-split", type=int, default=1, help="E2E: batches per row group (column subsets)")
+    ap.add_argument("--e2e-streams", type=int, default=2,
+                    help="E2E: decode streams (each with its twin context and the library's copy stream: the "
+                         "box has 4 hardware queues)")
+    ap.add_argument("--e2e-last", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--e2e-rg-batch", type=int, default=0,
+                    help="E2E: row groups per decode batch (batches alternate between a stream's twin contexts)")
     ap.add_argument("--e2e-copy", choices=("batch", "chunks"), default="batch",
                     help="E2E D2H: one copy per output arena (batch) or per chunk array (chunks)")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -886,14 +893,18 @@ def main():
             # kernels and a third's D2H overlap; the link is full duplex). Measured: 37-39 GB/s with
             # this plan, 35 with one row group per batch, 26 with the column split.
             e2e_plan, _, _ = units_for_rank(argparse.Namespace(**{**vars(args), "split": "rowgroups"}), pf, world, rank,
-                                            args.streams)
+                                            min(args.e2e_streams, len(decs)), batch=args.e2e_rg_batch)
             if args.e2e_split > 1:   # each row group's columns in e2e_split batches (earlier first D2H)
                 k = args.e2e_split
                 e2e_plan = [[[(g, p, cs[i::k]) for g, p, cs in units] for units in bl for i in range(k)]
                             for bl in e2e_plan]
             e2e_batches = [[BatchInput(pf, units, decs[0].h) for units in bl] for bl in e2e_plan]
-            e2e = measure_e2e(decs[:len(e2e_batches)], e2e_batches, pf, st_all, args.e2e_copy,
-                              barrier=dist.barrier if dist else None)
+            # --e2e-last: the last contexts instead of the first (analysis: which hardware queues the library's
+            # copy streams share with the decode streams)
+            ke = len(e2e_batches)
+            sel = slice(-ke, None) if args.e2e_last else slice(0, ke)
+            e2e = measure_e2e(decs[sel], e2e_batches, pf, st_all, args.e2e_copy,
+                              barrier=dist.barrier if dist else None, twins=twins[sel])
             for bl in e2e_batches:
                 for bi in bl:
                     bi.host.free()
@@ -1089,7 +1100,7 @@ def measure_write(path, pf, dec, passes=3, decs=None):
             "passes": passes}
 
 
-def measure_e2e(decs, batches, pf, st_all, copy_mode="batch", barrier=None):
+def measure_e2e(decs, batches, pf, st_all, copy_mode="batch", barrier=None, twins=None):
     """Whole rank share, E2E_PASSES times: per context, per batch: pinned H2D of the batch's chunk
     bytes (inside pf_decode_row_group), decode, pf_wait, then the D2H of the decoded columns into
     pinned host memory — copy_mode "batch": pf_copy_batch_async, one copy per output arena (3 per
@@ -1112,7 +1123,7 @@ def measure_e2e(decs, batches, pf, st_all, copy_mode="batch", barrier=None):
             row.append(infos)
         layouts.append(row)
     if copy_mode == "batch":
-        return _e2e_batch(decs, batches, layouts, pf, barrier)
+        return _e2e_batch(decs, batches, layouts, pf, barrier, twins)
     # pinned output buffers: one per context, sized for its largest batch
     outs = []
     for ctx_i, (d, bl) in enumerate(zip(decs, batches)):
@@ -1221,8 +1232,10 @@ def measure_link(nbytes, reps=3):
         return {"error": repr(e)}
 
 
-def _e2e_batch(decs, batches, layouts, pf, barrier=None):
-    """measure_e2e with pf_copy_batch_async: one pinned buffer per context (its largest batch).
+def _e2e_batch(decs, batches, layouts, pf, barrier=None, twins=None):
+    """measure_e2e with pf_copy_batch_async: per stream, batches alternate between the context and its
+    twin (own arenas, own pinned output buffer sized for the stream's largest batch), so batch j's
+    download (the library's copy stream) runs under batch j + 1's H2D and kernels.
     barrier (N > 1): aligns the ranks' timed passes, so the node rate is sum(bytes) / max(time)."""
     from pfloor import _native
     from pfloor.decoder import PinnedBuffer
@@ -1243,24 +1256,26 @@ def _e2e_batch(decs, batches, layouts, pf, barrier=None):
             _native.check(L.pf_batch_bytes(d.h, C.byref(n)), d.h, "pf_batch_bytes")
             need = max(need, n.value)
             copied += n.value
-        bufs.append(PinnedBuffer(d.h, max(need, 1)))
+        bufs.append([PinnedBuffer(d.h, max(need, 1)) for _ in range(2 if twins else 1)])
     h2d_per_pass = sum(bi.nbytes for bl in batches for bi in bl)
     errs = []
 
-    def worker(ci, d, bl):
+    def worker(ci, d, bl, passes=1):
         try:
-            buf = bufs[ci]
-            for bi in bl:
-                d.decode(bi.descs, bi.host.ptr.value, bi.nbytes, on_device=False)
-                if d.wait() != 0 and not _SKIP:
-                    raise RuntimeError(d.error())
-                _native.check(L.pf_copy_batch_async(d.h, buf.ptr, buf.nbytes), d.h, "pf_copy_batch_async")
-            _native.check(L.pf_sync(d.h), d.h, "pf_sync")
+            pair = (d, twins[ci]) if twins else (d,)
+            for j, bi in enumerate(list(bl) * passes):
+                dj, buf = pair[j % len(pair)], bufs[ci][j % len(pair)]
+                dj.decode(bi.descs, bi.host.ptr.value, bi.nbytes, on_device=False)
+                if dj.wait() != 0 and not _SKIP:
+                    raise RuntimeError(dj.error())
+                _native.check(L.pf_copy_batch_async(dj.h, buf.ptr, buf.nbytes), dj.h, "pf_copy_batch_async")
+            for dj in pair:
+                _native.check(L.pf_sync(dj.h), dj.h, "pf_sync")
         except Exception as e:
             errs.append(e)
 
-    def one_pass():
-        ts = [threading.Thread(target=worker, args=(i, d, bl)) for i, (d, bl) in enumerate(zip(decs, batches))]
+    def one_pass(passes=1):
+        ts = [threading.Thread(target=worker, args=(i, d, bl, passes)) for i, (d, bl) in enumerate(zip(decs, batches))]
         [t.start() for t in ts]
         [t.join() for t in ts]
         if errs:
@@ -1273,17 +1288,29 @@ def _e2e_batch(decs, batches, layouts, pf, barrier=None):
         one_pass()
     if barrier:
         barrier()
-    dt = (time.perf_counter() - t0) / E2E_PASSES
-    for b in bufs:
-        b.free()
+    dt_file = (time.perf_counter() - t0) / E2E_PASSES
+    # streamed: the passes back to back in each stream's worker (no join between files), so one file's
+    # first H2D and decode run under the previous file's last downloads
+    t0 = time.perf_counter()
+    one_pass(E2E_STREAM_PASSES)
+    if barrier:
+        barrier()
+    dt = (time.perf_counter() - t0) / E2E_STREAM_PASSES
+    for bb in bufs:
+        for b in bb:
+            b.free()
     t_link = max(h2d_per_pass, copied) / (PCIE_GBS * 1e9)
     link = measure_link(copied)
     return {"value": round(d2h_arrays / dt / 1e9, 3), "unit": "decoded GB/s (pinned host in -> host columns out)",
             "link_measured": link, "frac_of_measured_d2h": round(copied / link["d2h_gbs"] / 1e9 / dt, 4) if "d2h_gbs" in link else None,
-            "ms_per_pass": round(dt * 1e3, 3), "h2d_bytes": h2d_per_pass, "d2h_bytes": copied,
+            "ms_per_pass": round(dt * 1e3, 3), "streamed_passes": E2E_STREAM_PASSES,
+            "file": {"ms_per_pass": round(dt_file * 1e3, 3), "value": round(d2h_arrays / dt_file / 1e9, 3),
+                     "what": "one file per pass, the streams joined at its end (pipeline fill and drain in every pass)"},
+            "h2d_bytes": h2d_per_pass, "d2h_bytes": copied,
             "decoded_bytes": d2h_arrays, "pcie_bound_gbs": PCIE_GBS, "frac": round(t_link / dt, 4),
             "frac_definition": "max(H2D, D2H bytes) / 63 GB/s divided by the measured pass time",
-            "passes": E2E_PASSES, "d2h_copies": "one per output arena per batch (pf_copy_batch_async)"}
+            "passes": E2E_PASSES, "streams": len(decs), "twins": bool(twins),
+            "d2h_copies": "one per batch (pf_copy_batch_async: k_download writes the pinned pages on the library's copy stream)"}
 
 
 if __name__ == "__main__":

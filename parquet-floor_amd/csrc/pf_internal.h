@@ -33,6 +33,8 @@ struct PfOpts {
     bool exec_stream = false; // PF_EXEC_STREAM=1: the executor on a low-priority stream of its own
     bool zc = true;           // PF_ZC=0: SDMA copies for the batch tables instead of k_copy_words
     bool dl_kernel = true;    // PF_DL_KERNEL=0: pf_copy_batch_async by SDMA copies instead of k_download
+    bool h2d_kernel = false;  // PF_H2D_KERNEL=1: pinned chunk bytes to the device by a kernel instead of SDMA (E2E: no gain, r06)
+    bool dl_stream = true;    // PF_DL_STREAM=0: pf_copy_batch_async on the decode stream instead of the copy stream
     bool debug_plan = false;  // PF_DEBUG_PLAN=1: host planning phase times on stderr
     int64_t nest_seg = 0;     // PF_NEST_SEG=n: nested segment length, forced (0: default, not forced)
     bool nest_seg_set = false;

@@ -164,8 +164,13 @@ struct Streams {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t exec_stream = nullptr;
+    // pf_copy_batch_async's downloads (made on first use): the next batch's H2D and kernels on `stream`
+    // (a twin context's, with its own arenas) run while this batch's columns go to the host
+    hipStream_t copy_stream = nullptr;
+    std::mutex mu;
     ~Streams() {
         (void)hipSetDevice(device);
+        if (copy_stream) { (void)hipStreamSynchronize(copy_stream); (void)hipStreamDestroy(copy_stream); }
         if (exec_stream) { (void)hipStreamSynchronize(exec_stream); (void)hipStreamDestroy(exec_stream); }
         if (stream) { (void)hipStreamSynchronize(stream); (void)hipStreamDestroy(stream); }
     }
@@ -188,7 +193,8 @@ struct pf_ctx {
     hipEvent_t ev_done = nullptr;
     // recorded after the last enqueued D2H copy of this context's outputs: pf_copy_column / pf_sync
     // wait for it, not for the stream, so a peer's decode queued behind the copies keeps running
-    hipEvent_t ev_copy = nullptr;
+    hipEvent_t ev_copy = nullptr;          // after this context's last async copy (on whichever stream)
+    hipEvent_t ev_dl = nullptr;            // the decode a download on the copy stream follows
     bool timing = true;                    // per-stage events (pf_last_timing); pf_ctx_set_timing
     std::string err;
     DevBuf d_in, d_scratch, d_out, d_bits, d_chars, d_meta, d_tokmap;
@@ -585,7 +591,7 @@ extern "C" int pf_snappy_compress(pf_ctx* ctx, const uint8_t* src, size_t n, uin
     if (ctx->pending) return fail(ctx, PF_ERR_STATE, "previous decode not waited for");
     if (n > 0xffffffffull) return fail(ctx, PF_ERR_INVALID_ARG, "snappy: buffer too large");
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    if (ctx->copies_pending) HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->copies_pending) HIPCHK(ctx, hipEventSynchronize(ctx->ev_copy));
     ctx->copies_pending = false;
     HIPCHK(ctx, ctx->d_enc.ensure(std::max<size_t>(n, 1)));
     if (n) HIPCHK(ctx, hipMemcpyAsync(ctx->d_enc.p, src, n, hipMemcpyHostToDevice, ctx->stream));
@@ -620,7 +626,7 @@ extern "C" int pf_encode_chunk(pf_ctx* ctx, const pf_encode_column* col, int on_
     const int64_t dict_limit = std::min<int64_t>(col->dict_page_limit > 0 ? col->dict_page_limit : (1 << 20), 0x7fffffff);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    if (ctx->copies_pending) HIPCHK(ctx, hipStreamSynchronize(st));
+    if (ctx->copies_pending) HIPCHK(ctx, hipEventSynchronize(ctx->ev_copy));
     ctx->copies_pending = false;
 
     // host copies of validity / offsets (page plan, definition levels)
@@ -897,6 +903,8 @@ void opts_from_env(pf::PfOpts& o) {
     o.exec_stream = on("PF_EXEC_STREAM", o.exec_stream);
     o.zc = on("PF_ZC", o.zc);
     o.dl_kernel = on("PF_DL_KERNEL", o.dl_kernel);
+    o.dl_stream = on("PF_DL_STREAM", o.dl_stream);
+    o.h2d_kernel = on("PF_H2D_KERNEL", o.h2d_kernel);
     o.debug_plan = on("PF_DEBUG_PLAN", o.debug_plan);
     if (const char* e = std::getenv("PF_NEST_SEG")) {
         o.nest_seg = std::atoll(e);
@@ -938,6 +946,7 @@ int ctx_init(pf_ctx* ctx, pf_ctx* peer) {
     }
     HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
     HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
+    HIPCHK(nullptr, hipEventCreateWithFlags(&ctx->ev_dl, hipEventDisableTiming));
     for (auto& e : ctx->ev) HIPCHK(nullptr, hipEventCreate(&e));
     return PF_OK;
 }
@@ -985,6 +994,7 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);   // this context's work and any peer's ahead of it
     if (ctx->exec_stream) (void)hipStreamSynchronize(ctx->exec_stream);
+    if (ctx->copies_pending) (void)hipEventSynchronize(ctx->ev_copy);   // (a download on the copy stream)
     for (DevBuf* b : {&ctx->d_in, &ctx->d_scratch, &ctx->d_out, &ctx->d_bits, &ctx->d_chars, &ctx->d_meta, &ctx->d_tokmap,
                       &ctx->d_scan_in, &ctx->d_scan, &ctx->d_enc, &ctx->d_enc_sec, &ctx->d_enc_out})
         b->release();
@@ -996,6 +1006,7 @@ int pf_ctx_destroy(pf_ctx* ctx) {
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
     if (ctx->ev_copy) (void)hipEventDestroy(ctx->ev_copy);
+    if (ctx->ev_dl) (void)hipEventDestroy(ctx->ev_dl);
     ctx->streams.reset();   // destroys the stream(s) when no other context shares them
     delete ctx;
     return PF_OK;
@@ -1076,7 +1087,19 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     const uint8_t* d_bytes = bytes;
     if (!bytes_on_device && n_bytes) {
         HIPCHK(ctx, ctx->d_in.ensure(n_bytes));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, bytes, n_bytes, hipMemcpyHostToDevice, st));
+        // pinned pages with a 16-byte aligned device address: read by a kernel (k_download's loop), so the
+        // link runs both ways at once beside the downloads (an SDMA H2D waited behind them, r06 trace)
+        void* hd = nullptr;
+        if (ctx->opts.h2d_kernel && hipHostGetDevicePointer(&hd, const_cast<uint8_t*>(bytes), 0) == hipSuccess && hd &&
+            (reinterpret_cast<uintptr_t>(hd) & 15u) == 0) {
+            const DlRange r0{static_cast<uint8_t*>(ctx->d_in.p), static_cast<const uint8_t*>(hd), uint64_t(n_bytes)};
+            const DlRange rz{nullptr, nullptr, 0};
+            hipLaunchKernelGGL(k_download, dim3(256), dim3(256), 0, st, r0, rz, rz);
+            HIPCHK(ctx, hipGetLastError());
+        } else {
+            (void)hipGetLastError();
+            HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, bytes, n_bytes, hipMemcpyHostToDevice, st));
+        }
         d_bytes = static_cast<const uint8_t*>(ctx->d_in.p);
     }
     ctx->d_bytes = d_bytes;
@@ -1271,8 +1294,12 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     mark();
     // ---- allocate arenas ----
     size_t chars_cap = std::max<size_t>(size_t(2 * chars_hint) + (16u << 20), ctx->chars_need);
-    if (ctx->copies_pending && (out > ctx->d_out.cap || bits > ctx->d_bits.cap || chars_cap > ctx->d_chars.cap))
-        HIPCHK(ctx, hipStreamSynchronize(st));   // a growing output arena must not be freed under a pending D2H copy
+    if (ctx->copies_pending) {
+        if (out > ctx->d_out.cap || bits > ctx->d_bits.cap || chars_cap > ctx->d_chars.cap)
+            HIPCHK(ctx, hipEventSynchronize(ctx->ev_copy));   // a growing output arena must not be freed under a pending D2H copy
+        else
+            HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_copy, 0));   // (a download on the copy stream reads the arenas)
+    }
     ctx->copies_pending = false;
     ctx->npub_bytes = size_t(nest_pub);
     ctx->off_npub = take(scratch, ctx->npub_bytes, 256);
@@ -1725,19 +1752,29 @@ int pf_copy_batch_async(pf_ctx* ctx, void* host, size_t cap) {
             hd = nullptr;
         }
     }
+    hipStream_t cs = ctx->stream;
+    if (ctx->opts.dl_stream) {   // the download on the copy stream, after this context's decode
+        {
+            std::lock_guard<std::mutex> lk(ctx->streams->mu);
+            if (!ctx->streams->copy_stream) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->streams->copy_stream, hipStreamNonBlocking));
+        }
+        cs = ctx->streams->copy_stream;
+        HIPCHK(ctx, hipEventRecord(ctx->ev_dl, ctx->stream));
+        HIPCHK(ctx, hipStreamWaitEvent(cs, ctx->ev_dl, 0));
+    }
     if (hd) {
         uint8_t* hdev = static_cast<uint8_t*>(hd);
         const DlRange r0{hdev, static_cast<const uint8_t*>(ctx->d_out.p), b.out};
         const DlRange r1{hdev + b.bits_off, static_cast<const uint8_t*>(ctx->d_bits.p), b.bits};
         const DlRange r2{hdev + b.chars_off, static_cast<const uint8_t*>(ctx->d_chars.p), b.chars};
-        hipLaunchKernelGGL(k_download, dim3(256), dim3(256), 0, ctx->stream, r0, r1, r2);
+        hipLaunchKernelGGL(k_download, dim3(256), dim3(256), 0, cs, r0, r1, r2);
         HIPCHK(ctx, hipGetLastError());
     } else {
-        if (b.out) HIPCHK(ctx, hipMemcpyAsync(h, ctx->d_out.p, b.out, hipMemcpyDeviceToHost, ctx->stream));
-        if (b.bits) HIPCHK(ctx, hipMemcpyAsync(h + b.bits_off, ctx->d_bits.p, b.bits, hipMemcpyDeviceToHost, ctx->stream));
-        if (b.chars) HIPCHK(ctx, hipMemcpyAsync(h + b.chars_off, ctx->d_chars.p, b.chars, hipMemcpyDeviceToHost, ctx->stream));
+        if (b.out) HIPCHK(ctx, hipMemcpyAsync(h, ctx->d_out.p, b.out, hipMemcpyDeviceToHost, cs));
+        if (b.bits) HIPCHK(ctx, hipMemcpyAsync(h + b.bits_off, ctx->d_bits.p, b.bits, hipMemcpyDeviceToHost, cs));
+        if (b.chars) HIPCHK(ctx, hipMemcpyAsync(h + b.chars_off, ctx->d_chars.p, b.chars, hipMemcpyDeviceToHost, cs));
     }
-    HIPCHK(ctx, hipEventRecord(ctx->ev_copy, ctx->stream));
+    HIPCHK(ctx, hipEventRecord(ctx->ev_copy, cs));
     ctx->copies_pending = true;
     return PF_OK;
 }
@@ -1797,7 +1834,7 @@ int pf_snappy_decompress(pf_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     if (n > 0xffffffffull || ulen > 0xffffffffull) return fail(ctx, PF_ERR_INVALID_ARG, "snappy: buffer too large");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    if (ctx->copies_pending) HIPCHK(ctx, hipStreamSynchronize(st));   // arenas may be reallocated below
+    if (ctx->copies_pending) HIPCHK(ctx, hipEventSynchronize(ctx->ev_copy));   // arenas may be reallocated below
     ctx->copies_pending = false;
     ctx->n_chunks = 0;
     ctx->info.clear();
@@ -1865,7 +1902,7 @@ int pf_scan_pages(pf_ctx* ctx, const pf_scan_chunk* chunks, int n_chunks, const 
     if (slots > (int64_t(1) << 30)) return fail(ctx, PF_ERR_INVALID_ARG, "scan: too many page slots");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    if (ctx->copies_pending) HIPCHK(ctx, hipStreamSynchronize(st));
+    if (ctx->copies_pending) HIPCHK(ctx, hipEventSynchronize(ctx->ev_copy));
     ctx->copies_pending = false;
     const uint8_t* d_bytes = bytes;
     if (!bytes_on_device && n_bytes) {
