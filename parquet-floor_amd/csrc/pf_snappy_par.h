@@ -72,6 +72,35 @@ __device__ __forceinline__ SnapTok snap_tok(uint64_t v) {
     return t;
 }
 
+// 32-bit form for the executor's producer (round 6): straight-line selects (the 64-bit form compiles to
+// branches on the token kind), tl saturated at 0xffffffff (a 4 GiB literal), from the 8 stream bytes
+// lo | hi << 32 starting at the tag.
+struct SnapTok32 {
+    uint32_t tl, ol, kind, arg;
+};
+__device__ __forceinline__ SnapTok32 snap_tok32(uint32_t lo, uint32_t hi) {
+    const uint32_t tag = lo & 0xffu, kind = tag & 3u, L = tag >> 2;
+    const uint32_t b1 = __builtin_amdgcn_alignbyte(hi, lo, 1u);       // the 4 bytes after the tag
+    const uint32_t nb = L >= 60u ? L - 59u : 0u;                      // literal length bytes (1..4)
+    const uint32_t lmask = nb >= 4u ? 0xffffffffu : ~(0xffffffffu << (8u * nb));
+    const uint32_t lit_ol = (L < 60u ? L : (b1 & lmask)) + 1u;        // 0: a 4 GiB literal
+    const uint32_t lit_tl = lit_ol == 0u ? 0xffffffffu : __builtin_elementwise_add_sat(1u + nb, lit_ol);
+    const uint32_t cp_ol = kind == 1u ? 4u + (L & 7u) : L + 1u;
+    const uint32_t sh = (0x00101800u >> (8u * kind)) & 0xffu;         // offset bytes: kind 1 -> 1, 2 -> 2, 3 -> 4
+    const uint32_t cp_off = (b1 & (0xffffffffu >> sh)) | (kind == 1u ? ((tag >> 5) << 8) : 0u);
+    const uint32_t cp_tl = (0x05030200u >> (8u * kind)) & 0xffu;
+    const bool lit = kind == 0u;
+    return SnapTok32{lit ? lit_tl : cp_tl, lit ? lit_ol : cp_ol, kind, lit ? 1u + nb : cp_off};
+}
+
+// 8 bytes from LDS at byte offset a as two dwords, branch-free (three aligned dword reads; a + 8 + 3 staged).
+__device__ __forceinline__ void lds_read8_2(const uint8_t* s, uint32_t a, uint32_t& lo, uint32_t& hi) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(s + (a & ~3u));
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = a & 3u;
+    lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+}
+
 // Token lengths from the tag byte alone (literals with a length field, tag_long, need snap_tok).
 __device__ __forceinline__ uint32_t tag_tl(uint32_t tag) {   // input bytes (branch-free)
     const uint32_t kind = tag & 3u;

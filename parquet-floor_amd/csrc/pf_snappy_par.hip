@@ -1665,18 +1665,23 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
             X5T(0);   // chunk staging + token enumeration
             if (ok) {
                 // X5_TPL tokens a lane: token sb + 64 h + lane in half h (batches of up to 64 X5_TPL tokens)
-                const uint8_t* stg = L + X5_STAGE0 + cb * X5_STG;
+                const uint32_t stg_off = __builtin_amdgcn_readfirstlane(cb) ? X5_STAGE0 + X5_STG : X5_STAGE0;
+                const uint8_t* stg = L + stg_off;
                 uint32_t pos[X5_TPL], ol[X5_TPL], start[X5_TPL], endp[X5_TPL], inc[X5_TPL], otok[X5_TPL];
                 bool v[X5_TPL], take[X5_TPL];
-                SnapTok tk[X5_TPL];
+                SnapTok32 tk[X5_TPL];
                 #pragma unroll
                 for (int h = 0; h < X5_TPL; h++) {
                     const uint32_t t = sb + 64u * uint32_t(h) + uint32_t(lane);
                     v[h] = t < T;
-                    pos[h] = v[h] ? uint32_t(tokpos[t]) : 0u;
+                    pos[h] = uint32_t(tokpos[min(t, XCHUNK / 2u - 1u)]);   // (read unconditionally; v gates the use)
+                    if (!v[h]) pos[h] = 0u;
                 }
+                uint32_t tlo[X5_TPL], thi[X5_TPL];
                 #pragma unroll
-                for (int h = 0; h < X5_TPL; h++) tk[h] = snap_tok(lds_read8(stg, woff + pos[h]));
+                for (int h = 0; h < X5_TPL; h++) lds_read8_2(stg, woff + pos[h], tlo[h], thi[h]);
+                #pragma unroll
+                for (int h = 0; h < X5_TPL; h++) tk[h] = snap_tok32(tlo[h], thi[h]);
                 int nt = 0;
                 bool wrong = false;
                 uint32_t prevlast = ip, incbase = 0;
@@ -1684,7 +1689,7 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                 for (int h = 0; h < X5_TPL; h++) {
                     ol[h] = v[h] ? tk[h].ol : 0u;
                     start[h] = I + pos[h];
-                    endp[h] = tk[h].tl > uint64_t(0xffffffffu - start[h]) ? 0xffffffffu : start[h] + uint32_t(tk[h].tl);
+                    endp[h] = __builtin_elementwise_add_sat(start[h], tk[h].tl);
                     const uint32_t pdpp = dpp_prev(endp[h]);   // (every lane runs the DPP move)
                     const uint32_t prev = lane == 0 ? prevlast : pdpp;
                     inc[h] = incbase + dpp_incl_scan(ol[h]);
@@ -1800,7 +1805,7 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                                     const bool near = cp[h] && !far[h];
                                     d0 = relS | (near ? (X5_CP | (off[h] << 16)) : 0u);
                                     d1 = near ? __float_as_uint(__builtin_amdgcn_rcpf(float(off[h])))
-                                              : (lit[h] ? X5_STAGE0 + cb * X5_STG + woff + (srcv[h] - I) - relS
+                                              : (lit[h] ? stg_off + woff + (srcv[h] - I) - relS
                                                         : X5_FBUF0 + b * X5_FSL + frank[h] * X5_FSLOT + fsh[h] - relS);
                                 }
                                 D[b][1 + 64 * h + lane] = d0;
