@@ -1494,12 +1494,13 @@ static_assert(X5_BATCH + 3u <= 768u, "a batch and its alignment bytes are at mos
 static_assert((X5_FBUF0 & 15u) == 0u && (X5_FSLOT & 15u) == 0u, "far slots are 16-byte aligned");
 enum : uint32_t { R5_NORMAL = 0, R5_LONG = 1, R5_NOP = 2, R5_END = 3, R5_BAD = 4 };
 // Descriptor word 0: the token's first output byte relative to the batch's 4-byte aligned base S
-// (bits 0-14), bit 15 a copy whose source is read through the ring / the window, bits 16-31 its offset.
-// Word 1: a literal or far copy: the LDS address of its byte at base position x is word1 + x; a ring
-// copy: rcp(offset) as a float (byte x's source is x - offset * (1 + floor((x - start) / offset)), the
-// same byte an overlapping copy reads as (x - start) mod offset). Entry 0 is a dummy literal for the
-// batch's alignment bytes (token t of the batch is entry t + 1).
-constexpr uint32_t X5_CP = 0x8000u;
+// (bits 0-15); a copy whose source is read through the ring / the window: its offset (< 4 KiB) in bits
+// 16-30 and bit 31 set. Word 1: a literal or far copy: the LDS address of its byte at base position x is
+// word1 + x; a ring copy: m = floor(65536 / offset) + 1 (or one more), so that (j * m) >> 16 =
+// floor(j / offset) for the byte's index j < 64 in the token: byte x's source is
+// x - offset * (1 + floor(j / offset)), the byte an overlapping copy reads as j mod offset. Entry 0 is a
+// dummy literal for the batch's alignment bytes (token t of the batch is entry t + 1).
+constexpr uint32_t X5_CP = 0x80000000u;
 
 // Workgroup barrier for LDS hand-over only (no wait on outstanding global stores).
 __device__ __forceinline__ void x5_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -1804,7 +1805,7 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                                 if (inb[h]) {
                                     const bool near = cp[h] && !far[h];
                                     d0 = relS | (near ? (X5_CP | (off[h] << 16)) : 0u);
-                                    d1 = near ? __float_as_uint(__builtin_amdgcn_rcpf(float(off[h])))
+                                    d1 = near ? uint32_t(65536.0f * __builtin_amdgcn_rcpf(float(off[h]))) + 1u
                                               : (lit[h] ? stg_off + woff + (srcv[h] - I) - relS
                                                         : X5_FBUF0 + b * X5_FSL + frank[h] * X5_FSLOT + fsh[h] - relS);
                                 }
@@ -1882,13 +1883,17 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                     #pragma unroll
                     for (int u = 0; u < 4; u++) {
                         const uint32_t x = x0 + uint32_t(u);
-                        const uint32_t jj = x - (d0[u] & 0x7fffu);
-                        const bool cp = (d0[u] & X5_CP) != 0u;
-                        const uint32_t q = uint32_t((float(jj) + 0.5f) * __uint_as_float(d1[u]));
-                        const uint32_t y = x - (d0[u] >> 16) * (q + 1u);   // a copy's source (from Sb; may wrap)
+                        const uint32_t jj = x - (d0[u] & 0xffffu);
+                        const bool cp = int32_t(d0[u]) < 0;
+                        const uint32_t q = __umul24(jj, d1[u]) >> 16;        // floor(jj / offset) (copies)
+                        const uint32_t of = (d0[u] >> 16) & 0x7fffu;
+                        uint32_t t;   // of * q + of, kept a 24-bit multiply (the compiler folds it into v_mad_u64_u32)
+                        asm("v_mad_u32_u24 %0, %1, %2, %1" : "=v"(t) : "v"(of), "v"(q));
+                        const uint32_t y = x - t;                            // a copy's source (from Sb; may wrap)
                         pend[u] = cp && int32_t(y) >= int32_t(ws);
                         addr[u] = cp ? ((Sb + y) & XRMASK) : (d1[u] + x);
-                        pw[u] = 0x8000u | ((y - w0) << 1);
+                        // (bits above the window's 8 stay in the word: the rounds mask the address with 0x1fe)
+                        pw[u] = 0x8000u | (y << 1);
                     }
                     // the four source reads issued together (every addr is inside the workgroup's LDS)
                     uint32_t vv[4];
