@@ -1492,6 +1492,7 @@ constexpr int X5_TPL = PF_X5_TPL;                      // tokens a producer lane
 constexpr uint32_t X5_DS = 64u * X5_TPL + 1u;          // descriptor table: entry t at [t], its second word at [t + X5_DS]
 static_assert(X5_BATCH + 3u <= 768u, "a batch and its alignment bytes are at most three 256-byte windows");
 static_assert((X5_FBUF0 & 15u) == 0u && (X5_FSLOT & 15u) == 0u, "far slots are 16-byte aligned");
+static_assert(5u * XFAR <= 128u, "a batch's far-copy chunks are loaded by two LDS-DMA wave instructions");
 enum : uint32_t { R5_NORMAL = 0, R5_LONG = 1, R5_NOP = 2, R5_END = 3, R5_BAD = 4 };
 // Descriptor word 0: the token's first output byte relative to the batch's 4-byte aligned base S
 // (bits 0-15); a copy whose source is read through the ring / the window: its offset (< 4 KiB) in bits
