@@ -142,30 +142,41 @@ __device__ __forceinline__ uint64_t stage_tok(const uint8_t* stage, uint32_t a, 
     return t.tl;
 }
 
-// Walk the chain from c while positions stay below re (bits relative to rs).
+// Walk the chain from c while positions stay below re (bits relative to rs). The token-start bits are
+// OR-ed into the lane's four LDS words lb (one ds_or per token, no register selects; round 6) and read
+// back into L at the end.
 __device__ void lane_walk(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t rs, uint32_t re,
-                          uint32_t c, WinLane& L) {
-    // token-start bits in two 64-bit halves (one shift and one select per token instead of four)
-    uint64_t lo = 0, hi = 0;
-    uint32_t out = 0;
+                          uint32_t c, WinLane& L, uint32_t* lb) {
+    *reinterpret_cast<uint4*>(lb) = make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t n32 = uint32_t(n);   // (< 2^32 - 1: 0xffffffff marks a broken chain)
+    const uint32_t base = woff - W0;    // stage offset of stream position p: base + p
+    uint32_t out = 0, p = c;
     L.c = c;
-    uint64_t p = c;
-    bool bad = false;
     while (p < re) {
-        uint32_t ol;
-        const uint64_t tl = stage_tok(stage, woff + uint32_t(p - W0), ol);
-        const uint32_t i = uint32_t(p) - rs;
-        const uint64_t m = 1ull << (i & 63u);
-        lo |= i < 64 ? m : 0ull;
-        hi |= i < 64 ? 0ull : m;
-        const uint32_t o = out + ol;
-        out = o < out ? 0xffffffffu : o;
-        p += tl;
-        if (p > n) { bad = true; break; }
+        // the tag and the 3 bytes after it from one aligned dword pair; straight-line token lengths (a
+        // literal length field of 4 bytes, >= 16 MiB, cannot be in a page: it breaks the chain)
+        const uint32_t a = base + p;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(stage + (a & ~3u));
+        const uint32_t v = __builtin_amdgcn_alignbyte(w[1], w[0], a & 3u);
+        const uint32_t tag = v & 0xffu, kind = tag & 3u, Lv = tag >> 2;
+        const uint32_t nb = Lv >= 60u ? Lv - 59u : 0u;
+        const uint32_t lit_ol = (Lv < 60u ? Lv : ((v >> 8) & ((1u << (8u * min(nb, 3u))) - 1u))) + 1u;
+        const uint32_t lit_tl = nb >= 4u ? 0xffffffffu : 1u + nb + lit_ol;
+        // (selects as bit masks: v_bfi, where the compiler would branch on the kind)
+        const uint32_t mlit = 0u - uint32_t(kind == 0u), m1 = 0u - uint32_t(kind == 1u);
+        const uint32_t cp_ol = ((4u + (Lv & 7u)) & m1) | ((Lv + 1u) & ~m1);
+        const uint32_t tl = (lit_tl & mlit) | (((0x05030200u >> (8u * kind)) & 0xffu) & ~mlit);
+        const uint32_t ol = (lit_ol & mlit) | (cp_ol & ~mlit);
+        const uint32_t i = p - rs;
+        atomicOr(lb + (i >> 5), 1u << (i & 31u));
+        out = __builtin_elementwise_add_sat(out, ol);
+        const uint32_t np = __builtin_elementwise_add_sat(p, tl);
+        p = np > n32 ? 0xffffffffu : np;
     }
-    L.b0 = uint32_t(lo); L.b1 = uint32_t(lo >> 32); L.b2 = uint32_t(hi); L.b3 = uint32_t(hi >> 32);
+    const uint4 bv = *reinterpret_cast<const uint4*>(lb);
+    L.b0 = bv.x; L.b1 = bv.y; L.b2 = bv.z; L.b3 = bv.w;
     L.out = out;
-    L.x = bad ? SNAP_INVALID : uint32_t(p);
+    L.x = p;   // (SNAP_INVALID when the chain ran past the stream end)
 }
 
 // Speculative parse of one window whose chain enters at `entry` (W0 <= entry < min(W0 + SNAP_WIN,
@@ -176,8 +187,9 @@ __device__ void lane_walk(const uint8_t* stage, uint32_t woff, uint32_t W0, uint
 // lane). Returns the window exit; flags = WIN_BROKEN if the chain runs past the stream end,
 // WIN_NOCONV if max_rounds did not converge.
 __device__ uint32_t win_parse_spec(const uint8_t* stage, uint32_t woff, uint32_t W0, uint64_t n, uint32_t entry,
-                                   WinLane& L, uint32_t& flags, int max_rounds = WIN_ROUNDS) {
+                                   WinLane& L, uint32_t& flags, uint32_t* lbits, int max_rounds = WIN_ROUNDS) {
     const int lane = threadIdx.x & 63;
+    uint32_t* const lb = lbits + 4 * lane;   // the lane's bit words (SNAP_WWORDS words of LDS for the wave)
     const uint32_t rs = W0 + uint32_t(lane) * SNAP_RB;
     const uint32_t re = uint32_t(min(uint64_t(rs) + SNAP_RB, n));
     entry = __builtin_amdgcn_readfirstlane(entry);
@@ -186,7 +198,7 @@ __device__ uint32_t win_parse_spec(const uint8_t* stage, uint32_t woff, uint32_t
     L.out = 0;
     L.c = rs;
     L.x = SNAP_INVALID;
-    if (uint32_t(lane) >= L0 && uint64_t(rs) < n) lane_walk(stage, woff, W0, n, rs, re, uint32_t(lane) == L0 ? entry : rs, L);
+    if (uint32_t(lane) >= L0 && uint64_t(rs) < n) lane_walk(stage, woff, W0, n, rs, re, uint32_t(lane) == L0 ? entry : rs, L, lb);
     uint32_t ent = SNAP_INVALID, X = SNAP_INVALID;
     bool converged = false;
     flags = 0;
@@ -218,7 +230,7 @@ __device__ uint32_t win_parse_spec(const uint8_t* stage, uint32_t woff, uint32_t
 #else
         (void)__ballot(need);
 #endif
-        if (need) lane_walk(stage, woff, W0, n, rs, re, ent, L);
+        if (need) lane_walk(stage, woff, W0, n, rs, re, ent, L, lb);
     }
     if (!converged) flags = WIN_NOCONV;
     // lanes off the chain hold no tokens; drop the guessed prefix before a lane's true entry
@@ -557,7 +569,7 @@ __global__ __launch_bounds__(64) void k_snappy_index(const SnappyJob* __restrict
     const uint32_t woff = snap_stage(stage, job.src, n, W0, SNAP_WSTAGE, lane);
     __syncthreads();
     uint32_t flags;
-    uint32_t X = win_parse_spec(stage, woff, W0, n, entry, L, flags);
+    uint32_t X = win_parse_spec(stage, woff, W0, n, entry, L, flags, sbits);
 #ifdef PF_STAMPS
     { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (lane == 0) { CSTAMP(0, 1); CSTAMP(1, t_ - it0); if (flags & WIN_NOCONV) CSTAMP(2, 1); } it0 = t_; }
 #endif
