@@ -1562,6 +1562,25 @@ __device__ __forceinline__ u32x4 x5_load16(const PF_GLOBAL uint8_t* gin, uint32_
     return r;
 }
 
+// One input chunk [I - woff, I - woff + XSTAGE) as lane l's 16-byte chunks l and 64 + l (lanes < 5), and its
+// token-start bits (16 input bytes a lane): every load issued before any is used. Chunks wholly at or past n
+// read as zero (the chunk holding the last byte is read whole, as snap_stage does).
+static_assert(XSTAGE == 64u * 16u + 5u * 16u, "a staged chunk is 64 + 5 lane loads");
+__device__ __forceinline__ void x5_chunk_load(const PF_GLOBAL uint8_t* gin, const PF_GLOBAL uint16_t* tm16, uint64_t n, uint32_t I,
+                                              int lane, u32x4& va, u32x4& vb, uint32_t& bits) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(gin + I);
+    const uint32_t woff = uint32_t(a & 15u);
+    const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(a - woff);
+    const int64_t first = int64_t(I) - int64_t(woff);
+    va = u32x4{0u, 0u, 0u, 0u};
+    vb = u32x4{0u, 0u, 0u, 0u};
+    bits = 0u;
+    if (first + 16 * int64_t(lane) < int64_t(n)) va = src[lane];
+    if (lane < 5 && first + 16 * int64_t(64 + lane) < int64_t(n)) vb = src[64 + lane];
+    const uint32_t p16 = I + 16u * uint32_t(lane);
+    if (uint64_t(p16) < n) bits = uint32_t(tm16[p16 >> 4]);
+}
+
 // One piece (mode 0: pieces[item]) or one whole-page redo (mode 1: job item) by the workgroup's two waves.
 __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
                                             const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode, int item) {
@@ -1628,6 +1647,8 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
     // producer state
     uint32_t op = out_start, sb = 0, T = 0, I = 0, woff = 0, cb = 1;
     uint32_t ops_m1 = out_start, k_m1 = R5_NOP, k_m2 = R5_NOP, nops = 0;
+    uint32_t pfI = ~0u, pfbits = 0;   // prefetched input chunk (base, token-start bits, data)
+    u32x4 pfa = {0u, 0u, 0u, 0u}, pfb = {0u, 0u, 0u, 0u};
     // consumer state
     uint32_t F = out_start, cop = out_start;
     uint32_t last = R5_END;
@@ -1657,9 +1678,27 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                 } else {
                     I = ip & ~15u;
                     cb ^= 1u;
-                    woff = snap_stage(L + X5_STAGE0 + cb * X5_STG, in, n, I, XSTAGE, lane);
+                    // the chunk from the registers when the last staging prefetched it (the next chunk starts
+                    // where the last token of this one ends: past I + XCHUNK, in the same 16 bytes unless that
+                    // token is a literal)
+                    u32x4 va, vb;
+                    uint32_t bits;
+                    if (I == pfI) {
+                        va = pfa;
+                        vb = pfb;
+                        bits = pfbits;
+                    } else {
+                        x5_chunk_load(gin, tm16, n, I, lane, va, vb, bits);
+                    }
+                    u32x4* stq = reinterpret_cast<u32x4*>(L + X5_STAGE0 + cb * X5_STG);
+                    stq[lane] = va;
+                    if (lane < 5) stq[64 + lane] = vb;
+                    woff = uint32_t(reinterpret_cast<uintptr_t>(gin + I) & 15u);
+                    // prefetch the next chunk: its loads land while this chunk's batches are decoded
+                    pfI = I + XCHUNK;
+                    if (uint64_t(pfI) < n) x5_chunk_load(gin, tm16, n, pfI, lane, pfa, pfb, pfbits);
+                    else pfI = ~0u;
                     const uint32_t p16 = I + 16u * uint32_t(lane);
-                    uint32_t bits = uint64_t(p16) < n ? uint32_t(tm16[p16 >> 4]) : 0u;
                     if (p16 + 16u <= ip) bits = 0;
                     else if (p16 < ip) bits &= ~((1u << (ip - p16)) - 1u);
                     const uint32_t cnt = __popc(bits);
