@@ -1492,8 +1492,7 @@ constexpr uint32_t X5_STG = (XSTAGE + 15u) & ~15u;     // one staged input chunk
 constexpr uint32_t X5_FSLOT = 80u;                     // a far copy's source: 5 aligned 16-byte chunks (<= 64 B + shift < 16)
 constexpr uint32_t X5_FSL = XFAR * X5_FSLOT;           // far-copy source slots of one batch
 constexpr uint32_t X5_STAGE0 = XRING;                  // [ring | stage x2 | far slots x2]: one byte address
-constexpr uint32_t X5_FBUF0 = XRING + 2u * X5_STG;     // selects any byte source
-constexpr uint32_t X5_LDS = X5_FBUF0 + 2u * X5_FSL;
+constexpr uint32_t X5_LDS = XRING + 2u * X5_STG;       // selects any byte source (the far slots: their own array)
 constexpr uint32_t X5_W = 768u / 32u;                  // token-start words of a batch (+ its alignment bytes)
 constexpr uint32_t X5_LINE = 128u;                     // a far source's cache line must be wholly landed
 constexpr uint32_t X5_FREAD = 5u * 16u;                // bytes a far load reads from its 16-byte aligned base
@@ -1503,7 +1502,7 @@ constexpr uint32_t X5_FREAD = 5u * 16u;                // bytes a far load reads
 constexpr int X5_TPL = PF_X5_TPL;                      // tokens a producer lane decodes per batch
 constexpr uint32_t X5_DS = 64u * X5_TPL + 1u;          // descriptor table: entry t at [t], its second word at [t + X5_DS]
 static_assert(X5_BATCH + 3u <= 768u, "a batch and its alignment bytes are at most three 256-byte windows");
-static_assert((X5_FBUF0 & 15u) == 0u && (X5_FSLOT & 15u) == 0u, "far slots are 16-byte aligned");
+static_assert((X5_FSLOT & 15u) == 0u, "far slots are 16-byte aligned");
 static_assert(5u * XFAR <= 128u, "a batch's far-copy chunks are loaded by two LDS-DMA wave instructions");
 enum : uint32_t { R5_NORMAL = 0, R5_LONG = 1, R5_NOP = 2, R5_END = 3, R5_BAD = 4 };
 // Descriptor word 0: the token's first output byte relative to the batch's 4-byte aligned base S
@@ -1562,6 +1561,13 @@ __device__ __forceinline__ u32x4 x5_load16(const PF_GLOBAL uint8_t* gin, uint32_
     return r;
 }
 
+// 16 bytes a lane from global address g into LDS at m0 + 16 * lane (LDS-DMA). Issued from inline asm: the
+// compiler, which cannot tell the destination from the producer's other LDS accesses, would otherwise wait
+// for the load before the next of them; the producer waits for it itself before the batch's barrier.
+__device__ __forceinline__ void x5_dma16(uint64_t g, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(g), "s"(lds) : "memory", "m0");
+}
+
 // One input chunk [I - woff, I - woff + XSTAGE) as lane l's 16-byte chunks l and 64 + l (lanes < 5), and its
 // token-start bits (16 input bytes a lane): every load issued before any is used. Chunks wholly at or past n
 // read as zero (the chunk holding the last byte is read whole, as snap_stage does).
@@ -1582,7 +1588,7 @@ __device__ __forceinline__ void x5_chunk_load(const PF_GLOBAL uint8_t* gin, cons
 }
 
 // One piece (mode 0: pieces[item]) or one whole-page redo (mode 1: job item) by the workgroup's two waves.
-__device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
+__device__ __forceinline__ void exec5_piece(X5Lds& S, uint8_t* FS, const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
                                             const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode, int item) {
     uint8_t* const L = S.L;
     uint16_t* const tokpos = S.tokpos;
@@ -1592,6 +1598,11 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
     auto& REC = S.REC;
     uint8_t* const jvb = reinterpret_cast<uint8_t*>(S.jv);
     uint8_t* const ring = L;
+    // The far-copy slots are a separate LDS array, so the compiler can tell the producer's LDS-DMA from its
+    // other LDS accesses (one array: it waits for the loads before the first descriptor write); the
+    // consumer reaches them through the same byte address as the ring and stage, relative to L.
+    const uint32_t Lb = uint32_t(reinterpret_cast<uintptr_t>(L));   // (a flat LDS address's low half: the LDS offset)
+    const uint32_t FSB = uint32_t(reinterpret_cast<uintptr_t>(FS)) - Lb;
     const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
     const int lane = int(threadIdx.x) & 63;
     int j, k;
@@ -1820,7 +1831,7 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                         if (ok) {
                             uint32_t fsh[X5_TPL];
                             uint32_t nfar = 0;
-                            uint64_t* fa = reinterpret_cast<uint64_t*>(L + X5_FBUF0 + b * X5_FSL);   // (overwritten by the loads)
+                            uint64_t* fa = reinterpret_cast<uint64_t*>(FS + b * X5_FSL);   // (overwritten by the loads)
                             #pragma unroll
                             for (int h = 0; h < X5_TPL; h++) {
                                 const PF_GLOBAL uint8_t* fb0 = od.dd != nullptr && a[h] >= od.dlo ? od.dd + a[h] : gdst + a[h];
@@ -1841,12 +1852,10 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                                     const uint32_t l1 = l0 + 64u, f1 = (l1 * 205u) >> 10;
                                     s1a = fa[min(f1, XFAR - 1u)] + 16u * (l1 - 5u * f1);
                                 }
-                                uint8_t* slots = L + X5_FBUF0 + b * X5_FSL;
-                                if (l0 < 5u * nfar)
-                                    __builtin_amdgcn_global_load_lds((const PF_GLOBAL void*)s0a, (__attribute__((address_space(3))) void*)slots, 16, 0, 0);
-                                if (nfar > 12u && l0 + 64u < 5u * nfar)
-                                    __builtin_amdgcn_global_load_lds((const PF_GLOBAL void*)s1a,
-                                                                     (__attribute__((address_space(3))) void*)(slots + 1024), 16, 0, 0);
+                                uint8_t* slots = FS + b * X5_FSL;
+                                const uint32_t sl0 = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(slots)));
+                                if (l0 < 5u * nfar) x5_dma16(s0a, sl0);
+                                if (nfar > 12u && l0 + 64u < 5u * nfar) x5_dma16(s1a, sl0 + 1024u);
                             }
                             X5T(2);   // far-copy source loads (issued)
                             if (lane < int(X5_W)) SB[b][lane] = 0;
@@ -1859,7 +1868,7 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                                     d0 = relS | (near ? (X5_CP | (off[h] << 16)) : 0u);
                                     d1 = near ? uint32_t(65536.0f * __builtin_amdgcn_rcpf(float(off[h]))) + 1u
                                               : (lit[h] ? stg_off + woff + (srcv[h] - I) - relS
-                                                        : X5_FBUF0 + b * X5_FSL + frank[h] * X5_FSLOT + fsh[h] - relS);
+                                                        : FSB + b * X5_FSL + frank[h] * X5_FSLOT + fsh[h] - relS);
                                 }
                                 D[b][1 + 64 * h + lane] = d0;
                                 D[b][1 + X5_DS + 64 * h + lane] = d1;
@@ -1950,7 +1959,7 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
                     // the four source reads issued together (every addr is inside the workgroup's LDS)
                     uint32_t vv[4];
                     #pragma unroll
-                    for (int u = 0; u < 4; u++) vv[u] = uint32_t(L[addr[u]]);
+                    for (int u = 0; u < 4; u++) vv[u] = uint32_t(*reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>(size_t(Lb + addr[u])));
                     asm volatile("" : "+v"(vv[0]), "+v"(vv[1]), "+v"(vv[2]), "+v"(vv[3]));
                     // jump words, two per dword: (value << 1), or 0x8000 | (window position << 1) while pending
                     uint32_t Wa = (pend[0] ? pw[0] : (vv[0] << 1)) | ((pend[1] ? pw[1] : (vv[1] << 1)) << 16);
@@ -2027,7 +2036,8 @@ __device__ __forceinline__ void exec5_piece(X5Lds& S, const SnappyJob* __restric
 __global__ __launch_bounds__(128) void k_snappy_exec5(const SnappyJob* __restrict__ jobs, const int2* __restrict__ pieces,
                                                       const uint32_t* __restrict__ splits, int* __restrict__ fb, int mode) {
     __shared__ X5Lds S;
-    exec5_piece(S, jobs, pieces, splits, fb, mode, int(blockIdx.x));
+    __shared__ __attribute__((aligned(16))) uint8_t FS[2 * X5_FSL];   // far-copy source slots of two batches
+    exec5_piece(S, FS, jobs, pieces, splits, fb, mode, int(blockIdx.x));
 }
 
 #ifdef PF_STAMPS
