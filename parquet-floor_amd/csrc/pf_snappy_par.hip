@@ -142,6 +142,24 @@ __device__ __forceinline__ uint64_t stage_tok(const uint8_t* stage, uint32_t a, 
     return t.tl;
 }
 
+// The token at stream position p of a linear stage (base = stage offset of position 0): the tag and the 3
+// bytes after it from one aligned dword pair; straight-line lengths (a literal length field of 4 bytes,
+// >= 16 MiB, cannot be in a page: tl = 0xffffffff breaks the chain).
+__device__ __forceinline__ void walk_tok(const uint8_t* stage, uint32_t base, uint32_t p, uint32_t& ol, uint32_t& tl) {
+    const uint32_t a = base + p;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(stage + (a & ~3u));
+    const uint32_t v = __builtin_amdgcn_alignbyte(w[1], w[0], a & 3u);
+    const uint32_t tag = v & 0xffu, kind = tag & 3u, Lv = tag >> 2;
+    const uint32_t nb = Lv >= 60u ? Lv - 59u : 0u;
+    const uint32_t lit_ol = (Lv < 60u ? Lv : ((v >> 8) & ((1u << (8u * min(nb, 3u))) - 1u))) + 1u;
+    const uint32_t lit_tl = nb >= 4u ? 0xffffffffu : 1u + nb + lit_ol;
+    // (selects as bit masks: v_bfi, where the compiler would branch on the kind)
+    const uint32_t mlit = 0u - uint32_t(kind == 0u), m1 = 0u - uint32_t(kind == 1u);
+    const uint32_t cp_ol = ((4u + (Lv & 7u)) & m1) | ((Lv + 1u) & ~m1);
+    tl = (lit_tl & mlit) | (((0x05030200u >> (8u * kind)) & 0xffu) & ~mlit);
+    ol = (lit_ol & mlit) | (cp_ol & ~mlit);
+}
+
 // Walk the chain from c while positions stay below re (bits relative to rs). The token-start bits are
 // OR-ed into the lane's four LDS words lb (one ds_or per token, no register selects; round 6) and read
 // back into L at the end.
@@ -153,20 +171,8 @@ __device__ void lane_walk(const uint8_t* stage, uint32_t woff, uint32_t W0, uint
     uint32_t out = 0, p = c;
     L.c = c;
     while (p < re) {
-        // the tag and the 3 bytes after it from one aligned dword pair; straight-line token lengths (a
-        // literal length field of 4 bytes, >= 16 MiB, cannot be in a page: it breaks the chain)
-        const uint32_t a = base + p;
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(stage + (a & ~3u));
-        const uint32_t v = __builtin_amdgcn_alignbyte(w[1], w[0], a & 3u);
-        const uint32_t tag = v & 0xffu, kind = tag & 3u, Lv = tag >> 2;
-        const uint32_t nb = Lv >= 60u ? Lv - 59u : 0u;
-        const uint32_t lit_ol = (Lv < 60u ? Lv : ((v >> 8) & ((1u << (8u * min(nb, 3u))) - 1u))) + 1u;
-        const uint32_t lit_tl = nb >= 4u ? 0xffffffffu : 1u + nb + lit_ol;
-        // (selects as bit masks: v_bfi, where the compiler would branch on the kind)
-        const uint32_t mlit = 0u - uint32_t(kind == 0u), m1 = 0u - uint32_t(kind == 1u);
-        const uint32_t cp_ol = ((4u + (Lv & 7u)) & m1) | ((Lv + 1u) & ~m1);
-        const uint32_t tl = (lit_tl & mlit) | (((0x05030200u >> (8u * kind)) & 0xffu) & ~mlit);
-        const uint32_t ol = (lit_ol & mlit) | (cp_ol & ~mlit);
+        uint32_t ol, tl;
+        walk_tok(stage, base, p, ol, tl);
         const uint32_t i = p - rs;
         atomicOr(lb + (i >> 5), 1u << (i & 31u));
         out = __builtin_elementwise_add_sat(out, ol);
@@ -1564,8 +1570,10 @@ __device__ __forceinline__ u32x4 x5_load16(const PF_GLOBAL uint8_t* gin, uint32_
 // 16 bytes a lane from global address g into LDS at m0 + 16 * lane (LDS-DMA). Issued from inline asm: the
 // compiler, which cannot tell the destination from the producer's other LDS accesses, would otherwise wait
 // for the load before the next of them; the producer waits for it itself before the batch's barrier.
+// (m0 is a reserved register the compiler does not take as a clobber; no code it generates for this file's
+// kernels reads m0 -- checked in the assembly, round 6 -- so every m0 value is this function's.)
 __device__ __forceinline__ void x5_dma16(uint64_t g, uint32_t lds) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(g), "s"(lds) : "memory", "m0");
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(g), "s"(lds) : "memory");
 }
 
 // One input chunk [I - woff, I - woff + XSTAGE) as lane l's 16-byte chunks l and 64 + l (lanes < 5), and its
