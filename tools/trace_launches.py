@@ -20,3 +20,13 @@ print(f"{'kernel':24s} {'launches':>8s} {'avg_us':>10s} {'avg_last%d_us' % passe
 for n, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
     last = v[-passes:]
     print(f"{n:24s} {len(v):8d} {sum(v) / len(v):10.1f} {sum(last) / len(last):14.1f}")
+# the dominant kernel's last launches one by one (start relative to the first of them, queue, duration)
+dom = max(per, key=lambda k: sum(per[k]))
+rows_d = [r for r in rows if r["Kernel_Name"].split("(")[0].replace("pf::", "").replace("void ", "") == dom]
+tail = rows_d[-3 * passes:]
+if tail:
+    t0 = int(tail[0]["Start_Timestamp"])
+    print(f"\nlast {len(tail)} launches of {dom}: start_us queue dur_us")
+    for r in tail:
+        print(f"  {(int(r['Start_Timestamp']) - t0) / 1e3:10.1f} {r.get('Queue_Id', r.get('Stream_Id', '?')):>4s} "
+              f"{(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3:8.1f}")
