@@ -76,7 +76,7 @@ STAGE_LABEL = {"snappy_exec": "Snappy executor stage: k_snappy_exec%s (+ redo, s
                "delta": "DELTA_BINARY_PACKED stage: k_dbp_pos / k_dbp_blk / k_dbp_scan + k_delta",
                "levels": "level / id run stage: k_runs + k_lvl + k_dlen",
                "count": "count stage: k_nest_lvl, k_count[_flat|_seg], k_nest_scan / ids / chars, PLAIN BYTE_ARRAY k_ba_*",
-               "scan": "k_scan", "flat": "flat stage: k_flat_null<4/8> + k_flat_fb + k_flat_all",
+               "scan": "k_scan", "flat": "flat stage: k_flat_null<4/8> + k_flat_fixed + k_flat_all (+ its fallback-queue workgroups)",
                "decode": "decode stage: k_decode + k_decode_seg + k_dba_chars"}
 # the algorithmic bytes each stage is priced with (bench.stage_bytes)
 STAGE_BYTES_DEF = {

@@ -25,7 +25,7 @@ struct PfOpts {
     int null_stagger = 0;     // PF_DEBUG_NULL_STAGGER=k: k_flat_null's blocks > 0 wait k rounds (race tests)
     bool nest_timeout = false;   // PF_DEBUG_NEST_TIMEOUT=1: every k_nest_lvl hand-over times out (whole-page path; tests)
     uint32_t null_dcap = 0;   // PF_NULL_DCAP=b: k_flat_null's level-byte stage instead of the batch's (16: blocks with
-                              // level bytes do not fit, so k_lvl refuses the page and k_flat_fb decodes it; tests)
+                              // level bytes do not fit, so k_lvl refuses the page and the fallback queue decodes it; tests)
     bool piece_order = true;  // PF_PIECE_ORDER=0: Snappy pieces in page order
     unsigned debug_skip = 0;  // PF_DEBUG_SKIP=parse,exec,ba,levels,count,flat,decode (results are wrong)
     int force_serial = 0;     // PF_DEBUG_FORCE_SERIAL=k: every k-th Snappy job to the serial kernel

@@ -2563,7 +2563,7 @@ __device__ __forceinline__ bool flat_fixed_block(FixedLds& S, const DevChunk* __
 }
 
 // Fallback queue (device, zeroed with the batch metadata): word 0 counts the (page, block) pairs that
-// start at word 4; k_flat_null and k_flat_fixed append the blocks they do not take, k_flat_fb decodes them.
+// start at word 4; k_flat_null and k_flat_fixed append the blocks they do not take, the last workgroups of k_flat_all decode them.
 __device__ __forceinline__ void null_fallback(int* fbq, int2 pbk) {
     if (threadIdx.x == 0) reinterpret_cast<int2*>(fbq + 4)[atomicAdd(fbq, 1)] = pbk;
 }
@@ -2571,7 +2571,7 @@ __device__ __forceinline__ void null_fallback(int* fbq, int2 pbk) {
 // k_flat_fixed (round 5): the blocks of flat fixed-width pages, in a list of their own. Its register
 // budget is the fixed-width body's (73 VGPRs, 21 KiB LDS: six workgroups per CU, against four of
 // k_flat_all's 127-VGPR union of both bodies); blocks it does not take (a page with nulls that
-// k_flat_null did not take, levels that are not RLE, ...) go to the fallback queue for k_flat_fb.
+// k_flat_null did not take, levels that are not RLE, ...) go to the fallback queue (k_flat_all's last workgroups).
 #ifndef PF_FIXED_OCC
 #define PF_FIXED_OCC 6
 #endif
@@ -2918,36 +2918,32 @@ __device__ __forceinline__ void flat_block(FlatLds& S, const DevChunk* __restric
 #ifndef PF_FLAT_OCC
 #define PF_FLAT_OCC 5   // round 5 (with CV_CAP 2048 and the chars copies inlined): SF1 2.74 -> 2.69 ms; 4 before
 #endif
+// Workgroups n.. of the grid take the fallback queue (round 6: k_flat_fb's launch folded in; the producers
+// of the queue, k_flat_fixed and k_flat_null, are earlier in stream order): a grid stride over the queued
+// blocks, nearly always none.
 __global__ __launch_bounds__(NT, PF_FLAT_OCC) void k_flat_all(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                                 const int2* __restrict__ blocks, DevChunkResult* res) {
+                                                 const int2* __restrict__ blocks, int n, const int* __restrict__ fbq,
+                                                 DevChunkResult* res) {
     __shared__ union FlatAllLds {
         FixedLds f;
         FlatLds g;
     } S;
+    if (int(blockIdx.x) >= n) {
+        const int nq = fbq[0], g = int(gridDim.x) - n;
+        for (int i = int(blockIdx.x) - n; i < nq; i += g) {
+            const int2 pq = reinterpret_cast<const int2*>(fbq + 4)[i];
+            if (!flat_fixed_block(S.f, chunks, pages, pq, res)) {
+                __syncthreads();
+                flat_block(S.g, chunks, pages, pq, res);
+            }
+            __syncthreads();   // the block's LDS reads are done before the next one reuses it
+        }
+        return;
+    }
     const int2 pbk = blocks[blockIdx.x];
     if (flat_fixed_block(S.f, chunks, pages, pbk, res)) return;
     __syncthreads();   // the fixed body's LDS reads are done before the general body reuses it
     flat_block(S.g, chunks, pages, pbk, res);
-}
-
-// k_flat_fb: the blocks k_flat_null and k_flat_fixed did not take (the fallback queue, filled earlier
-// in stream order), grid-stride over 32 workgroups (the queue is nearly always empty: a page with no
-// block table, one k_page_null took, levels that are not RLE). Same bodies as k_flat_all.
-__global__ __launch_bounds__(NT, PF_FLAT_OCC) void k_flat_fb(const DevChunk* __restrict__ chunks, DevPage* pages,
-                                                const int* __restrict__ fbq, DevChunkResult* res) {
-    __shared__ union FlatAllLds {
-        FixedLds f;
-        FlatLds g;
-    } S;
-    const int n = fbq[0];
-    for (int i = int(blockIdx.x); i < n; i += int(gridDim.x)) {
-        const int2 pbk = reinterpret_cast<const int2*>(fbq + 4)[i];
-        if (!flat_fixed_block(S.f, chunks, pages, pbk, res)) {
-            __syncthreads();
-            flat_block(S.g, chunks, pages, pbk, res);
-        }
-        __syncthreads();   // the block's LDS reads are done before the next one reuses it
-    }
 }
 
 // ---- nullable flat pages: definition-level run table + block-parallel decode ------------------
@@ -3343,7 +3339,7 @@ __global__ __launch_bounds__(LT_NT, PF_LVL_OCC) void k_lvl(const DevChunk* __res
 // rank popc(fv & (2^k - 1)). The stage is latency-bound (Σ block latency / resident blocks), so what
 // sets it is the entries in flight per CU: 16 per lane (round 5; 8 per lane at 512 threads: config 4's
 // flat launch 0.97 -> 0.81 ms, gpurun_out/ntn). The runtime gives the kernel only nullable pages of its
-// width (its own block lists); a page it does not take goes to the fallback queue for k_flat_fb.
+// width (its own block lists); a page it does not take goes to the fallback queue (k_flat_all's last workgroups).
 #ifndef PF_NTN
 #define PF_NTN 256
 #endif
@@ -3409,7 +3405,7 @@ __global__ __launch_bounds__(NTN) void k_flat_null(const DevChunk* __restrict__ 
     const DevChunk& ck = chunks[pg.chunk];
     const int tid = threadIdx.x;
     const uint32_t* LT = pg.lvltab;
-    // pages this kernel does not take (whole pages: the conditions are the page's) go to k_flat_fb
+    // pages this kernel does not take (whole pages: the conditions are the page's) go to the fallback queue
     // (not DONE_NULL: blocks of this page that finished first set it, and a block starting later must still run)
     if (!LT || res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.width != W ||
         (pg.done & (DONE_FIXED | DONE_PAGE)) || LT[1] != 1u) {   // (k_page_null took it, or no block table)
@@ -4584,7 +4580,7 @@ void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
     // d_list: nfix (page, block) pairs of flat fixed-width pages (k_flat_fixed), then n of every other
     // flat page (k_flat_all), then n4 / n8 of nullable 4 / 8-byte pages (k_flat_null<4> / <8>; they mark
     // their pages DONE_NULL). Blocks k_flat_null and k_flat_fixed do not take are queued in d_fbq for
-    // k_flat_fb. nc: k_flat_null's LDS stages (dictionary: nc.dlds bytes); stagger (diagnostics build,
+    // k_flat_all's last workgroups. nc: k_flat_null's LDS stages (dictionary: nc.dlds bytes); stagger (diagnostics build,
     // tests): k_flat_null's blocks > 0 of a page wait that many sleep rounds (~3 us each) for block 0
     const int2* blocks = reinterpret_cast<const int2*>(d_list);
     const size_t dyn = size_t(nc.dcap) + 32u + nc.icap + 32u + nc.dlds;
@@ -4594,11 +4590,13 @@ void launch_flat(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, 
         hipLaunchKernelGGL(k_flat_null<8>, dim3(n8), dim3(NTN), dyn, st, d_chunks, d_pages, blocks + nfix + n + n4, d_res, nc, stagger,
                            d_fbq);
     if (nfix > 0) hipLaunchKernelGGL(k_flat_fixed, dim3(nfix), dim3(NT), 0, st, d_chunks, d_pages, blocks, d_res, d_fbq);
-    if (n > 0) hipLaunchKernelGGL(k_flat_all, dim3(n), dim3(NT), 0, st, d_chunks, d_pages, blocks + nfix, d_res);
+    // k_flat_all last, with min(nq, 32) more workgroups for the fallback queue (nearly always empty; each
+    // needs a CU with room for a k_flat_all workgroup: a grid of min(nq, 1024) waited ~0.1 ms under load,
+    // and a launch of its own added one more wait per batch)
     const int nq = nfix + n4 + n8;
-    // (the queue is nearly always empty, and each of k_flat_fb's workgroups needs a CU with room for
-    // k_flat_all-sized workgroups: a grid of min(nq, 1024) waited ~0.1 ms a launch under load on SF1)
-    if (nq > 0) hipLaunchKernelGGL(k_flat_fb, dim3(nq < 32 ? nq : 32), dim3(NT), 0, st, d_chunks, d_pages, d_fbq, d_res);
+    const int nqw = nq < 32 ? nq : 32;
+    if (n + nqw > 0)
+        hipLaunchKernelGGL(k_flat_all, dim3(n + nqw), dim3(NT), 0, st, d_chunks, d_pages, blocks + nfix, n, d_fbq, d_res);
 }
 void launch_decode(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int n_first,
                    DevChunkResult* d_res, hipStream_t st, int idle_grid) {

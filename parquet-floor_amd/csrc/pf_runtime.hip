@@ -1424,7 +1424,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     // interleaved into the grid; short ones are padded with (-1, 0).
     // Four such grids, one after the other in l_flat: fixed-width pages (k_flat_fixed), the other flat
     // pages (k_flat_all), then the blocks of nullable 4- and 8-byte pages (k_flat_null<4> / <8>);
-    // k_flat_fixed and k_flat_null queue what they do not take for k_flat_fb.
+    // k_flat_fixed and k_flat_null queue what they do not take for k_flat_all's last workgroups.
     constexpr uint32_t STICKY_DICT = 64u << 10;
     std::vector<int> spread[4];
     std::vector<std::vector<int>> sticky[4];

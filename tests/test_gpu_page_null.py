@@ -138,7 +138,7 @@ def test_null_blocks_staggered(oracle, tmp_path, switches, page_null):
 
 @pytest.mark.parametrize("stagger", ["0", "100"])
 def test_null_fallback_queue(oracle, tmp_path, switches, stagger):
-    """Pages k_flat_null does not take go to its fallback queue and k_flat_fb decodes them (round 5:
+    """Pages k_flat_null does not take go to its fallback queue and the fallback queue (k_flat_all's last workgroups) decodes them (round 5:
     k_flat_all no longer walks the nullable blocks). PF_NULL_DCAP=16 leaves no room for any block's
     level bytes, so k_lvl refuses every nullable page (fit word 0) and all of them take that path;
     INT32 / INT64 / DOUBLE dictionary columns and a PLAIN INT64 one, 30 % nulls, bit-exact."""
@@ -164,7 +164,7 @@ def test_null_fallback_queue(oracle, tmp_path, switches, stagger):
     assert got["_status"] == 0, got["_error"]
     with oracle.open(path) as of:
         for c in range(4):
-            assert_chunk_equal(got[(0, c)], of.decode(0, c), f"column {c} via k_flat_fb")
+            assert_chunk_equal(got[(0, c)], of.decode(0, c), f"column {c} via the fallback queue")
     nullable = [f for f in flags if f[0] & 4 or f[1] != 0]
     assert not nullable, flags   # no page was taken by k_flat_null / k_page_null
 

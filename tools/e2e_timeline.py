@@ -57,3 +57,16 @@ for c in cats:
 dl = [(a, b) for a, b, c, _ in ev if c in ("dl", "d2h")]
 h2d = [(a, b) for a, b, c, _ in ev if c == "h2d"]
 print(f"  link busy (any H2D or download) {union(dl + h2d) / 1e6:.2f} ms; download-or-D2H busy {union(dl) / 1e6:.2f} ms")
+# downloads one by one: duration and the gap since the previous download ended (any stream)
+dls = sorted((a, b, s) for a, b, c, s in ev if c == "dl")
+if dls:
+    durs = [(b - a) / 1e3 for a, b, _ in dls]
+    gaps, last = [], None
+    for a, b, _ in dls:
+        if last is not None and a > last:
+            gaps.append((a - last) / 1e3)
+        last = b if last is None else max(last, b)
+    print(f"  downloads: {len(dls)}, duration us min {min(durs):.0f} avg {sum(durs) / len(durs):.0f} max {max(durs):.0f}; "
+          f"idle gaps between downloads {len(gaps)}, total {sum(gaps) / 1e3:.2f} ms, max {max(gaps) if gaps else 0:.0f} us")
+    conc = sum(1 for i in range(1, len(dls)) if dls[i][0] < dls[i - 1][1])
+    print(f"  downloads starting while the previous one runs: {conc}")
