@@ -128,3 +128,34 @@ def test_executors_agree(oracle, switches, executor):
             got, fb = dec.snappy_decompress(oracle.snappy_compress(data, mode=0))
             assert got == data, (executor, name, len(data))
             assert fb == 0, (executor, name)
+
+
+def _far_dense(seed):
+    """Copies of 10-30 bytes from 4-12 KiB back, several dozen per executor batch: every batch's far-copy
+    slots fill (the producer cuts at XFAR), at every source alignment."""
+    rng = np.random.default_rng(seed)
+    out = bytearray(rng.integers(0, 256, 12288, dtype=np.uint8).tobytes())
+    while len(out) < 200_000:
+        back = int(rng.integers(4096, 12288))
+        ln = int(rng.integers(10, 31))
+        out += out[len(out) - back:len(out) - back + ln]
+        out += bytes([int(rng.integers(0, 256))])   # (a literal byte between the copies)
+    return bytes(out)
+
+
+def _periodic_all_offsets(seed):
+    """Runs of period 1-200 (copies that overlap their own output, offsets 1..200, lengths to 64):
+    the consumer's source arithmetic floor(j / offset) for every j < 64."""
+    rng = np.random.default_rng(seed)
+    parts = []
+    for per in list(range(1, 201)) * 2:
+        unit = rng.integers(0, 256, per, dtype=np.uint8).tobytes()
+        parts.append(unit * (int(rng.integers(130, 400)) // per + 2))
+    return b"".join(parts)
+
+
+def test_executor_far_slots_and_periodic_copies(dec, oracle):
+    for name, data in (("far_dense", _far_dense(3)), ("periodic", _periodic_all_offsets(4))):
+        got, fb = dec.snappy_decompress(oracle.snappy_compress(data, mode=0))
+        assert got == data, (name, len(data))
+        assert fb == 0, name
