@@ -821,6 +821,20 @@ __device__ int64_t ba_relink_wg(BaJob& J, uint32_t* tmp) {
 
 // Grid-stride over the jobs with a small grid: nearly every walk was accepted by the checks above,
 // and a block per job (21 KB of LDS each) would wait for CUs held by other streams' kernels.
+#ifdef PF_DIAG   // diagnostics build: jobs k_ba_fallback re-linked / walked exactly (tests)
+__device__ unsigned long long pf_ba_counts[2];
+extern "C" int pf_debug_ba_counts(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_ba_counts), sizeof(unsigned long long) * 2) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned long long z[2] = {0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(pf_ba_counts), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#define BA_COUNT(i) (threadIdx.x == 0 ? (void)atomicAdd(&pf_ba_counts[i], 1ull) : (void)0)
+#else
+#define BA_COUNT(i) ((void)0)
+#endif
 __global__ __launch_bounds__(NT) void k_ba_fallback(BaJob* __restrict__ jobs, int n_jobs, DevChunkResult* res) {
     __shared__ BinWalkLds W;
     __shared__ long long s_chars;
@@ -834,6 +848,7 @@ __global__ __launch_bounds__(NT) void k_ba_fallback(BaJob* __restrict__ jobs, in
             __syncthreads();
             if (c >= 0) {
                 if (threadIdx.x == 0 && J.chars_out) *J.chars_out = s_chars;
+                BA_COUNT(0);
                 __syncthreads();
                 continue;
             }
@@ -841,6 +856,7 @@ __global__ __launch_bounds__(NT) void k_ba_fallback(BaJob* __restrict__ jobs, in
             continue;
         }
         const int64_t t = binary_walk_wg(J.p, J.n, J.count, J.pos, J.len, W);
+        BA_COUNT(1);
         if (threadIdx.x == 0) {
             if (t < 0) set_status(res, J.chunk, ST_CORRUPT, J.page);
             else if (J.chars_out) *J.chars_out = t;

@@ -57,8 +57,8 @@ def test_plain_strings(decoder, oracle, tmp_path, mix, version, nulls):
 @pytest.mark.parametrize("version", ["1.0", "2.0"])
 def test_plain_strings_rare_long(decoder, oracle, tmp_path, version):
     """Short values with a few long ones (page average under k_ba_tile's 48-byte limit, some values
-    past its 124-byte halo): the fused walk cannot link those values, the page takes the exact
-    fallback walk; a second, all-long column in the same batch sends the batch to the round-3 walk
+    past its 124-byte halo): the fused walk cannot link those values, so k_ba_fallback re-links the
+    job over its whole candidate bitmap (test_rare_long_values_relinked_not_walked); a second, all-long column in the same batch sends the batch to the round-3 walk
     kernels. Both columns bit-exact vs the oracle (k_ba_tile, round 4)."""
     import pyarrow as pa
     import pyarrow.parquet as pq
@@ -85,6 +85,42 @@ def test_plain_strings_rare_long(decoder, oracle, tmp_path, version):
         with oracle.open(path) as of:
             for c in cols:
                 assert_chunk_equal(got[(0, c)], of.decode(0, c), f"rare long v{version} col {c} of {cols}")
+
+
+def test_rare_long_values_relinked_not_walked(oracle, tmp_path):
+    """a PLAIN string page with a few values longer than k_ba_tile's halo fails the fused
+    walk's chain check (BA_RELINK); k_ba_fallback must re-link it from the tiles' candidate words
+    (ba_relink_wg), not drop to the exact serial walk -- which needs every tile to write its words even
+    after another tile rejected the job. Diagnostics build counters (pf_debug_ba_counts)."""
+    import ctypes as C
+
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from pfloor import _native
+    from pfloor.decoder import GpuDecoder, decode_file
+    rng = np.random.default_rng(23)
+    n = 60_000
+    alphabet = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz ,.0123456789", np.uint8)
+    lens = rng.integers(8, 30, n)
+    lens[rng.random(n) < 0.005] = rng.integers(200, 600)
+    chars = alphabet[rng.integers(0, len(alphabet), int(lens.sum()))].tobytes()
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    t = pa.table({"a": pa.array([chars[offs[i]:offs[i + 1]].decode() for i in range(n)], type=pa.string())})
+    path = str(tmp_path / "relink.parquet")
+    pq.write_table(t, path, compression="snappy", use_dictionary=False, row_group_size=n, data_page_size=1 << 20)
+    with _native.diagnostics() as L:
+        f = L.pf_debug_ba_counts
+        f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+        buf = (C.c_ulonglong * 2)()
+        with GpuDecoder(0) as dec:
+            assert f(buf, 1) == 0
+            got = decode_file(path, decoder=dec)
+            assert f(buf, 1) == 0
+        assert got["_status"] == 0, got["_error"]
+        with oracle.open(path) as of:
+            assert_chunk_equal(got[(0, 0)], of.decode(0, 0), "rare long relink")
+        relinked, walked = int(buf[0]), int(buf[1])
+        assert relinked >= 1 and walked == 0, (relinked, walked)
 
 
 @pytest.mark.parametrize("nulls", [False, True])
