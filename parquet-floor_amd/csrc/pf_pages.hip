@@ -1726,26 +1726,13 @@ __device__ __forceinline__ uint32_t run_value(const Run& r, const uint8_t* p, ui
     return r.packed ? bits_le(p, n, uint64_t(r.data) + uint64_t(i - r.first) * uint64_t(bw), bw) : r.data;
 }
 
-// Dictionary-string pages k_count_flat takes: flat, levels all present (k_runs: T[3]), a run table.
-__device__ __forceinline__ bool count_dict_page(const DevPage& pg, const DevChunk& ck, const Sections& s) {
-    const uint32_t* T = pg.runtab;
-    return T != nullptr && T[3] == 1u && T[0] <= uint32_t(RUN_CAP) && T[1] >= uint32_t(pg.num_values) && ck.dict_len &&
-           s.val_n > 0 && flat_block_chars(pg) != nullptr;
-}
-constexpr uint64_t BC_BAD = ~0ull;   // a block's chars word when one of its ids is out of the dictionary
-
 // One 128-thread workgroup per dictionary data page of a flat chunk: walks the page's
 // dictionary-id run headers ONCE (wave 1) and checks whether every definition level is present
 // (wave 0), so that k_flat's blocks of the page load a ready run table instead of each walking
-// the headers from the page start. Flat dictionary BYTE_ARRAY pages then sum the dictionary lengths
-// of each 4096-entry block's ids into the page's block chars words (round 6: k_count_dict's pass,
-// done while the run table is in LDS; k_count_flat scans the words).
-constexpr int RNT = 256;
-__global__ __launch_bounds__(RNT) void k_runs(const DevChunk* __restrict__ chunks, DevPage* pages,
+// the headers from the page start.
+__global__ __launch_bounds__(128) void k_runs(const DevChunk* __restrict__ chunks, DevPage* pages,
                                               const int* __restrict__ list, DevChunkResult* res) {
     __shared__ Run R[RUN_CAP];
-    __shared__ uint32_t s_len[DSTR_CAP];   // lengths of small dictionaries
-    __shared__ unsigned long long s_acc;
     __shared__ int s_allp, s_nr, s_res;
     __shared__ uint32_t s_cov;
     const int pi = list[blockIdx.x];
@@ -1763,7 +1750,7 @@ __global__ __launch_bounds__(RNT) void k_runs(const DevChunk* __restrict__ chunk
     const int id_bw = int(s.val[0]);
     if (tid == 0) {
         s_allp = ck.max_def == 0 ? 1 : (s.def_rle ? all_present(s.def, s.def_n, bit_width(ck.max_def), ne, uint32_t(ck.max_def)) : 0);
-    } else if (tid >= 64 && tid < 128) {   // wave 1: the id runs, discovered wave-parallel
+    } else if (tid >= 64) {   // wave 1: the id runs, discovered wave-parallel
         __shared__ RunWalk s_st;
         int nr = 0;
         uint32_t cov = 0;
@@ -1776,63 +1763,97 @@ __global__ __launch_bounds__(RNT) void k_runs(const DevChunk* __restrict__ chunk
         if (tid == 0) { T[2] = 0; T[3] = 0; }
         return;
     }
-    for (int i = tid; i < nr; i += RNT) {
+    for (int i = tid; i < nr; i += 128) {
         T[4 + 2 * i] = R[i].first | (R[i].packed << 31);
         T[5 + 2 * i] = R[i].data;
     }
     // T[2]: the id table is valid (indexed by value: pages with nulls hold fewer ids than entries, the
     // walk then ends with the stream); T[3]: valid and every level present (k_flat_fixed / k_flat split)
     if (tid == 0) { T[0] = uint32_t(nr); T[1] = s_cov; T[2] = 1u; T[3] = s_allp ? 1u : 0u; }
-    // ---- chars of each 4096-entry block (the pages count_dict_page admits, from this run table)
-    uint64_t* bc = flat_block_chars(pg);
-    if (!(ck.ptype == 6 && ck.max_rep == 0 && is_dict_enc(pg.encoding) && s_allp && nr <= RUN_CAP && s_cov >= ne &&
-          ck.dict_len != nullptr && bc != nullptr))
-        return;
-    const bool lstage = ck.dict_n > 0 && ck.dict_n <= int64_t(DSTR_CAP);
-    if (lstage)
-        for (uint32_t i = tid; i < uint32_t(ck.dict_n); i += RNT) s_len[i] = gptr(ck.dict_len)[i];
-    const uint8_t* ids = s.val + 1;
-    const uint64_t ids_n = s.val_n - 1;
-    const uint32_t nb = max(1u, (ne + FBLK - 1) / FBLK);
-    constexpr int EPB = int(FBLK) / RNT;   // entries of a block per thread
-    int r = -1;
-    for (uint32_t b = 0; b < nb; b++) {
-        if (tid == 0) s_acc = 0;
-        __syncthreads();   // (s_len staged; the last block's s_acc read)
-        const uint32_t b0 = b * FBLK, b1 = min(ne, b0 + FBLK);
-        int bad = 0;
-        // ids of the thread's EPB entries first (their loads in flight together), then the lengths
-        uint32_t idk[EPB];
-        #pragma unroll
-        for (int k = 0; k < EPB; k++) {
-            const uint32_t e = b0 + uint32_t(k) * RNT + uint32_t(tid);
-            idk[k] = 0xffffffffu;
-            if (e >= b1) continue;
-            if (r < 0) r = run_find(R, nr, e);
-            while (e >= R[r].first + R[r].count) r++;
-            const Run& Rr = R[r];
-            uint32_t id = Rr.data;
-            if (Rr.packed) {
-                const uint64_t bit = uint64_t(Rr.data) + uint64_t(e - Rr.first) * uint64_t(id_bw);
-                id = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
-                                              : bits_le(ids, ids_n, bit, id_bw);
-            }
-            if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
-            idk[k] = id;
-        }
-        uint64_t acc = 0;
-        #pragma unroll
-        for (int k = 0; k < EPB; k++)
-            if (idk[k] != 0xffffffffu) acc += lstage ? s_len[idk[k]] : gptr(ck.dict_len)[idk[k]];
-        if (acc) atomicAdd(&s_acc, (unsigned long long)acc);
-        bad = __syncthreads_or(bad);
-        if (tid == 0) bc[b] = bad ? BC_BAD : uint64_t(s_acc);
-    }
 }
 
+// Dictionary-string pages k_count_flat takes: flat, levels all present (k_runs: T[3]), a run table.
+__device__ __forceinline__ bool count_dict_page(const DevPage& pg, const DevChunk& ck, const Sections& s) {
+    const uint32_t* T = pg.runtab;
+    return T != nullptr && T[3] == 1u && T[0] <= uint32_t(RUN_CAP) && T[1] >= uint32_t(pg.num_values) && ck.dict_len &&
+           s.val_n > 0 && flat_block_chars(pg) != nullptr;
+}
+constexpr uint64_t BC_BAD = ~0ull;   // a block's chars word when one of its ids is out of the dictionary
+
+// k_count_dict (round 5): the chars of one 4096-entry block of a flat dictionary BYTE_ARRAY page per
+// workgroup -- the block's ids from the page's run table (k_runs), their dictionary lengths summed --
+// into the page's per-block chars word bc[block]; k_count_flat scans those words into the blocks'
+// chars bases and the page's chars. (Round 4 summed a page's blocks one after another in
+// k_count_flat's one workgroup per page: SF1's pages of ~1M entries were 256 dependent rounds.)
+__global__ __launch_bounds__(NT) void k_count_dict(const DevChunk* __restrict__ chunks, DevPage* pages,
+                                                   const int2* __restrict__ blocks, DevChunkResult* res) {
+    __shared__ Run R[RUN_CAP];
+    __shared__ uint32_t s_len[DSTR_CAP];   // lengths of small dictionaries
+    __shared__ unsigned long long s_acc;
+    const int2 pb = blocks[blockIdx.x];
+    DevPage& pg = pages[pb.x];
+    const DevChunk& ck = chunks[pg.chunk];
+    const int tid = threadIdx.x;
+    if (res[pg.chunk].status != 0 || ck.max_rep != 0 || ck.ptype != 6 || !is_dict_enc(pg.encoding)) return;
+    Sections s;
+    if (!page_sections(pg, ck, s) || !count_dict_page(pg, ck, s)) return;
+    const uint32_t ne = uint32_t(pg.num_values);
+    const uint32_t b0 = uint32_t(pb.y) * FBLK;
+    if (pb.y > 0 && b0 >= ne) return;
+    const uint32_t b1 = min(ne, b0 + FBLK);
+    const uint32_t* T = pg.runtab;
+    const uint32_t nr = T[0], cov = T[1];
+    for (uint32_t i = tid; i < nr; i += NT) {
+        const uint32_t f = T[4 + 2 * i];
+        const uint32_t nf = i + 1 < nr ? (T[4 + 2 * (i + 1)] & 0x7fffffffu) : cov;
+        Run r;
+        r.first = f & 0x7fffffffu;
+        r.count = nf - r.first;
+        r.data = T[5 + 2 * i];
+        r.packed = f >> 31;
+        R[i] = r;
+    }
+    const bool lstage = ck.dict_n > 0 && ck.dict_n <= int64_t(DSTR_CAP);
+    if (lstage)
+        for (uint32_t i = tid; i < uint32_t(ck.dict_n); i += NT) s_len[i] = gptr(ck.dict_len)[i];
+    if (tid == 0) s_acc = 0;
+    __syncthreads();
+    const uint8_t* ids = s.val + 1;
+    const uint64_t ids_n = s.val_n - 1;
+    const int id_bw = int(s.val[0]);
+    constexpr int EPB = int(FBLK) / NT;   // entries of the block per thread
+    int bad = 0;
+    uint64_t acc = 0;
+    // ids of the thread's EPB entries first (their loads in flight together), then the lengths
+    uint32_t idk[EPB];
+    int r = -1;
+    #pragma unroll
+    for (int k = 0; k < EPB; k++) {
+        const uint32_t e = b0 + uint32_t(k) * NT + uint32_t(tid);
+        idk[k] = 0xffffffffu;
+        if (e >= b1) continue;
+        if (r < 0) r = run_find(R, int(nr), e);
+        while (e >= R[r].first + R[r].count) r++;
+        const Run& Rr = R[r];
+        uint32_t id = Rr.data;
+        if (Rr.packed) {
+            const uint64_t bit = uint64_t(Rr.data) + uint64_t(e - Rr.first) * uint64_t(id_bw);
+            id = (bit >> 3) + 12 <= ids_n ? bits_fast(ids + (bit >> 3), uint32_t(bit & 7), id_bw)
+                                          : bits_le(ids, ids_n, bit, id_bw);
+        }
+        if (int64_t(id) >= ck.dict_n) { bad = 1; continue; }
+        idk[k] = id;
+    }
+    #pragma unroll
+    for (int k = 0; k < EPB; k++)
+        if (idk[k] != 0xffffffffu) acc += lstage ? s_len[idk[k]] : gptr(ck.dict_len)[idk[k]];
+    if (acc) atomicAdd(&s_acc, (unsigned long long)acc);
+    bad = __syncthreads_or(bad);
+    if (tid == 0) flat_block_chars(pg)[pb.y] = bad ? BC_BAD : uint64_t(s_acc);
+}
 
 // k_count for flat BYTE_ARRAY pages whose levels are all present: slots = rows = values =
-// entries; dictionary strings scan k_runs's per-block chars (k_flat's per-block chars bases,
+// entries; dictionary strings scan k_count_dict's per-block chars (k_flat's per-block chars bases,
 // the page's chars); PLAIN pages hand their value chain to the k_ba walk. Marks the page counted
 // (pg.counted) so k_count skips it; pages it leaves alone (nulls, corrupt) go through k_count.
 __global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ chunks, DevPage* pages,
@@ -1852,7 +1873,7 @@ __global__ __launch_bounds__(NT) void k_count_flat(const DevChunk* __restrict__ 
     uint64_t total = 0;
     if (dict) {
         if (!count_dict_page(pg, ck, s)) return;
-        // k_runs's block sums -> exclusive bases in place (a page of 1M entries: 256 words)
+        // k_count_dict's block sums -> exclusive bases in place (a page of 1M entries: 256 words)
         uint64_t* bc = flat_block_chars(pg);
         const uint32_t nb = (ne + FBLK - 1) / FBLK;
         int bad = 0;
@@ -4436,11 +4457,13 @@ void launch_nest_decode(const DevChunk* d_chunks, DevPage* d_pages, const int2* 
                         hipStream_t st) {
     if (n_segs > 0) hipLaunchKernelGGL(k_decode_seg, dim3(n_segs), dim3(NT), 0, st, d_chunks, d_pages, d_segs, d_res);
 }
-void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int n_flat,
+void launch_count(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, int n_flat, const int2* d_dblk, int n_dblk,
                   DevChunkResult* d_res, BaJob* d_bajobs, hipStream_t st, int idle_grid) {
     // d_list: the n_flat flat BYTE_ARRAY pages (k_count_flat's grid; none: no launch) first, then the
-    // other pages that need counts. (The dictionary pages' block chars come from k_runs, round 6.)
+    // other pages that need counts. d_dblk: (page, block) pairs of the flat dictionary BYTE_ARRAY
+    // pages (k_count_dict, before k_count_flat)
     if (n <= 0) return;
+    if (n_dblk > 0) hipLaunchKernelGGL(k_count_dict, dim3(n_dblk), dim3(NT), 0, st, d_chunks, d_pages, d_dblk, d_res);
     if (n_flat > 0) hipLaunchKernelGGL(k_count_flat, dim3(n_flat), dim3(NT), 0, st, d_chunks, d_pages, d_list, d_res, d_bajobs);
     hipLaunchKernelGGL(k_count, dim3(std::min(n, idle_grid)), dim3(NT), 0, st, d_chunks, d_pages, d_list, n, d_res, d_bajobs);
 }
@@ -4577,7 +4600,7 @@ void launch_scan(DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n,
 }
 void launch_runs(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                  hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_runs, dim3(n), dim3(RNT), 0, st, d_chunks, d_pages, d_list, d_res);
+    if (n > 0) hipLaunchKernelGGL(k_runs, dim3(n), dim3(128), 0, st, d_chunks, d_pages, d_list, d_res);
 }
 void launch_lvl(const DevChunk* d_chunks, DevPage* d_pages, const int* d_list, int n, DevChunkResult* d_res,
                 hipStream_t st, bool page_null, NullCaps nc) {

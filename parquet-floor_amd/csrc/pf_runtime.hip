@@ -35,7 +35,7 @@ void launch_snappy_litcopy(const SnappyJob*, const int*, int, const int*, hipStr
 void launch_delta(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, hipStream_t);
 void launch_dlen(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
 void launch_dba_chars(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t);
-void launch_count(const DevChunk*, DevPage*, const int*, int, int, DevChunkResult*, BaJob*, hipStream_t, int);
+void launch_count(const DevChunk*, DevPage*, const int*, int, int, const int2*, int, DevChunkResult*, BaJob*, hipStream_t, int);
 void launch_scan(DevChunk*, DevPage*, const int*, int, DevChunkResult*, uint8_t*, uint64_t, unsigned long long*, hipStream_t);
 void launch_flat(const DevChunk*, DevPage*, const int*, int, int, int, int, int*, DevChunkResult*, hipStream_t, NullCaps, int);
 void launch_lvl(const DevChunk*, DevPage*, const int*, int, DevChunkResult*, hipStream_t, bool, NullCaps);
@@ -212,7 +212,8 @@ struct pf_ctx {
     std::vector<DevChunk> chunks;          // host copies (device pointers)
     std::vector<DevPage> pages;
     std::vector<SnappyJob> jobs;
-    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode, l_runs, l_dlen, l_dba, l_lvl, l_djobs, l_nest, l_nseg;
+    std::vector<int> l_dictbin, l_delta, l_count, l_scan, l_flat, l_decode, l_runs, l_dlen, l_dba, l_lvl, l_djobs, l_nest, l_nseg,
+        l_cdict;   // l_cdict: (page, block) pairs of flat dictionary BYTE_ARRAY pages (k_count_dict)
     std::vector<int2> wins, pieces;       // Snappy index windows / 64 KiB pieces (job, index)
     std::vector<BaJob> bajobs;             // PLAIN BYTE_ARRAY walks: dictionary pages, then data pages
     std::vector<int2> ba_tiles;            // (job relative to its batch, tile)
@@ -301,6 +302,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     int* d_djobs = lists + lo; lo += ctx->l_djobs.size();
     int* d_nest = lists + lo; lo += ctx->l_nest.size();
     const int2* d_nseg = reinterpret_cast<const int2*>(lists + lo); lo += ctx->l_nseg.size();
+    const int2* d_cdict = reinterpret_cast<const int2*>(lists + lo); lo += ctx->l_cdict.size();
     const int n_nest = int(ctx->l_nest.size()), n_nseg = int(ctx->l_nseg.size() / 2);
     unsigned long long* used = reinterpret_cast<unsigned long long*>(meta + ctx->meta_bytes - 256);
     const int2* d_pieces = reinterpret_cast<const int2*>(meta + ctx->off_pieces);
@@ -355,7 +357,7 @@ int enqueue_kernels(pf_ctx* ctx) {
     launch_dlen(d_chunks, d_pages, d_dlen, int(ctx->l_dlen.size()), d_res, st);
     EVREC(ctx, ctx->ev[6], st);
     launch_nest_lvl(d_chunks, d_pages, d_nest, n_nest, ctx->max_nwin, d_res, st, ctx->opts.nest_timeout);
-    if (!(skip & 16u)) launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), ctx->n_count_flat,
+    if (!(skip & 16u)) launch_count(d_chunks, d_pages, d_count, int(ctx->l_count.size()), ctx->n_count_flat, d_cdict, int(ctx->l_cdict.size() / 2),
                                        d_res, d_bajobs, st, ctx->opts.count_grid);
     launch_nest_count(d_chunks, d_pages, d_nest, n_nest, d_nseg, n_nseg, d_res, st);
     if (!(skip & 4u))
@@ -470,7 +472,7 @@ int upload_meta(pf_ctx* ctx) {
     int* lists = reinterpret_cast<int*>(h + ctx->off_lists);
     size_t lo = 0;
     for (auto* v : {&ctx->l_dictbin, &ctx->l_delta, &ctx->l_count, &ctx->l_scan, &ctx->l_flat, &ctx->l_decode, &ctx->l_runs,
-                    &ctx->l_dlen, &ctx->l_dba, &ctx->l_lvl, &ctx->l_djobs, &ctx->l_nest, &ctx->l_nseg}) {
+                    &ctx->l_dlen, &ctx->l_dba, &ctx->l_lvl, &ctx->l_djobs, &ctx->l_nest, &ctx->l_nseg, &ctx->l_cdict}) {
         std::copy(v->begin(), v->end(), lists + lo);
         lo += v->size();
     }
@@ -1058,7 +1060,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->chunks.assign(n_chunks, DevChunk{});
     ctx->pages.clear(); ctx->jobs.clear();
     ctx->l_dictbin.clear(); ctx->l_delta.clear(); ctx->l_count.clear(); ctx->l_scan.clear(); ctx->l_flat.clear(); ctx->l_decode.clear();
-    ctx->l_runs.clear(); ctx->l_dlen.clear(); ctx->l_dba.clear(); ctx->l_lvl.clear(); ctx->l_djobs.clear();
+    ctx->l_runs.clear(); ctx->l_dlen.clear(); ctx->l_dba.clear(); ctx->l_lvl.clear(); ctx->l_djobs.clear(); ctx->l_cdict.clear();
     ctx->null_dict_lds = 0;
     ctx->null_dcap = ctx->null_icap = 16;
     ctx->l_nest.clear(); ctx->l_nseg.clear();
@@ -1436,6 +1438,11 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
         const DevChunk& ck = ctx->chunks[pg.chunk];
         if (pg.encoding == PF_ENC_DELTA_BINARY_PACKED && pg.aux && ck.ptype != PF_BYTE_ARRAY) ctx->l_delta.push_back(int(i));
         if (ck.needs_count) (ck.ptype == PF_BYTE_ARRAY && ck.max_rep == 0 ? ctx->l_count : count_rest).push_back(int(i));
+        if (ck.ptype == PF_BYTE_ARRAY && ck.max_rep == 0 && pg.runtab != nullptr &&
+            (pg.encoding == PF_ENC_PLAIN_DICTIONARY || pg.encoding == PF_ENC_RLE_DICTIONARY)) {
+            const int nb = std::max(1, int((int64_t(pg.num_values) + FLAT_BLK - 1) / FLAT_BLK));
+            for (int b = 0; b < nb; b++) { ctx->l_cdict.push_back(int(i)); ctx->l_cdict.push_back(b); }
+        }
         if (ck.max_rep == 0) {   // (page, block) pairs
             // fixed-width pages without a level table (no nulls) take blocks of FLAT_BLK << fix_shift
             // entries (the block index carries the shift in bits 28..31): a block's metadata chain and
@@ -1523,7 +1530,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
     ctx->off_lists = take(m, sizeof(int) * (ctx->l_dictbin.size() + ctx->l_delta.size() + ctx->l_count.size() +
                                             ctx->l_scan.size() + ctx->l_flat.size() + ctx->l_decode.size() + ctx->l_runs.size() +
                                             ctx->l_dlen.size() + ctx->l_dba.size() + ctx->l_lvl.size() + ctx->l_djobs.size() +
-                                            ctx->l_nest.size() + ctx->l_nseg.size()));
+                                            ctx->l_nest.size() + ctx->l_nseg.size() + ctx->l_cdict.size()));
     ctx->off_res = take(m, sizeof(DevChunkResult) * n_chunks);
     ctx->off_pieces = take(m, sizeof(int2) * ctx->pieces.size());
     ctx->off_splits = take(m, sizeof(uint32_t) * ctx->n_splits);

@@ -375,7 +375,7 @@ def test_reader_multi_device_error_at_its_row_group(tmp_path):
 def test_dictionary_ids_out_of_range(decoder, oracle, tmp_path, kind):
     """Ids past the dictionary in a flat dictionary data page (0xff bytes written over an uncompressed v2
     page's bit-packed ids, 10-bit ids into 700 entries): the oracle reports the chunk; the GPU must too,
-    from whichever kernel sees it first (strings: k_runs marks its block and k_count reports the
+    from whichever kernel sees it first (strings: k_count_dict marks its block and k_count reports the
     page, round 5; fixed width: k_flat_fixed's id check), without a fault; a clean column of the same
     batch stays bit-exact."""
     import pyarrow as pa
