@@ -207,7 +207,10 @@ int pf_copy_columns_async(pf_ctx* ctx, int n, const int* chunks, const pf_column
  * levels, validity bits, chars) into a caller buffer of pf_batch_bytes bytes (pinned), instead of
  * up to 8 copies per chunk. After pf_sync, pf_column_info_host returns chunk i's pf_column_info
  * with its d_* pointers rebased into that host buffer (same layout rules as the device arrays).
- * Valid after pf_wait until the next decode on this context. */
+ * Valid after pf_wait until the next decode on this context. A mapped pinned buffer (pf_host_alloc,
+ * hipHostMalloc) is written by a download kernel on a copy stream the context shares with its twin
+ * (pf_ctx_create_shared), ordered after the decode, so the link carries uploads and downloads at
+ * once (round 6); any other buffer takes SDMA copies on the context stream. */
 int pf_batch_bytes(pf_ctx* ctx, size_t* bytes);
 int pf_copy_batch_async(pf_ctx* ctx, void* host, size_t cap);
 int pf_column_info_host(pf_ctx* ctx, int chunk, const void* host, pf_column_info* out);
