@@ -34,7 +34,9 @@ struct PfOpts {
     bool zc = true;           // PF_ZC=0: SDMA copies for the batch tables instead of k_copy_words
     bool dl_kernel = true;    // PF_DL_KERNEL=0: pf_copy_batch_async by SDMA copies instead of k_download
     bool h2d_kernel = false;  // PF_H2D_KERNEL=1: pinned chunk bytes to the device by a kernel instead of SDMA (E2E: no gain, r06)
+    int h2d_grid = 256;       // PF_H2D_GRID: that kernel's workgroups (fewer: a slower upload beside the downloads)
     bool dl_stream = true;    // PF_DL_STREAM=0: pf_copy_batch_async on the decode stream instead of the copy stream
+    bool dl_prio = false;     // PF_DL_PRIO=1: the copy stream at the device's highest stream priority
     bool debug_plan = false;  // PF_DEBUG_PLAN=1: host planning phase times on stderr
     int64_t nest_seg = 0;     // PF_NEST_SEG=n: nested segment length, forced (0: default, not forced)
     bool nest_seg_set = false;

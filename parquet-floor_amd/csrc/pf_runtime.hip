@@ -905,6 +905,8 @@ void opts_from_env(pf::PfOpts& o) {
     o.dl_kernel = on("PF_DL_KERNEL", o.dl_kernel);
     o.dl_stream = on("PF_DL_STREAM", o.dl_stream);
     o.h2d_kernel = on("PF_H2D_KERNEL", o.h2d_kernel);
+    o.h2d_grid = std::max(1, num("PF_H2D_GRID", o.h2d_grid));
+    o.dl_prio = on("PF_DL_PRIO", o.dl_prio);
     o.debug_plan = on("PF_DEBUG_PLAN", o.debug_plan);
     if (const char* e = std::getenv("PF_NEST_SEG")) {
         o.nest_seg = std::atoll(e);
@@ -1094,7 +1096,7 @@ int pf_decode_row_group(pf_ctx* ctx, const pf_chunk_desc* cds, int n_chunks, con
             (reinterpret_cast<uintptr_t>(hd) & 15u) == 0) {
             const DlRange r0{static_cast<uint8_t*>(ctx->d_in.p), static_cast<const uint8_t*>(hd), uint64_t(n_bytes)};
             const DlRange rz{nullptr, nullptr, 0};
-            hipLaunchKernelGGL(k_download, dim3(256), dim3(256), 0, st, r0, rz, rz);
+            hipLaunchKernelGGL(k_download, dim3(ctx->opts.h2d_grid), dim3(256), 0, st, r0, rz, rz);
             HIPCHK(ctx, hipGetLastError());
         } else {
             (void)hipGetLastError();
@@ -1756,7 +1758,13 @@ int pf_copy_batch_async(pf_ctx* ctx, void* host, size_t cap) {
     if (ctx->opts.dl_stream) {   // the download on the copy stream, after this context's decode
         {
             std::lock_guard<std::mutex> lk(ctx->streams->mu);
-            if (!ctx->streams->copy_stream) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->streams->copy_stream, hipStreamNonBlocking));
+            if (!ctx->streams->copy_stream) {
+                int least = 0, greatest = 0;
+                if (ctx->opts.dl_prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+                    HIPCHK(ctx, hipStreamCreateWithPriority(&ctx->streams->copy_stream, hipStreamNonBlocking, greatest));
+                else
+                    HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->streams->copy_stream, hipStreamNonBlocking));
+            }
         }
         cs = ctx->streams->copy_stream;
         HIPCHK(ctx, hipEventRecord(ctx->ev_dl, ctx->stream));
