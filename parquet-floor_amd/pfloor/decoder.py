@@ -233,14 +233,31 @@ class GpuDecoder:
         names = ["h2d", "snappy_parse", "snappy_exec", "dict", "delta", "levels", "count", "scan", "flat", "decode"]
         return dict(zip(names, list(buf)[:n.value]))
 
-    def fetch_batch(self, chunk_types):
+    def fetch_batch(self, chunk_types, pageable=False):
         """All chunks of the last decode with ONE D2H per output arena (pf_copy_batch_async), then
         per chunk the canonical arrays cut from the host copy (pf_column_info_host).
-        chunk_types: [(physical_type, max_def, max_rep)] per chunk."""
+        chunk_types: [(physical_type, max_def, max_rep)] per chunk. pageable: an ordinary host array
+        instead of a mapped pinned buffer (the library's SDMA copy path instead of its download kernel)."""
         L = lib()
         n = C.c_size_t()
         check(L.pf_batch_bytes(self.h, C.byref(n)), self.h, "pf_batch_bytes")
-        buf = PinnedBuffer(self.h, max(1, n.value))
+        if pageable:
+            class _Host:   # (same interface as PinnedBuffer for the code below)
+                def __init__(self, nbytes):
+                    self.arr = np.zeros(nbytes + 256, np.uint8)
+                    a = self.arr.ctypes.data
+                    self.off = (-a) % 256
+                    self.ptr = C.c_void_p(a + self.off)
+                    self.nbytes = nbytes
+
+                def array(self):
+                    return self.arr[self.off:self.off + self.nbytes]
+
+                def free(self):
+                    self.arr = None
+            buf = _Host(max(1, n.value))
+        else:
+            buf = PinnedBuffer(self.h, max(1, n.value))
         try:
             check(L.pf_copy_batch_async(self.h, buf.ptr, buf.nbytes), self.h, "pf_copy_batch_async")
             check(L.pf_sync(self.h), self.h, "pf_sync")

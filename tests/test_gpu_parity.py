@@ -257,10 +257,13 @@ def test_shared_stream_contexts_pipelined(oracle):
     b.close()
 
 
+@pytest.mark.parametrize("pageable", [False, True])
 @pytest.mark.parametrize("name", golden_files())
-def test_batch_copy_matches_per_chunk_copy(decoder, oracle, name):
+def test_batch_copy_matches_per_chunk_copy(decoder, oracle, name, pageable):
     """pf_copy_batch_async (one D2H per output arena) + pf_column_info_host give the same arrays
-    as pf_copy_column per chunk, and both match the oracle (E2E path of bench.py)."""
+    as pf_copy_column per chunk, and both match the oracle (E2E path of bench.py). A mapped pinned
+    buffer is written by the library's download kernel on its copy stream; an ordinary host array
+    takes the SDMA copies (round 6)."""
     from pfloor.decoder import ParquetFile
     path = os.path.join(GOLDEN, name + ".parquet")
     with ParquetFile(path) as pf, oracle.open(path) as of:
@@ -275,7 +278,7 @@ def test_batch_copy_matches_per_chunk_copy(decoder, oracle, name):
         rc = decoder.wait()
         types = [(pf.columns[col].physical_type, pf.columns[col].max_def, pf.columns[col].max_rep)
                  for _rg, col, *_r in items]
-        got = decoder.fetch_batch(types)
+        got = decoder.fetch_batch(types, pageable=pageable)
         for i, (rg, col, *_r) in enumerate(items):
             one = decoder.fetch(i, *types[i])
             assert got[i]["status"] == one["status"]
