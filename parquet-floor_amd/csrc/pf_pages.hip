@@ -407,10 +407,18 @@ __device__ __forceinline__ uint32_t ba_stage(uint8_t* stg, const uint8_t* p, uin
     const uint32_t woff = uint32_t(a & 15u);
     const uint4* src = reinterpret_cast<const uint4*>(a - woff);
     const int64_t first = int64_t(base) - int64_t(woff);
-    for (uint32_t c = threadIdx.x; c < BA_STAGE / 16; c += NT) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (first + int64_t(c) * 16 < int64_t(n)) v = src[c];
-        reinterpret_cast<uint4*>(stg)[c] = v;
+    constexpr uint32_t NCH = BA_STAGE / 16, BU = (NCH + NT - 1) / NT;   // (all loads in flight, round 6)
+    uint4 v[BU];
+    #pragma unroll
+    for (uint32_t u = 0; u < BU; u++) {
+        const uint32_t c = threadIdx.x + NT * u;
+        v[u] = make_uint4(0, 0, 0, 0);
+        if (c < NCH && first + int64_t(c) * 16 < int64_t(n)) v[u] = src[c];
+    }
+    #pragma unroll
+    for (uint32_t u = 0; u < BU; u++) {
+        const uint32_t c = threadIdx.x + NT * u;
+        if (c < NCH) reinterpret_cast<uint4*>(stg)[c] = v[u];
     }
     return woff;
 }
@@ -537,11 +545,19 @@ __global__ __launch_bounds__(NT) void k_ba_tile(BaJob* __restrict__ jobs, const 
         // holding byte 0 is read whole, as ba_stage does)
         const int64_t first = sb - int64_t(woff);
         const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(a0 - woff);
-        for (uint32_t c = threadIdx.x; c < (BA_FSTAGE + 16) / 16; c += NT) {
+        constexpr uint32_t NCH = (BA_FSTAGE + 16) / 16, BU = (NCH + NT - 1) / NT;   // (all loads in flight, round 6)
+        u32x4 v[BU];
+        #pragma unroll
+        for (uint32_t u = 0; u < BU; u++) {
+            const uint32_t c = threadIdx.x + NT * u;
             const int64_t q = first + int64_t(c) * 16;
-            u32x4 v = {0u, 0u, 0u, 0u};
-            if (q + 16 > 0 && q < int64_t(n)) v = src[c];
-            reinterpret_cast<u32x4*>(stg)[c] = v;
+            v[u] = u32x4{0u, 0u, 0u, 0u};
+            if (c < NCH && q + 16 > 0 && q < int64_t(n)) v[u] = src[c];
+        }
+        #pragma unroll
+        for (uint32_t u = 0; u < BU; u++) {
+            const uint32_t c = threadIdx.x + NT * u;
+            if (c < NCH) reinterpret_cast<u32x4*>(stg)[c] = v[u];
         }
     }
     for (uint32_t i = threadIdx.x; i < BA_NW; i += NT) { C[i] = 0; L1[i] = 0; L2[i] = 0; }

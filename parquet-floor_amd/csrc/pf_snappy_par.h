@@ -141,11 +141,23 @@ __device__ __forceinline__ uint32_t snap_stage(uint8_t* stage, const uint8_t* in
     const uint32_t woff = uint32_t(a & 15u);
     const PF_GLOBAL u32x4* src = (const PF_GLOBAL u32x4*)(a - woff);
     const int64_t first = int64_t(base) - int64_t(woff);
-    for (uint32_t c = uint32_t(lane); c < bytes / 16; c += 64) {
-        const int64_t p = first + int64_t(c) * 16;
-        u32x4 v = {0u, 0u, 0u, 0u};
-        if (p < int64_t(n)) v = src[c];
-        reinterpret_cast<u32x4*>(stage)[c] = v;
+    const uint32_t nch = bytes / 16;
+    // STAGE_U loads a lane in flight before their stores (round 6: one load -> store round trip per
+    // chunk serialised the 9 global latencies of an 8 KiB window)
+    constexpr uint32_t STAGE_U = 8;
+    for (uint32_t c0 = uint32_t(lane); c0 < nch; c0 += 64u * STAGE_U) {
+        u32x4 v[STAGE_U];
+        #pragma unroll
+        for (uint32_t u = 0; u < STAGE_U; u++) {
+            const uint32_t c = c0 + 64u * u;
+            v[u] = u32x4{0u, 0u, 0u, 0u};
+            if (c < nch && first + int64_t(c) * 16 < int64_t(n)) v[u] = src[c];
+        }
+        #pragma unroll
+        for (uint32_t u = 0; u < STAGE_U; u++) {
+            const uint32_t c = c0 + 64u * u;
+            if (c < nch) reinterpret_cast<u32x4*>(stage)[c] = v[u];
+        }
     }
     return woff;
 }

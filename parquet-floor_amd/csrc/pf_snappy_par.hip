@@ -98,13 +98,25 @@ constexpr uint32_t XS_SAT = 0x7fffu;       // saturated region exit (a literal l
 __device__ void stage_pad(uint8_t* sp, const uint8_t* in, uint64_t n, uint32_t W0, int lane) {
     const uintptr_t base = reinterpret_cast<uintptr_t>(in);
     const uintptr_t lastw = (base + n - 1) & ~uintptr_t(3);
-    for (uint32_t idx = uint32_t(lane); idx < SNAP_PSTAGE / 4; idx += 64) {
-        const uint32_t k = idx / (SNAP_PB / 4), jd = idx - k * (SNAP_PB / 4);
-        const uintptr_t a = base + W0 + k * SNAP_RB + jd * 4;
-        const uintptr_t a0 = a & ~uintptr_t(3);
-        const uint32_t lo = a0 <= lastw ? *(const PF_GLOBAL uint32_t*)a0 : 0u;
-        const uint32_t hi = a0 + 4 <= lastw ? *(const PF_GLOBAL uint32_t*)(a0 + 4) : 0u;
-        reinterpret_cast<uint32_t*>(sp)[idx] = __builtin_amdgcn_alignbyte(hi, lo, uint32_t(a & 3u));
+    constexpr uint32_t PU = 8;   // dwords a lane in flight before their stores (round 6: 35 serial round trips)
+    for (uint32_t i0 = uint32_t(lane); i0 < SNAP_PSTAGE / 4; i0 += 64u * PU) {
+        uint32_t lo[PU], hi[PU], sh[PU];
+        #pragma unroll
+        for (uint32_t u = 0; u < PU; u++) {
+            const uint32_t idx = i0 + 64u * u;
+            const uint32_t k = idx / (SNAP_PB / 4), jd = idx - k * (SNAP_PB / 4);
+            const uintptr_t a = base + W0 + k * SNAP_RB + jd * 4;
+            const uintptr_t a0 = a & ~uintptr_t(3);
+            const bool in_range = idx < SNAP_PSTAGE / 4;
+            lo[u] = in_range && a0 <= lastw ? *(const PF_GLOBAL uint32_t*)a0 : 0u;
+            hi[u] = in_range && a0 + 4 <= lastw ? *(const PF_GLOBAL uint32_t*)(a0 + 4) : 0u;
+            sh[u] = uint32_t(a & 3u);
+        }
+        #pragma unroll
+        for (uint32_t u = 0; u < PU; u++) {
+            const uint32_t idx = i0 + 64u * u;
+            if (idx < SNAP_PSTAGE / 4) reinterpret_cast<uint32_t*>(sp)[idx] = __builtin_amdgcn_alignbyte(hi[u], lo[u], sh[u]);
+        }
     }
 }
 
