@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 final measurements of this tree: part A = GPU suite, smoke, the default SF1 bench
 # line (CPU baselines, PMC traffic, E2E, write), the per-config lines; part B = SF1 kernel trace and
-# per-launch times, parse-pass phase stamps, SQ counters of every kernel.
+# per-launch times, parse-pass phase stamps (needs `make -C parquet-floor_amd stamps` first), SQ counters of every kernel.
 #   tools/gpu_r6_final.sh TAG A|B
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-/root/repo}"
